@@ -1,0 +1,120 @@
+/*
+ * lodestar_bls.h -- C-ABI of the MI355X BLS12-381 signature-set verifier.
+ *
+ * Drop-in boundary for Lodestar's BLS verification hot path.  The reference
+ * crosses JS -> native inside @chainsafe/blst (SWIG N-API, [ext]); the seam this
+ * library replaces is the worker RPC
+ *     WorkerApi.verifyManySignatureSets(BlsWorkReq[]) -> BlsWorkResult
+ * (packages/beacon-node/src/chain/bls/multithread/index.ts:59-61, worker.ts:26-108,
+ *  types.ts:8-38), which sits behind
+ *     IBlsVerifier.verifySignatureSets(sets, opts) (chain/bls/interface.ts:20-46).
+ * The N-API binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions: plain pointers and sizes; the caller owns every buffer for the
+ * duration of the call (the library copies into pinned staging); no call throws
+ * across the ABI -- functions return 0 on success and a negative value on a
+ * runtime failure (message via bls_gpu_last_error).  Per-request verdicts use
+ *     1 = valid, 0 = invalid, < 0 = -(BLST-style error code)
+ * with the codes below (values 1..7 follow blst's BLST_ERROR enum).
+ */
+#ifndef LODESTAR_BLS_H
+#define LODESTAR_BLS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  BLS_CODE_OK = 0,
+  BLS_CODE_BAD_ENCODING = 1,         /* "BLST_BAD_ENCODING" */
+  BLS_CODE_POINT_NOT_ON_CURVE = 2,   /* "BLST_POINT_NOT_ON_CURVE" */
+  BLS_CODE_POINT_NOT_IN_GROUP = 3,   /* "BLST_POINT_NOT_IN_GROUP" */
+  BLS_CODE_PK_IS_INFINITY = 6,       /* "BLST_PK_IS_INFINITY" */
+  BLS_CODE_INVALID_SIZE = 8,         /* "BLST_INVALID_SIZE" (multithread.test.ts:100) */
+  BLS_CODE_ZERO_SIGNATURE = 9,       /* infinity signature on the 1-set path */
+  BLS_CODE_EMPTY_SET = 10,           /* "Empty signature set" (maybeBatch.ts:29-31) */
+  BLS_CODE_EMPTY_AGGREGATE = 11      /* "EMPTY_AGGREGATE_ARRAY" (PublicKey.aggregate([])) */
+};
+
+/* One verifyManySignatureSets() call: n_reqs BlsWorkReq, n_sets SerializedSet in
+ * request order (types.ts:8-17).  Request r owns sets [req_set_offsets[r],
+ * req_set_offsets[r+1]).  Public keys come either raw (96-byte uncompressed
+ * affine, what index.ts:160 sends the worker) or as index lists into the
+ * context's device-resident pubkey table (bls_gpu_load_pubkeys); an index list
+ * of length k > 1 is an aggregate set, summed on the GPU (chain/bls/utils.ts:5-16). */
+typedef struct bls_batch {
+  uint32_t n_sets;
+  uint32_t n_reqs;
+  const uint32_t* req_set_offsets; /* n_reqs + 1 */
+  const uint8_t* req_batchable;    /* n_reqs, 0/1 (VerifySignatureOpts.batchable) */
+  const uint8_t* pubkeys;          /* n_sets * 96; used when set_pk_offsets == NULL */
+  const uint32_t* set_pk_offsets;  /* n_sets + 1 into pk_indices, or NULL */
+  const uint32_t* pk_indices;      /* device pubkey-table indices */
+  const uint8_t* messages;         /* n_sets * 32 (signing roots) */
+  const uint8_t* signatures;       /* n_sets * 96 (compressed G2; bytes past signature_lens[i] ignored) */
+  const uint32_t* signature_lens;  /* n_sets, or NULL = all 96 */
+  const uint8_t* seed;             /* 32 bytes for the random scalars, or NULL = fresh OS randomness */
+} bls_batch;
+
+/* BlsWorkResult bookkeeping (types.ts:26-38) */
+typedef struct bls_stats {
+  uint32_t batch_retries;      /* batchable chunks that failed and were re-verified per request */
+  uint32_t batch_sigs_success; /* sets accepted by a successful batch */
+  uint32_t n_chunks;           /* batchable chunks (chunkifyMaximizeChunkSize(reqs, 16)) */
+  uint32_t n_individual;       /* requests verified on their own */
+  double device_ms;            /* device time of the call (HIP events) */
+} bls_stats;
+
+typedef struct bls_gpu_ctx bls_gpu_ctx;
+
+/* Number of visible HIP devices (0 when there is no GPU). */
+int bls_gpu_device_count(void);
+
+/* Create a verifier bound to one device (one process per GPU; the device index is
+ * local to the process).  Replaces BlsMultiThreadWorkerPool's worker creation
+ * (multithread/index.ts:199-233). */
+int bls_gpu_init(int device, bls_gpu_ctx** out);
+
+/* Release device memory and streams (IBlsVerifier.close, index.ts:176-197). */
+void bls_gpu_close(bls_gpu_ctx* ctx);
+
+const char* bls_gpu_last_error(const bls_gpu_ctx* ctx);
+
+/* Load / append trusted validator pubkeys into the device table (Index2PubkeyCache,
+ * state-transition/src/cache/pubkeyCache.ts:56-77).  pk_len is 48 (compressed) or 96
+ * (uncompressed).  codes (nullable, n entries) receive a per-key decode code; keys
+ * are not subgroup-checked (trusted, pubkeyCache.ts:72-75).  Returns the new table
+ * size (>= 0) or < 0 on failure. */
+int64_t bls_gpu_load_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes);
+
+/* verifyManySignatureSets (worker.ts:32-108) on the GPU: per-request verdicts with
+ * the reference's batch / fallback semantics:
+ *   - batchable requests are grouped by chunkifyMaximizeChunkSize(reqs, 16) and each
+ *     chunk is checked by one random-scalar batch (maybeBatch.ts:18-25);
+ *   - a failing or erroring chunk is re-verified request by request;
+ *   - non-batchable requests are verified on their own (maybeBatch.ts:16-39).
+ * verdicts: n_reqs int32 (see top of file).  stats nullable. */
+int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* batch, int32_t* verdicts, bls_stats* stats);
+
+/* getAggregatedPubkey (chain/bls/utils.ts:5-16) for n_sets index lists over the device
+ * table; out: n_sets * 96 bytes uncompressed (PointFormat.uncompressed, index.ts:126,160);
+ * codes: n_sets (0 ok, BLS_CODE_EMPTY_AGGREGATE for an empty list). */
+int bls_gpu_aggregate_pubkeys(bls_gpu_ctx* ctx, const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
+                              uint32_t n_sets, uint8_t* out96, int32_t* codes);
+
+/* hash_to_G2 with the POP DST for n 32-byte messages; out: n * 192 bytes (uncompressed
+ * ZCash order x.c1 || x.c0 || y.c1 || y.c0). */
+int bls_gpu_hash_to_g2(bls_gpu_ctx* ctx, const uint8_t* msgs, uint32_t n, uint8_t* out192);
+
+/* Fixture helpers (signing is out of the verify path; used to synthesise inputs).
+ * sks: n * 32 bytes big-endian scalars. */
+int bls_gpu_sk_to_pk(bls_gpu_ctx* ctx, const uint8_t* sks, uint32_t n, uint8_t* out48);
+int bls_gpu_sign(bls_gpu_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LODESTAR_BLS_H */

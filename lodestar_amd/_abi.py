@@ -1,0 +1,117 @@
+"""ctypes view of the C-ABI in include/lodestar_bls.h.
+
+The product path loads lodestar_amd/_native/liblodestar_bls.so (built in-tree by
+lodestar_amd/build.py) and fails loudly if it is missing: there is no CPU
+fallback anywhere in the package.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "_native" / "liblodestar_bls.so"
+
+# verdict / error codes (include/lodestar_bls.h)
+CODE_OK = 0
+CODE_BAD_ENCODING = 1
+CODE_POINT_NOT_ON_CURVE = 2
+CODE_POINT_NOT_IN_GROUP = 3
+CODE_PK_IS_INFINITY = 6
+CODE_INVALID_SIZE = 8
+CODE_ZERO_SIGNATURE = 9
+CODE_EMPTY_SET = 10
+CODE_EMPTY_AGGREGATE = 11
+
+# Error messages carry the BLST_* code the reference surfaces through @chainsafe/blst
+# (only "BLST_INVALID_SIZE" is pinned by the reference's own tests, multithread.test.ts:100).
+ERROR_MESSAGES = {
+    CODE_BAD_ENCODING: "BLST_ERROR: BLST_BAD_ENCODING",
+    CODE_POINT_NOT_ON_CURVE: "BLST_ERROR: BLST_POINT_NOT_ON_CURVE",
+    CODE_POINT_NOT_IN_GROUP: "BLST_ERROR: BLST_POINT_NOT_IN_GROUP",
+    CODE_PK_IS_INFINITY: "BLST_ERROR: BLST_PK_IS_INFINITY",
+    CODE_INVALID_SIZE: "BLST_ERROR: BLST_INVALID_SIZE",
+    CODE_ZERO_SIGNATURE: "ZERO_SIGNATURE",
+    CODE_EMPTY_SET: "Empty signature set",
+    CODE_EMPTY_AGGREGATE: "EMPTY_AGGREGATE_ARRAY",
+}
+
+SYMBOLS = (
+    "bls_gpu_device_count",
+    "bls_gpu_init",
+    "bls_gpu_close",
+    "bls_gpu_last_error",
+    "bls_gpu_load_pubkeys",
+    "bls_gpu_verify",
+    "bls_gpu_aggregate_pubkeys",
+    "bls_gpu_hash_to_g2",
+    "bls_gpu_sk_to_pk",
+    "bls_gpu_sign",
+)
+
+
+class BlsBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_sets", ctypes.c_uint32),
+        ("n_reqs", ctypes.c_uint32),
+        ("req_set_offsets", ctypes.c_void_p),
+        ("req_batchable", ctypes.c_void_p),
+        ("pubkeys", ctypes.c_void_p),
+        ("set_pk_offsets", ctypes.c_void_p),
+        ("pk_indices", ctypes.c_void_p),
+        ("messages", ctypes.c_void_p),
+        ("signatures", ctypes.c_void_p),
+        ("signature_lens", ctypes.c_void_p),
+        ("seed", ctypes.c_void_p),
+    ]
+
+
+class BlsStats(ctypes.Structure):
+    _fields_ = [
+        ("batch_retries", ctypes.c_uint32),
+        ("batch_sigs_success", ctypes.c_uint32),
+        ("n_chunks", ctypes.c_uint32),
+        ("n_individual", ctypes.c_uint32),
+        ("device_ms", ctypes.c_double),
+    ]
+
+
+def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
+    """Attach argtypes/restype to the entry points (also used for the CPU test harness)."""
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    if hasattr(lib, "bls_gpu_init"):
+        lib.bls_gpu_device_count.restype = i32
+        lib.bls_gpu_init.argtypes = [i32, ctypes.POINTER(vp)]
+        lib.bls_gpu_init.restype = i32
+        lib.bls_gpu_close.argtypes = [vp]
+        lib.bls_gpu_close.restype = None
+        lib.bls_gpu_last_error.argtypes = [vp]
+        lib.bls_gpu_last_error.restype = ctypes.c_char_p
+        lib.bls_gpu_load_pubkeys.argtypes = [vp, vp, u32, u32, vp]
+        lib.bls_gpu_load_pubkeys.restype = ctypes.c_int64
+        lib.bls_gpu_verify.argtypes = [vp, ctypes.POINTER(BlsBatch), vp, ctypes.POINTER(BlsStats)]
+        lib.bls_gpu_verify.restype = i32
+        lib.bls_gpu_aggregate_pubkeys.argtypes = [vp, vp, vp, u32, vp, vp]
+        lib.bls_gpu_aggregate_pubkeys.restype = i32
+        lib.bls_gpu_hash_to_g2.argtypes = [vp, vp, u32, vp]
+        lib.bls_gpu_hash_to_g2.restype = i32
+        lib.bls_gpu_sk_to_pk.argtypes = [vp, vp, u32, vp]
+        lib.bls_gpu_sk_to_pk.restype = i32
+        lib.bls_gpu_sign.argtypes = [vp, vp, vp, u32, vp]
+        lib.bls_gpu_sign.restype = i32
+    return lib
+
+
+_LIB: ctypes.CDLL | None = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load the in-tree HIP library; raises (never falls back) when it is absent."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -m lodestar_amd.build` "
+                "(or __graft_entry__.build()); there is no CPU fallback"
+            )
+        _LIB = bind(ctypes.CDLL(str(LIB_PATH)))
+    return _LIB

@@ -1,0 +1,94 @@
+"""In-tree build of the gfx950 HIP library (lodestar_amd/_native/liblodestar_bls.so).
+
+Each kernel lives in its own translation unit (lodestar_amd/csrc/kernels/*.hip) so
+the TUs compile in parallel; objects are cached by a hash of the sources, flags
+and headers so an unchanged tree relinks in seconds.  Used by
+__graft_entry__.build() and runnable directly:  python -m lodestar_amd.build
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "lodestar_amd"
+CSRC = PKG / "csrc"
+OUT_DIR = PKG / "_native"
+OBJ_DIR = ROOT / "build" / "obj"
+LIB = OUT_DIR / "liblodestar_bls.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(ROOT / "include"), "-I", str(CSRC)]
+
+
+def _headers_digest() -> str:
+    h = hashlib.sha256()
+    for p in sorted(list(CSRC.rglob("*.hpp")) + list((ROOT / "include").glob("*.h"))):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def sources() -> list[Path]:
+    return [CSRC / "bls_gpu.hip"] + sorted((CSRC / "kernels").glob("*.hip"))
+
+
+def _compile(src: Path, hdr: str, verbose: bool) -> Path:
+    key = hashlib.sha256((hdr + " ".join(FLAGS)).encode() + src.read_bytes()).hexdigest()[:16]
+    obj = OBJ_DIR / f"{src.stem}.{key}.o"
+    if obj.exists():
+        return obj
+    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj) + ".tmp"]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(str(obj) + ".tmp", obj)
+    return obj
+
+
+def build(jobs: int | None = None, verbose: bool = True) -> Path:
+    OUT_DIR.mkdir(parents=True, exist_ok=True)
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    hdr = _headers_digest()
+    srcs = sources()
+    jobs = jobs or min(len(srcs), os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
+    stamp = hashlib.sha256("".join(str(o) for o in objs).encode()).hexdigest()
+    stamp_file = OUT_DIR / ".lib_stamp"
+    if LIB.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB) + ".tmp", *map(str, objs)]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(str(LIB) + ".tmp", LIB)
+    stamp_file.write_text(stamp)
+    return LIB
+
+
+def build_hostsim(verbose: bool = True) -> Path:
+    """CPU build of the kernels' math for tests/ (test infrastructure, not the product)."""
+    src = ROOT / "tests" / "native" / "hostsim.cpp"
+    out = ROOT / "tests" / "native" / "libhostsim.so"
+    hdr = _headers_digest()
+    key = hashlib.sha256(hdr.encode() + src.read_bytes()).hexdigest()[:16]
+    stamp = out.with_suffix(".stamp")
+    if out.exists() and stamp.exists() and stamp.read_text() == key:
+        return out
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-DBLS_COUNT_OPS", "-I", str(CSRC), "-I",
+           str(ROOT / "include"), "-o", str(out), str(src)]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    stamp.write_text(key)
+    return out
+
+
+if __name__ == "__main__":
+    build(jobs=int(sys.argv[1]) if len(sys.argv) > 1 else None)
+    build_hostsim()

@@ -1,0 +1,437 @@
+// BLS12-381 groups G1 (E1/Fp: y^2 = x^3 + 4) and G2 (E2/Fp2: y^2 = x^3 + 4(1+u)).
+//
+// Jacobian coordinates (x = X/Z^2, y = Y/Z^3; Z = 0 is the point at infinity),
+// one point per lane.  The formulas are field-generic (template over Fp / Fp2):
+//   dbl-2009-l (2M + 5S), add-2007-bl (11M + 5S), madd-2007-bl (7M + 4S),
+// with the exceptional cases (P == Q, P == -Q, infinity) handled explicitly so
+// the same code is correct for adversarial signature points that are on the
+// curve but outside G2 (subgroup check input).
+//
+// Replaces blst's p1/p2 arithmetic behind @chainsafe/blst (SURVEY.md 2.2 items
+// 2, 3, 5): PublicKey.aggregate (beacon-node/src/chain/bls/utils.ts:11),
+// Signature.fromBytes(.., validate=true) (chain/bls/maybeBatch.ts:23,36).
+#pragma once
+
+#include "field.hpp"
+
+namespace bls {
+
+// ---- field-generic shims (overloads) ---------------------------------------
+BLS_HD Fp f_add(const Fp& a, const Fp& b) { return fp_add(a, b); }
+BLS_HD Fp f_sub(const Fp& a, const Fp& b) { return fp_sub(a, b); }
+BLS_HD Fp f_mul(const Fp& a, const Fp& b) { return fp_mul(a, b); }
+BLS_HD Fp f_sqr(const Fp& a) { return fp_sqr(a); }
+BLS_HD Fp f_dbl(const Fp& a) { return fp_dbl(a); }
+BLS_HD Fp f_neg(const Fp& a) { return fp_neg(a); }
+BLS_HD bool f_is_zero(const Fp& a) { return fp_is_zero(a); }
+BLS_HD bool f_eq(const Fp& a, const Fp& b) { return fp_eq(a, b); }
+BLS_HD Fp f_inv(const Fp& a) { return fp_inv(a); }
+BLS_HD void f_set_zero(Fp& a) { a = fp_zero(); }
+BLS_HD void f_set_one(Fp& a) { a = c_one(); }
+
+BLS_HD Fp2 f_add(const Fp2& a, const Fp2& b) { return fp2_add(a, b); }
+BLS_HD Fp2 f_sub(const Fp2& a, const Fp2& b) { return fp2_sub(a, b); }
+BLS_HD Fp2 f_mul(const Fp2& a, const Fp2& b) { return fp2_mul(a, b); }
+BLS_HD Fp2 f_sqr(const Fp2& a) { return fp2_sqr(a); }
+BLS_HD Fp2 f_dbl(const Fp2& a) { return fp2_dbl(a); }
+BLS_HD Fp2 f_neg(const Fp2& a) { return fp2_neg(a); }
+BLS_HD bool f_is_zero(const Fp2& a) { return fp2_is_zero(a); }
+BLS_HD bool f_eq(const Fp2& a, const Fp2& b) { return fp2_eq(a, b); }
+BLS_HD Fp2 f_inv(const Fp2& a) { return fp2_inv(a); }
+BLS_HD void f_set_zero(Fp2& a) { a = fp2_zero(); }
+BLS_HD void f_set_one(Fp2& a) { a = fp2_one(); }
+
+template <class F>
+struct Jac {
+  F x, y, z;
+};
+template <class F>
+struct Aff {
+  F x, y;
+  bool inf;
+};
+
+typedef Jac<Fp> G1J;
+typedef Aff<Fp> G1A;
+typedef Jac<Fp2> G2J;
+typedef Aff<Fp2> G2A;
+
+template <class F>
+BLS_HD Jac<F> jac_infinity() {
+  Jac<F> r;
+  f_set_one(r.x);
+  f_set_one(r.y);
+  f_set_zero(r.z);
+  return r;
+}
+
+template <class F>
+BLS_HD bool jac_is_inf(const Jac<F>& p) {
+  return f_is_zero(p.z);
+}
+
+template <class F>
+BLS_HD Jac<F> jac_from_aff(const Aff<F>& a) {
+  if (a.inf) return jac_infinity<F>();
+  Jac<F> r;
+  r.x = a.x;
+  r.y = a.y;
+  f_set_one(r.z);
+  return r;
+}
+
+template <class F>
+BLS_HD Jac<F> jac_neg(const Jac<F>& p) {
+  Jac<F> r = p;
+  r.y = f_neg(p.y);
+  return r;
+}
+
+// dbl-2009-l (a = 0)
+template <class F>
+BLS_HD Jac<F> jac_dbl(const Jac<F>& p) {
+  F A = f_sqr(p.x);
+  F B = f_sqr(p.y);
+  F C = f_sqr(B);
+  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
+  F E = f_add(f_dbl(A), A);
+  F Fv = f_sqr(E);
+  Jac<F> r;
+  r.x = f_sub(Fv, f_dbl(D));
+  F C8 = f_dbl(f_dbl(f_dbl(C)));
+  r.y = f_sub(f_mul(E, f_sub(D, r.x)), C8);
+  r.z = f_dbl(f_mul(p.y, p.z));
+  return r;
+}
+
+// add-2007-bl with exceptional cases
+template <class F>
+BLS_HD Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+  if (jac_is_inf(p)) return q;
+  if (jac_is_inf(q)) return p;
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  F U1 = f_mul(p.x, Z2Z2);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
+  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  F H = f_sub(U2, U1);
+  F rr = f_sub(S2, S1);
+  if (f_is_zero(H)) {
+    if (f_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  rr = f_dbl(rr);
+  F I = f_sqr(f_dbl(H));
+  F J = f_mul(H, I);
+  F V = f_mul(U1, I);
+  Jac<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(S1, J)));
+  r.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return r;
+}
+
+// madd-2007-bl: p Jacobian + q affine (q not infinity)
+template <class F>
+BLS_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
+  if (q.inf) return p;
+  if (jac_is_inf(p)) return jac_from_aff(q);
+  F Z1Z1 = f_sqr(p.z);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  F H = f_sub(U2, p.x);
+  F rr = f_sub(S2, p.y);
+  if (f_is_zero(H)) {
+    if (f_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  F HH = f_sqr(H);
+  F I = f_dbl(f_dbl(HH));
+  F J = f_mul(H, I);
+  rr = f_dbl(rr);
+  F V = f_mul(p.x, I);
+  Jac<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
+  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
+  return r;
+}
+
+template <class F>
+BLS_HD Aff<F> jac_to_aff(const Jac<F>& p) {
+  Aff<F> r;
+  if (jac_is_inf(p)) {
+    f_set_zero(r.x);
+    f_set_zero(r.y);
+    r.inf = true;
+    return r;
+  }
+  F zi = f_inv(p.z);
+  F zi2 = f_sqr(zi);
+  r.x = f_mul(p.x, zi2);
+  r.y = f_mul(p.y, f_mul(zi2, zi));
+  r.inf = false;
+  return r;
+}
+
+// Jacobian equality (both may be infinity)
+template <class F>
+BLS_HD bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
+  bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  if (!f_eq(f_mul(p.x, Z2Z2), f_mul(q.x, Z1Z1))) return false;
+  return f_eq(f_mul(f_mul(p.y, q.z), Z2Z2), f_mul(f_mul(q.y, p.z), Z1Z1));
+}
+
+// [k]P for a 64-bit scalar k (left-to-right double-and-add, generic add: safe for
+// points of any order).
+template <class F>
+BLS_HD Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
+  Jac<F> acc = jac_infinity<F>();
+  if (k == 0) return acc;
+  int top = 63;
+  while (!((k >> top) & 1ull)) --top;
+  acc = p;
+  for (int i = top - 1; i >= 0; --i) {
+    acc = jac_dbl(acc);
+    if ((k >> i) & 1ull) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+
+// [k]P for an affine base (mixed additions)
+template <class F>
+BLS_HD Jac<F> aff_mul_u64(const Aff<F>& p, uint64_t k) {
+  Jac<F> acc = jac_infinity<F>();
+  if (k == 0 || p.inf) return acc;
+  int top = 63;
+  while (!((k >> top) & 1ull)) --top;
+  acc = jac_from_aff(p);
+  for (int i = top - 1; i >= 0; --i) {
+    acc = jac_dbl(acc);
+    if ((k >> i) & 1ull) acc = jac_add_aff(acc, p);
+  }
+  return acc;
+}
+
+// [k]P for a scalar given as 8 little-endian 32-bit words (secret keys, up to 256 bits)
+template <class F>
+BLS_HD Jac<F> aff_mul_u256(const Aff<F>& p, const uint32_t k[8]) {
+  Jac<F> acc = jac_infinity<F>();
+  if (p.inf) return acc;
+  for (int i = 255; i >= 0; --i) {
+    acc = jac_dbl(acc);
+    if ((k[i >> 5] >> (i & 31)) & 1u) acc = jac_add_aff(acc, p);
+  }
+  return acc;
+}
+
+// [|x|]P, |x| = 0xd201000000010000 (the BLS parameter is x = -|x|)
+template <class F>
+BLS_HD Jac<F> jac_mul_xabs(const Jac<F>& p) {
+  return jac_mul_u64(p, (uint64_t)BLS_X_ABS);
+}
+
+// ---- G1 --------------------------------------------------------------------
+BLS_HD bool g1_on_curve(const G1A& a) {
+  if (a.inf) return true;
+  Fp rhs = fp_add(fp_mul(fp_sqr(a.x), a.x), c_b1());
+  return fp_eq(fp_sqr(a.y), rhs);
+}
+
+BLS_HD G1A g1_generator() {
+  G1A g;
+  g.x = c_g1_x();
+  g.y = c_g1_y();
+  g.inf = false;
+  return g;
+}
+
+// ---- G2 --------------------------------------------------------------------
+BLS_HD bool g2_on_curve(const G2A& a) {
+  if (a.inf) return true;
+  Fp2 rhs = fp2_add(fp2_mul(fp2_sqr(a.x), a.x), c_b2());
+  return fp2_eq(fp2_sqr(a.y), rhs);
+}
+
+BLS_HD G2A g2_generator() {
+  G2A g;
+  g.x = c_g2_x();
+  g.y = c_g2_y();
+  g.inf = false;
+  return g;
+}
+
+// psi(x, y) = (conj(x) * c_x, conj(y) * c_y) (RFC 9380 Appendix G.3), Jacobian form
+BLS_HD G2J g2_psi(const G2J& p) {
+  G2J r;
+  r.x = fp2_mul(fp2_conj(p.x), c_psi_x());
+  r.y = fp2_mul(fp2_conj(p.y), c_psi_y());
+  r.z = fp2_conj(p.z);
+  return r;
+}
+
+// G2 membership: psi(P) == [x]P  (x = -|x|), Scott's test; equals r*P == O on E2.
+BLS_HD bool g2_in_subgroup(const G2A& a) {
+  if (a.inf) return true;
+  G2J p = jac_from_aff(a);
+  G2J xp = jac_neg(jac_mul_xabs(p));
+  return jac_eq(g2_psi(p), xp);
+}
+
+// Budroni-Pintore cofactor clearing = [h_eff]P (RFC 9380 Appendix G.3)
+BLS_HD G2J g2_clear_cofactor(const G2J& p) {
+  G2J t1 = jac_neg(jac_mul_xabs(p));  // [x]P
+  G2J t2 = g2_psi(p);
+  G2J t3 = g2_psi(g2_psi(jac_dbl(p)));
+  t3 = jac_add(t3, jac_neg(t2));
+  t2 = jac_add(t1, t2);
+  t2 = jac_neg(jac_mul_xabs(t2));     // [x](t1 + t2)
+  t3 = jac_add(t3, t2);
+  t3 = jac_add(t3, jac_neg(t1));
+  return jac_add(t3, jac_neg(p));
+}
+
+// ---- serialization (ZCash format) ---------------------------------------------
+// Error codes follow blst's BLST_ERROR enum; values >= 8 are Lodestar/chainsafe-level.
+enum BlsCode : int32_t {
+  BLS_OK = 0,
+  BLS_BAD_ENCODING = 1,
+  BLS_POINT_NOT_ON_CURVE = 2,
+  BLS_POINT_NOT_IN_GROUP = 3,
+  BLS_PK_IS_INFINITY = 6,
+  BLS_INVALID_SIZE = 8,
+  BLS_ZERO_SIGNATURE = 9,
+  BLS_EMPTY_SET = 10,
+  BLS_EMPTY_AGGREGATE = 11,
+};
+
+// 96-byte uncompressed G1 (x || y big-endian), blst_p1_deserialize semantics
+// (on-curve check, no subgroup check: pubkeys are trusted, pubkeyCache.ts:72-75).
+BLS_HD int32_t g1_deserialize96(const uint8_t* b, G1A& out) {
+  out.inf = false;
+  if (b[0] & 0x80) return BLS_BAD_ENCODING;
+  if (b[0] & 0x40) {
+    uint8_t acc = b[0] & 0x3f;
+    for (int i = 1; i < 96; ++i) acc |= b[i];
+    if (acc) return BLS_BAD_ENCODING;
+    out.inf = true;
+    out.x = fp_zero();
+    out.y = fp_zero();
+    return BLS_OK;
+  }
+  if (b[0] & 0x20) return BLS_BAD_ENCODING;
+  Fp x = fp_from_be48(b);
+  Fp y = fp_from_be48(b + 48);
+  if (!fp_plain_is_canonical(x) || !fp_plain_is_canonical(y)) return BLS_BAD_ENCODING;
+  out.x = fp_to_mont(x);
+  out.y = fp_to_mont(y);
+  if (!g1_on_curve(out)) return BLS_POINT_NOT_ON_CURVE;
+  return BLS_OK;
+}
+
+// 48-byte compressed G1 (pubkey cache load), blst_p1_uncompress semantics.
+BLS_HD int32_t g1_decompress48(const uint8_t* b, G1A& out) {
+  out.inf = false;
+  if (!(b[0] & 0x80)) return BLS_BAD_ENCODING;
+  if (b[0] & 0x40) {
+    uint8_t acc = b[0] & 0x3f;
+    for (int i = 1; i < 48; ++i) acc |= b[i];
+    if (acc) return BLS_BAD_ENCODING;
+    out.inf = true;
+    out.x = fp_zero();
+    out.y = fp_zero();
+    return BLS_OK;
+  }
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; ++i) tmp[i] = b[i];
+  tmp[0] &= 0x1f;
+  Fp x = fp_from_be48(tmp);
+  if (!fp_plain_is_canonical(x)) return BLS_BAD_ENCODING;
+  out.x = fp_to_mont(x);
+  Fp y;
+  if (!fp_sqrt(fp_add(fp_mul(fp_sqr(out.x), out.x), c_b1()), y)) return BLS_POINT_NOT_ON_CURVE;
+  bool s = (b[0] & 0x20) != 0;
+  if (fp_lex_largest(y) != s) y = fp_neg(y);
+  out.y = y;
+  return BLS_OK;
+}
+
+BLS_HD void g1_serialize96(const G1A& a, uint8_t* b) {
+  if (a.inf) {
+    b[0] = 0x40;
+    for (int i = 1; i < 96; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(fp_from_mont(a.x), b);
+  fp_to_be48(fp_from_mont(a.y), b + 48);
+}
+
+BLS_HD void g1_compress48(const G1A& a, uint8_t* b) {
+  if (a.inf) {
+    b[0] = 0xc0;
+    for (int i = 1; i < 48; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(fp_from_mont(a.x), b);
+  b[0] |= 0x80;
+  if (fp_lex_largest(a.y)) b[0] |= 0x20;
+}
+
+// 96-byte compressed G2 signature, blst_p2_uncompress semantics (no subgroup check)
+BLS_HD int32_t g2_decompress96(const uint8_t* b, G2A& out) {
+  out.inf = false;
+  if (!(b[0] & 0x80)) return BLS_BAD_ENCODING;
+  if (b[0] & 0x40) {
+    uint8_t acc = b[0] & 0x3f;
+    for (int i = 1; i < 96; ++i) acc |= b[i];
+    if (acc) return BLS_BAD_ENCODING;
+    out.inf = true;
+    out.x = fp2_zero();
+    out.y = fp2_zero();
+    return BLS_OK;
+  }
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; ++i) tmp[i] = b[i];
+  tmp[0] &= 0x1f;
+  Fp x1 = fp_from_be48(tmp);
+  Fp x0 = fp_from_be48(b + 48);
+  if (!fp_plain_is_canonical(x1) || !fp_plain_is_canonical(x0)) return BLS_BAD_ENCODING;
+  out.x = Fp2{fp_to_mont(x0), fp_to_mont(x1)};
+  Fp2 y;
+  if (!fp2_sqrt(fp2_add(fp2_mul(fp2_sqr(out.x), out.x), c_b2()), y)) return BLS_POINT_NOT_ON_CURVE;
+  bool s = (b[0] & 0x20) != 0;
+  if (fp2_lex_largest(y) != s) y = fp2_neg(y);
+  out.y = y;
+  return BLS_OK;
+}
+
+// 192-byte uncompressed G2: x.c1 || x.c0 || y.c1 || y.c0
+BLS_HD void g2_serialize192(const G2A& a, uint8_t* b) {
+  if (a.inf) {
+    b[0] = 0x40;
+    for (int i = 1; i < 192; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(fp_from_mont(a.x.c1), b);
+  fp_to_be48(fp_from_mont(a.x.c0), b + 48);
+  fp_to_be48(fp_from_mont(a.y.c1), b + 96);
+  fp_to_be48(fp_from_mont(a.y.c0), b + 144);
+}
+
+BLS_HD void g2_compress96(const G2A& a, uint8_t* b) {
+  if (a.inf) {
+    b[0] = 0xc0;
+    for (int i = 1; i < 96; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(fp_from_mont(a.x.c1), b);
+  fp_to_be48(fp_from_mont(a.x.c0), b + 48);
+  b[0] |= 0x80;
+  if (fp2_lex_largest(a.y)) b[0] |= 0x20;
+}
+
+}  // namespace bls

@@ -1,0 +1,524 @@
+// BLS12-381 base-field tower for CDNA4 (gfx950): Fp, Fp2, Fp6, Fp12.
+//
+// Replaces the field arithmetic that the reference reaches through its
+// un-vendored npm dependency @chainsafe/blst@0.2.4 -> supranational blst
+// (yarn.lock:445-451); see SURVEY.md 2.2 items 1 and 6-7.
+//
+// Representation: Fp = 12 x 32-bit little-endian limbs in Montgomery form
+// (R = 2^384).  One 381-bit element lives in 12 VGPRs of one lane; the VALU
+// does the 32x32+64 multiply-adds (v_mad_u64_u32) of the CIOS product.  The
+// modulus has 3 spare bits, so the "no-carry" CIOS variant applies (top limb of
+// p < 2^31 - 1): the running 12-limb accumulator never needs a 13th word.
+//
+// Tower (same basis as the test oracle, oracle/bls_oracle.py):
+//   Fp2  = Fp[u]  / (u^2 + 1)
+//   Fp6  = Fp2[v] / (v^3 - xi),  xi = 1 + u
+//   Fp12 = Fp6[w] / (w^2 - v)
+// The Fp12 coefficient of w^k is (c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2)[k].
+//
+// Every function is __host__ __device__ so the same source is compiled for the
+// GPU (the product) and for the CPU test harness tests/native/hostsim.cpp.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BLS_HD __host__ __device__ __forceinline__
+#define BLS_NOINLINE static __host__ __device__ __attribute__((noinline))
+#else
+#define BLS_HD static inline
+#define BLS_NOINLINE static __attribute__((noinline))
+#endif
+
+#if defined(BLS_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+// Host-only operation counter (tests/native/hostsim.cpp): pins the algorithmic
+// work model (Fp multiplications per stage) used for the roofline figure.
+extern unsigned long long bls_fpm_counter;
+#define BLS_COUNT_FPM() (++bls_fpm_counter)
+#else
+#define BLS_COUNT_FPM() ((void)0)
+#endif
+
+namespace bls {
+
+struct Fp {
+  uint32_t l[12];
+};
+struct Fp2 {
+  Fp c0, c1;
+};
+struct Fp6 {
+  Fp2 c0, c1, c2;
+};
+struct Fp12 {
+  Fp6 c0, c1;
+};
+
+}  // namespace bls
+
+#include "constants.hpp"
+
+namespace bls {
+
+BLS_HD uint32_t p_limb(int i) {
+  const uint32_t t[12] = {BLS_P_LIMBS};
+  return t[i];
+}
+
+// ---------------------------------------------------------------------------
+// Fp
+// ---------------------------------------------------------------------------
+BLS_HD Fp fp_zero() {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = 0;
+  return r;
+}
+
+BLS_HD bool fp_is_zero(const Fp& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.l[i];
+  return acc == 0;
+}
+
+BLS_HD bool fp_eq(const Fp& a, const Fp& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.l[i] ^ b.l[i];
+  return acc == 0;
+}
+
+BLS_HD Fp fp_select(bool c, const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+
+// a - p with borrow; returns borrow (1 if a < p)
+BLS_HD uint32_t fp_sub_p(const Fp& a, Fp& d) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.l[i] - p_limb(i) - borrow;
+    d.l[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  return borrow;
+}
+
+// Reduce a value < 2p to [0, p).
+BLS_HD Fp fp_reduce_once(const Fp& s) {
+  Fp d;
+  uint32_t borrow = fp_sub_p(s, d);
+  return fp_select(borrow != 0, s, d);
+}
+
+BLS_HD Fp fp_add(const Fp& a, const Fp& b) {
+  Fp s;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)a.l[i] + b.l[i];
+    s.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return fp_reduce_once(s);  // a + b < 2p < 2^382: no carry out
+}
+
+BLS_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
+
+BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
+  Fp d;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.l[i] - b.l[i] - borrow;
+    d.l[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  // if a < b add p back
+  uint32_t mask = 0u - borrow;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)d.l[i] + (p_limb(i) & mask);
+    d.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return d;
+}
+
+BLS_HD Fp fp_neg(const Fp& a) {
+  Fp z = fp_zero();
+  return fp_sub(z, a);
+}
+
+// a / 2 mod p
+BLS_HD Fp fp_half(const Fp& a) {
+  uint32_t mask = 0u - (a.l[0] & 1u);
+  Fp s;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)a.l[i] + (p_limb(i) & mask);
+    s.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) r.l[i] = (s.l[i] >> 1) | (s.l[i + 1] << 31);
+  r.l[11] = s.l[11] >> 1;  // a + p < 2^382: bit 384 never set
+  return r;
+}
+
+// Montgomery product a*b/R mod p, CIOS with the no-carry optimisation
+// (valid because p's top limb 0x1a0111ea < 2^31 - 1).  Inputs < p, output < p.
+BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
+  BLS_COUNT_FPM();
+  uint32_t t[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint32_t bi = b.l[i];
+    uint64_t A = (uint64_t)a.l[0] * bi + t[0];
+    const uint32_t m = (uint32_t)A * BLS_NP0;
+    uint64_t C = (uint64_t)m * p_limb(0) + (uint32_t)A;
+    A >>= 32;
+    C >>= 32;
+#pragma unroll
+    for (int j = 1; j < 12; ++j) {
+      A = (uint64_t)a.l[j] * bi + t[j] + A;
+      C = (uint64_t)m * p_limb(j) + (uint32_t)A + C;
+      t[j - 1] = (uint32_t)C;
+      A >>= 32;
+      C >>= 32;
+    }
+    t[11] = (uint32_t)(C + A);
+  }
+  Fp r;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) r.l[j] = t[j];
+  return fp_reduce_once(r);
+}
+
+BLS_HD Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }
+
+BLS_HD Fp fp_to_mont(const Fp& a) { return fp_mul(a, c_r2()); }
+
+BLS_HD Fp fp_from_mont(const Fp& a) {
+  Fp one = fp_zero();
+  one.l[0] = 1;
+  return fp_mul(a, one);
+}
+
+// a^e for an exponent given as a limb accessor (wave-uniform, MSB first).
+template <uint32_t (*E)(int), int BITS>
+BLS_HD Fp fp_pow_const(const Fp& a) {
+  Fp r = a;  // top bit of every exponent used here is 1
+  for (int i = BITS - 2; i >= 0; --i) {
+    r = fp_sqr(r);
+    if ((E(i >> 5) >> (i & 31)) & 1u) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+BLS_HD Fp fp_inv(const Fp& a) { return fp_pow_const<e_p_minus_2, E_P_MINUS_2_BITS>(a); }
+
+// Is the (plain, non-Montgomery) value a > (p-1)/2 ?  (ZCash "lexicographically largest")
+BLS_HD bool fp_plain_gt_half(const Fp& a) {
+  const uint32_t h[12] = {BLS_HALF_P_LIMBS};
+  // compute h - a; borrow => a > h
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)h[i] - a.l[i] - borrow;
+    borrow = (uint32_t)(t >> 63);
+  }
+  return borrow != 0;
+}
+
+BLS_HD bool fp_lex_largest(const Fp& a_mont) { return fp_plain_gt_half(fp_from_mont(a_mont)); }
+
+// plain a < p ?
+BLS_HD bool fp_plain_is_canonical(const Fp& a) {
+  Fp d;
+  return fp_sub_p(a, d) != 0;
+}
+
+// 48 big-endian bytes -> plain limbs (no reduction)
+BLS_HD Fp fp_from_be48(const uint8_t* b) {
+  Fp r;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    const uint8_t* q = b + 44 - 4 * k;
+    r.l[k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+  return r;
+}
+
+BLS_HD void fp_to_be48(const Fp& a, uint8_t* b) {
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    uint8_t* q = b + 44 - 4 * k;
+    q[0] = (uint8_t)(a.l[k] >> 24);
+    q[1] = (uint8_t)(a.l[k] >> 16);
+    q[2] = (uint8_t)(a.l[k] >> 8);
+    q[3] = (uint8_t)a.l[k];
+  }
+}
+
+// Fp square root (p = 3 mod 4): returns true and r with r^2 = a if a is a square.
+BLS_HD bool fp_sqrt(const Fp& a, Fp& r) {
+  r = fp_pow_const<e_p_plus_1_div_4, E_P_PLUS_1_DIV_4_BITS>(a);
+  return fp_eq(fp_sqr(r), a);
+}
+
+// ---------------------------------------------------------------------------
+// Fp2 = Fp[u]/(u^2+1)
+// ---------------------------------------------------------------------------
+BLS_HD Fp2 fp2_zero() { return Fp2{fp_zero(), fp_zero()}; }
+BLS_HD Fp2 fp2_one() { return Fp2{c_one(), fp_zero()}; }
+BLS_HD bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+BLS_HD bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+BLS_HD Fp2 fp2_select(bool c, const Fp2& a, const Fp2& b) {
+  return Fp2{fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)};
+}
+BLS_HD Fp2 fp2_add(const Fp2& a, const Fp2& b) { return Fp2{fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+BLS_HD Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return Fp2{fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+BLS_HD Fp2 fp2_dbl(const Fp2& a) { return Fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
+BLS_HD Fp2 fp2_neg(const Fp2& a) { return Fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
+BLS_HD Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
+BLS_HD Fp2 fp2_half(const Fp2& a) { return Fp2{fp_half(a.c0), fp_half(a.c1)}; }
+BLS_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& b) { return Fp2{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+
+BLS_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+  Fp t0 = fp_mul(a.c0, b.c0);
+  Fp t1 = fp_mul(a.c1, b.c1);
+  Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+BLS_HD Fp2 fp2_sqr(const Fp2& a) {
+  Fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fp t1 = fp_mul(a.c0, a.c1);
+  return Fp2{t0, fp_dbl(t1)};
+}
+
+// a * (1 + u)
+BLS_HD Fp2 fp2_mul_xi(const Fp2& a) { return Fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+BLS_HD Fp2 fp2_inv(const Fp2& a) {
+  Fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  Fp ni = fp_inv(n);
+  return Fp2{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+
+// RFC 9380 sgn0 for m = 2 (on Montgomery inputs)
+BLS_HD uint32_t fp2_sgn0(const Fp2& a) {
+  Fp p0 = fp_from_mont(a.c0);
+  Fp p1 = fp_from_mont(a.c1);
+  uint32_t s0 = p0.l[0] & 1u;
+  uint32_t z0 = fp_is_zero(p0) ? 1u : 0u;
+  uint32_t s1 = p1.l[0] & 1u;
+  return s0 | (z0 & s1);
+}
+
+// ZCash serialization sign bit for G2 y (compare c1 first, c0 if c1 == 0)
+BLS_HD bool fp2_lex_largest(const Fp2& a) {
+  Fp p1 = fp_from_mont(a.c1);
+  if (!fp_is_zero(p1)) return fp_plain_gt_half(p1);
+  return fp_plain_gt_half(fp_from_mont(a.c0));
+}
+
+// Square root in Fp2 via the norm (two Fp exponentiations).  Returns false iff a
+// is not a square.  For a square a the result satisfies r^2 = a (either root).
+//   alpha = a0^2 + a1^2, gamma = sqrt(alpha)        (a square <=> alpha square)
+//   d = (a0 + gamma)/2, t = d^((p-3)/4)
+//   d square:      r = d t + (a1 t / 2) u
+//   d non-square:  r = (a1 t / 2) - (d t) u
+BLS_HD bool fp2_sqrt(const Fp2& a, Fp2& r) {
+  if (fp_is_zero(a.c1)) {
+    Fp s;
+    if (fp_sqrt(a.c0, s)) {
+      r = Fp2{s, fp_zero()};
+      return true;
+    }
+    // a0 non-square in Fp: sqrt(a0) = u * sqrt(-a0) since -1 is a non-square
+    fp_sqrt(fp_neg(a.c0), s);
+    r = Fp2{fp_zero(), s};
+    return true;
+  }
+  Fp alpha = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  Fp gamma;
+  if (!fp_sqrt(alpha, gamma)) return false;
+  Fp d = fp_half(fp_add(a.c0, gamma));
+  Fp t = fp_pow_const<e_p_minus_3_div_4, E_P_MINUS_3_DIV_4_BITS>(d);
+  Fp dt = fp_mul(d, t);
+  Fp a1t2 = fp_half(fp_mul(a.c1, t));
+  if (fp_eq(fp_sqr(dt), d)) {
+    r = Fp2{dt, a1t2};
+  } else {
+    r = Fp2{a1t2, fp_neg(dt)};
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Fp6 = Fp2[v]/(v^3 - xi)
+// ---------------------------------------------------------------------------
+BLS_HD Fp6 fp6_zero() { return Fp6{fp2_zero(), fp2_zero(), fp2_zero()}; }
+BLS_HD Fp6 fp6_one() { return Fp6{fp2_one(), fp2_zero(), fp2_zero()}; }
+BLS_HD Fp6 fp6_add(const Fp6& a, const Fp6& b) {
+  return Fp6{fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)};
+}
+BLS_HD Fp6 fp6_sub(const Fp6& a, const Fp6& b) {
+  return Fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)};
+}
+BLS_HD Fp6 fp6_neg(const Fp6& a) { return Fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+BLS_HD bool fp6_eq(const Fp6& a, const Fp6& b) {
+  return fp2_eq(a.c0, b.c0) && fp2_eq(a.c1, b.c1) && fp2_eq(a.c2, b.c2);
+}
+// a * v
+BLS_HD Fp6 fp6_mul_v(const Fp6& a) { return Fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+BLS_HD Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+  Fp2 t0 = fp2_mul(a.c0, b.c0);
+  Fp2 t1 = fp2_mul(a.c1, b.c1);
+  Fp2 t2 = fp2_mul(a.c2, b.c2);
+  Fp2 c0 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2);
+  c0 = fp2_add(fp2_mul_xi(c0), t0);
+  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1);
+  c1 = fp2_add(c1, fp2_mul_xi(t2));
+  Fp2 c2 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2);
+  c2 = fp2_add(c2, t1);
+  return Fp6{c0, c1, c2};
+}
+
+BLS_HD Fp6 fp6_sqr(const Fp6& a) { return fp6_mul(a, a); }
+
+// a * (d0 + d1 v)
+BLS_HD Fp6 fp6_mul_01(const Fp6& a, const Fp2& d0, const Fp2& d1) {
+  Fp2 a0d0 = fp2_mul(a.c0, d0);
+  Fp2 a1d1 = fp2_mul(a.c1, d1);
+  Fp2 c0 = fp2_add(a0d0, fp2_mul_xi(fp2_mul(a.c2, d1)));
+  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(d0, d1)), a0d0), a1d1);
+  Fp2 c2 = fp2_add(a1d1, fp2_mul(a.c2, d0));
+  return Fp6{c0, c1, c2};
+}
+
+// a * (d1 v)
+BLS_HD Fp6 fp6_mul_1(const Fp6& a, const Fp2& d1) {
+  return Fp6{fp2_mul_xi(fp2_mul(a.c2, d1)), fp2_mul(a.c0, d1), fp2_mul(a.c1, d1)};
+}
+
+BLS_HD Fp6 fp6_inv(const Fp6& a) {
+  Fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  Fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  Fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  Fp2 n = fp2_add(fp2_mul(a.c0, t0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, t1), fp2_mul(a.c1, t2))));
+  Fp2 ni = fp2_inv(n);
+  return Fp6{fp2_mul(t0, ni), fp2_mul(t1, ni), fp2_mul(t2, ni)};
+}
+
+// ---------------------------------------------------------------------------
+// Fp12 = Fp6[w]/(w^2 - v)
+// ---------------------------------------------------------------------------
+BLS_HD Fp12 fp12_one() { return Fp12{fp6_one(), fp6_zero()}; }
+BLS_HD bool fp12_eq(const Fp12& a, const Fp12& b) { return fp6_eq(a.c0, b.c0) && fp6_eq(a.c1, b.c1); }
+BLS_HD bool fp12_is_one(const Fp12& a) { return fp12_eq(a, fp12_one()); }
+BLS_HD Fp12 fp12_conj(const Fp12& a) { return Fp12{a.c0, fp6_neg(a.c1)}; }
+
+BLS_NOINLINE Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
+  Fp6 t0 = fp6_mul(a.c0, b.c0);
+  Fp6 t1 = fp6_mul(a.c1, b.c1);
+  Fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  Fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return Fp12{c0, c1};
+}
+
+// complex squaring: (A + Bw)^2 = (A^2 + v B^2) + 2AB w
+BLS_NOINLINE Fp12 fp12_sqr(const Fp12& a) {
+  Fp6 ab = fp6_mul(a.c0, a.c1);
+  Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  Fp6 c0 = fp6_sub(fp6_sub(s, ab), fp6_mul_v(ab));
+  Fp6 c1 = fp6_add(ab, ab);
+  return Fp12{c0, c1};
+}
+
+// f * (l0 + l2 w^2 + l3 w^3): the M-twist line shape (arkworks mul_by_014)
+BLS_NOINLINE Fp12 fp12_mul_line(const Fp12& f, const Fp2& l0, const Fp2& l2, const Fp2& l3) {
+  Fp6 aa = fp6_mul_01(f.c0, l0, l2);
+  Fp6 bb = fp6_mul_1(f.c1, l3);
+  Fp6 c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l2, l3)), aa), bb);
+  Fp6 c0 = fp6_add(aa, fp6_mul_v(bb));
+  return Fp12{c0, c1};
+}
+
+BLS_HD Fp12 fp12_inv(const Fp12& a) {
+  Fp6 n = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
+  Fp6 ni = fp6_inv(n);
+  return Fp12{fp6_mul(a.c0, ni), fp6_neg(fp6_mul(a.c1, ni))};
+}
+
+// f^p: coefficient k of w^k -> conj(c_k) * xi^(k(p-1)/6)
+BLS_HD Fp12 fp12_frob(const Fp12& a) {
+  Fp12 r;
+  r.c0.c0 = fp2_conj(a.c0.c0);                          // w^0
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), c_frob1_1());    // w^1
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), c_frob1_2());    // w^2
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), c_frob1_3());    // w^3
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), c_frob1_4());    // w^4
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), c_frob1_5());    // w^5
+  return r;
+}
+
+// f^(p^2): coefficient k -> c_k * xi^(k(p^2-1)/6)  (an Fp scalar)
+BLS_HD Fp12 fp12_frob2(const Fp12& a) {
+  Fp12 r;
+  r.c0.c0 = a.c0.c0;
+  r.c1.c0 = fp2_mul_fp(a.c1.c0, c_frob2_1());
+  r.c0.c1 = fp2_mul_fp(a.c0.c1, c_frob2_2());
+  r.c1.c1 = fp2_mul_fp(a.c1.c1, c_frob2_3());
+  r.c0.c2 = fp2_mul_fp(a.c0.c2, c_frob2_4());
+  r.c1.c2 = fp2_mul_fp(a.c1.c2, c_frob2_5());
+  return r;
+}
+
+// Granger-Scott squaring for elements of the cyclotomic subgroup G_{Phi_12(p)}.
+// View f = g0 + g1 w + g2 w^2 over Fp4 = Fp2[s]/(s^2 - xi), s = w^3, with
+// g0 = c0 + c3 s, g1 = c1 + c4 s, g2 = c2 + c5 s (c_k = coefficient of w^k).
+//   f^2 = (3 g0^2 - 2 conj(g0)) + (3 s g2^2 + 2 conj(g1)) w + (3 g1^2 - 2 conj(g2)) w^2
+// where conj negates the s part.
+BLS_HD void fp4_sqr(const Fp2& x, const Fp2& y, Fp2& rx, Fp2& ry) {
+  Fp2 t0 = fp2_sqr(x);
+  Fp2 t1 = fp2_sqr(y);
+  rx = fp2_add(t0, fp2_mul_xi(t1));
+  ry = fp2_sub(fp2_sub(fp2_sqr(fp2_add(x, y)), t0), t1);
+}
+
+BLS_NOINLINE Fp12 fp12_cyclotomic_sqr(const Fp12& f) {
+  // c_k: c0=f.c0.c0 c1=f.c1.c0 c2=f.c0.c1 c3=f.c1.c1 c4=f.c0.c2 c5=f.c1.c2
+  Fp2 a0, a1, b0, b1, d0, d1;
+  fp4_sqr(f.c0.c0, f.c1.c1, a0, a1);  // g0^2
+  fp4_sqr(f.c1.c0, f.c0.c2, b0, b1);  // g1^2
+  fp4_sqr(f.c0.c1, f.c1.c2, d0, d1);  // g2^2
+  Fp12 r;
+  // new g0 = 3 g0^2 - 2 conj(g0):  (3 a0 - 2 c0,  3 a1 + 2 c3)
+  r.c0.c0 = fp2_add(fp2_dbl(fp2_sub(a0, f.c0.c0)), a0);
+  r.c1.c1 = fp2_add(fp2_dbl(fp2_add(a1, f.c1.c1)), a1);
+  // new g1 = 3 s g2^2 + 2 conj(g1):  s (d0 + d1 s) = xi d1 + d0 s
+  //   (3 xi d1 + 2 c1,  3 d0 - 2 c4)
+  Fp2 xd1 = fp2_mul_xi(d1);
+  r.c1.c0 = fp2_add(fp2_dbl(fp2_add(xd1, f.c1.c0)), xd1);
+  r.c0.c2 = fp2_add(fp2_dbl(fp2_sub(d0, f.c0.c2)), d0);
+  // new g2 = 3 g1^2 - 2 conj(g2):  (3 b0 - 2 c2,  3 b1 + 2 c5)
+  r.c0.c1 = fp2_add(fp2_dbl(fp2_sub(b0, f.c0.c1)), b0);
+  r.c1.c2 = fp2_add(fp2_dbl(fp2_add(b1, f.c1.c2)), b1);
+  return r;
+}
+
+}  // namespace bls

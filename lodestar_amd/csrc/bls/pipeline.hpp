@@ -1,0 +1,290 @@
+// Per-thread stage bodies of the batch-verify pipeline, shared by the HIP kernels
+// (lodestar_amd/csrc/bls_gpu.hip: one lane per set / request / chunk) and the CPU
+// test harness (tests/native/hostsim.cpp, which loops the same bodies).
+//
+// Semantics follow the reference worker (beacon-node/src/chain/bls/multithread/
+// worker.ts:32-108) and verifySignatureSetsMaybeBatch (chain/bls/maybeBatch.ts:16-39):
+//   stage_pk          deserializeSet / getAggregatedPubkey      (worker.ts:110-116, utils.ts:5-16)
+//   stage_sig         Signature.fromBytes(sig, affine, true)    (maybeBatch.ts:23,36)
+//   stage_h2c         hash_to_G2(signingRoot)                   ([ext] blst)
+//   stage_scale       r_i * pk_i, r_i * sig_i, 64-bit r_i       ([ext] verifyMultipleSignatures)
+//   stage_miller_set  f_i = ML(r_i pk_i, H(m_i))
+//   stage_req_status  per-request error precedence              (worker.ts:45, maybeBatch.ts:16-39)
+//   stage_chunk       prod f_i * ML(-g1, sum r_i sig_i) -> FE == 1 per chunk of >= 16 requests
+//   stage_indiv       the same per request (fallback / non-batchable, worker.ts:76-98)
+#pragma once
+
+#include "../../../include/lodestar_bls.h"
+#include "hash_to_curve.hpp"
+#include "pairing.hpp"
+
+namespace bls {
+
+struct PipeBufs {
+  uint32_t n_sets, n_reqs, n_chunks, n_indiv;
+  // inputs
+  const uint32_t* req_off;     // n_reqs + 1
+  const uint8_t* pubkeys;      // raw mode: n_sets * 96
+  const uint32_t* set_pk_off;  // table mode (nullable)
+  const uint32_t* pk_idx;
+  const G1A* pk_table;
+  uint32_t pk_table_n;
+  const uint8_t* msgs;         // n_sets * 32
+  const uint8_t* sigs;         // n_sets * 96
+  const uint32_t* sig_lens;    // nullable
+  const uint32_t* seed;        // 8 words
+  const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs
+  const uint32_t* chunk_reqs;
+  const uint32_t* indiv_reqs;  // n_indiv
+  // intermediates
+  G2A* sig;
+  int32_t* sig_status;
+  G1J* pk;
+  int32_t* pk_status;
+  G2A* H;
+  G1J* rpk;
+  G2J* rsig;
+  Fp12* f;
+  int32_t* req_status;
+  // outputs
+  int32_t* chunk_ok;       // n_chunks: 1 ok, 0 failed (retry)
+  int32_t* indiv_verdict;  // n_indiv: 1 / 0 / -code
+};
+
+BLS_HD void scalar_words_from_be32(const uint8_t* b, uint32_t k[8]) {
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* q = b + 28 - 4 * i;
+    k[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+}
+
+// r_i = first 8 bytes of SHA-256(seed || LE32(i)), forced non-zero
+// (the reference draws randomBytesNonZero(8) per set, [ext] @chainsafe/blst).
+BLS_HD uint64_t set_scalar(const uint32_t seed[8], uint32_t i) {
+  uint32_t W[16];
+  for (int k = 0; k < 8; ++k) W[k] = seed[k];
+  W[8] = ((i & 0xffu) << 24) | (((i >> 8) & 0xffu) << 16) | (((i >> 16) & 0xffu) << 8) | (i >> 24);
+  W[9] = 0x80000000u;
+  for (int k = 10; k < 15; ++k) W[k] = 0;
+  W[15] = 36 * 8;
+  uint32_t s[8];
+  sha256_init(s);
+  sha256_compress(s, W);
+  uint64_t r = ((uint64_t)s[0] << 32) | s[1];
+  return r ? r : 1ull;
+}
+
+BLS_HD void stage_pk(const PipeBufs& b, uint32_t i) {
+  if (i >= b.n_sets) return;
+  int32_t code = BLS_OK;
+  G1J acc = jac_infinity<Fp>();
+  if (b.set_pk_off) {
+    uint32_t beg = b.set_pk_off[i], end = b.set_pk_off[i + 1];
+    if (beg == end) code = BLS_EMPTY_AGGREGATE;
+    for (uint32_t k = beg; k < end; ++k) {
+      uint32_t idx = b.pk_idx[k];
+      if (idx >= b.pk_table_n) {
+        code = BLS_BAD_ENCODING;
+        break;
+      }
+      acc = jac_add_aff(acc, b.pk_table[idx]);
+    }
+  } else {
+    G1A a;
+    code = g1_deserialize96(b.pubkeys + 96ull * i, a);
+    if (code == BLS_OK) acc = jac_from_aff(a);
+  }
+  b.pk[i] = acc;
+  b.pk_status[i] = code;
+}
+
+BLS_HD void stage_sig(const PipeBufs& b, uint32_t i) {
+  if (i >= b.n_sets) return;
+  G2A s;
+  s.inf = true;
+  s.x = fp2_zero();
+  s.y = fp2_zero();
+  int32_t code;
+  if (b.sig_lens && b.sig_lens[i] != 96) {
+    code = BLS_INVALID_SIZE;
+  } else {
+    code = g2_decompress96(b.sigs + 96ull * i, s);
+    if (code == BLS_OK && !g2_in_subgroup(s)) code = BLS_POINT_NOT_IN_GROUP;
+  }
+  b.sig[i] = s;
+  b.sig_status[i] = code;
+}
+
+BLS_HD void stage_h2c(const PipeBufs& b, uint32_t i) {
+  if (i >= b.n_sets) return;
+  uint32_t w[8];
+  msg_words_from_bytes(b.msgs + 32ull * i, w);
+  b.H[i] = hash_to_g2(w);
+}
+
+BLS_HD void stage_scale(const PipeBufs& b, uint32_t i) {
+  if (i >= b.n_sets) return;
+  uint64_t r = set_scalar(b.seed, i);
+  if (b.pk_status[i] == BLS_OK && b.sig_status[i] == BLS_OK) {
+    b.rpk[i] = jac_mul_u64(b.pk[i], r);
+    b.rsig[i] = aff_mul_u64(b.sig[i], r);
+  } else {
+    b.rpk[i] = jac_infinity<Fp>();
+    b.rsig[i] = jac_infinity<Fp2>();
+  }
+}
+
+BLS_HD void stage_miller_set(const PipeBufs& b, uint32_t i) {
+  if (i >= b.n_sets) return;
+  if (b.pk_status[i] == BLS_OK && b.sig_status[i] == BLS_OK && !jac_is_inf(b.rpk[i])) {
+    b.f[i] = miller_loop(g1_eval_from_jac(b.rpk[i]), b.H[i]);
+  } else {
+    b.f[i] = fp12_one();
+  }
+}
+
+// Error precedence per request (r): pk decode / aggregation errors (deserializeSet
+// runs first, worker.ts:45), then signature decode errors in set order
+// (maybeBatch.ts:19-24 maps fromBytes over the sets), then the infinity rules
+// of Signature.verify / verifyMultipleSignatures (oracle core_verify / verify_multiple).
+BLS_HD void stage_req_status(const PipeBufs& b, uint32_t r) {
+  if (r >= b.n_reqs) return;
+  uint32_t beg = b.req_off[r], end = b.req_off[r + 1];
+  int32_t code = BLS_OK;
+  if (beg == end) code = BLS_EMPTY_SET;
+  for (uint32_t i = beg; i < end && code == BLS_OK; ++i)
+    if (b.pk_status[i] != BLS_OK) code = b.pk_status[i];
+  for (uint32_t i = beg; i < end && code == BLS_OK; ++i)
+    if (b.sig_status[i] != BLS_OK) code = b.sig_status[i];
+  if (code == BLS_OK) {
+    if (end - beg == 1) {
+      if (b.sig[beg].inf) code = BLS_ZERO_SIGNATURE;
+      else if (jac_is_inf(b.pk[beg])) code = BLS_PK_IS_INFINITY;
+    } else {
+      for (uint32_t i = beg; i < end && code == BLS_OK; ++i)
+        if (jac_is_inf(b.pk[i])) code = BLS_PK_IS_INFINITY;
+    }
+  }
+  b.req_status[r] = code;
+}
+
+// prod_{i in sets} f_i * ML(-g1, sum r_i sig_i), final exponentiation, == 1
+BLS_HD bool check_sets(const PipeBufs& b, Fp12 F, const G2J& S) {
+  G1Eval ng1;
+  ng1.xz = c_g1_x();
+  ng1.y = c_g1_negy();
+  ng1.z3 = c_one();
+  G2A Sa = jac_to_aff(S);
+  F = fp12_mul(F, miller_loop(ng1, Sa));
+  return fp12_is_one(final_exponentiation(F));
+}
+
+BLS_HD void stage_chunk(const PipeBufs& b, uint32_t c) {
+  if (c >= b.n_chunks) return;
+  uint32_t beg = b.chunk_off[c], end = b.chunk_off[c + 1];
+  for (uint32_t k = beg; k < end; ++k) {
+    if (b.req_status[b.chunk_reqs[k]] != BLS_OK) {
+      b.chunk_ok[c] = 0;  // the batch would throw -> retry every request (worker.ts:81-87)
+      return;
+    }
+  }
+  Fp12 F = fp12_one();
+  G2J S = jac_infinity<Fp2>();
+  for (uint32_t k = beg; k < end; ++k) {
+    uint32_t r = b.chunk_reqs[k];
+    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) {
+      F = fp12_mul(F, b.f[i]);
+      S = jac_add(S, b.rsig[i]);
+    }
+  }
+  b.chunk_ok[c] = check_sets(b, F, S) ? 1 : 0;
+}
+
+BLS_HD void stage_indiv(const PipeBufs& b, uint32_t t) {
+  if (t >= b.n_indiv) return;
+  uint32_t r = b.indiv_reqs[t];
+  int32_t code = b.req_status[r];
+  if (code != BLS_OK) {
+    b.indiv_verdict[t] = -code;
+    return;
+  }
+  Fp12 F = fp12_one();
+  G2J S = jac_infinity<Fp2>();
+  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) {
+    F = fp12_mul(F, b.f[i]);
+    S = jac_add(S, b.rsig[i]);
+  }
+  b.indiv_verdict[t] = check_sets(b, F, S) ? 1 : 0;
+}
+
+}  // namespace bls
+
+// Host-side planning (plain host functions; parsed but not emitted in the device pass).
+#include <stdlib.h>
+#include <vector>
+
+namespace bls {
+
+// chunkifyMaximizeChunkSize (beacon-node/src/chain/bls/multithread/utils.ts:4-19)
+static inline void chunkify_maximize_chunk_size(uint32_t n, uint32_t min_per_chunk, std::vector<uint32_t>& bounds) {
+  bounds.clear();
+  uint32_t chunk_count = n / min_per_chunk;
+  bounds.push_back(0);
+  if (chunk_count <= 1) {
+    bounds.push_back(n);
+    return;
+  }
+  uint32_t per = (n + chunk_count - 1) / chunk_count;
+  for (uint32_t i = per; i < n; i += per) bounds.push_back(i);
+  bounds.push_back(n);
+}
+
+// Host-side plan of one verify call: chunks over the batchable requests
+// (BATCHABLE_MIN_PER_CHUNK = 16, worker.ts:17,56) and the non-batchable list.
+struct BatchPlan {
+  std::vector<uint32_t> chunk_off, chunk_reqs, nonbatch_reqs;
+};
+
+static inline void plan_batch(const bls_batch* in, BatchPlan& p) {
+  std::vector<uint32_t> batchable;
+  p.nonbatch_reqs.clear();
+  for (uint32_t r = 0; r < in->n_reqs; ++r) {
+    if (in->req_batchable && in->req_batchable[r]) batchable.push_back(r);
+    else p.nonbatch_reqs.push_back(r);
+  }
+  p.chunk_off.clear();
+  p.chunk_reqs = batchable;
+  if (batchable.empty()) {
+    p.chunk_off.push_back(0);
+    return;
+  }
+  chunkify_maximize_chunk_size((uint32_t)batchable.size(), 16, p.chunk_off);
+}
+
+// Fill verdicts / stats from chunk results and the individual pass.
+static inline void assemble_verdicts(const bls_batch* in, const BatchPlan& p, const int32_t* chunk_ok,
+                                     const std::vector<uint32_t>& indiv_reqs, const int32_t* indiv_verdict,
+                                     int32_t* verdicts, bls_stats* stats) {
+  uint32_t n_chunks = (uint32_t)p.chunk_off.size() - 1;
+  uint32_t retries = 0, sigs_ok = 0;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    if (chunk_ok[c] == 1) {
+      for (uint32_t k = p.chunk_off[c]; k < p.chunk_off[c + 1]; ++k) {
+        uint32_t r = p.chunk_reqs[k];
+        verdicts[r] = 1;
+        sigs_ok += in->req_set_offsets[r + 1] - in->req_set_offsets[r];
+      }
+    } else {
+      ++retries;
+    }
+  }
+  for (size_t t = 0; t < indiv_reqs.size(); ++t) verdicts[indiv_reqs[t]] = indiv_verdict[t];
+  if (stats) {
+    stats->batch_retries = retries;
+    stats->batch_sigs_success = sigs_ok;
+    stats->n_chunks = n_chunks;
+    stats->n_individual = (uint32_t)indiv_reqs.size();
+  }
+}
+
+}  // namespace bls

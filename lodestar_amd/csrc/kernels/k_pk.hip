@@ -1,0 +1,50 @@
+// Pubkey stage: deserialize raw 96-byte keys or sum device-table keys (aggregate sets),
+// plus the pubkey-table loader and the per-request status pass (small kernels).
+#include "../launchers.hpp"
+
+using namespace bls;
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_pk(PipeBufs b) { stage_pk(b, blockIdx.x * BLS_BLOCK + threadIdx.x); }
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_aggregate(PipeBufs b, uint8_t* out96) {
+  uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  stage_pk(b, i);
+  if (i < b.n_sets) g1_serialize96(jac_to_aff(b.pk[i]), out96 + 96ull * i);
+}
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len,
+                                                            G1A* out, int32_t* codes) {
+  uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  G1A a;
+  int32_t c = pk_len == 48 ? g1_decompress48(pks + 48ull * i, a) : g1_deserialize96(pks + 96ull * i, a);
+  if (c != BLS_OK) {
+    a.inf = true;
+    a.x = fp_zero();
+    a.y = fp_zero();
+  }
+  out[i] = a;
+  codes[i] = c;
+}
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_status(PipeBufs b) {
+  stage_req_status(b, blockIdx.x * BLS_BLOCK + threadIdx.x);
+}
+
+hipError_t launch_k_pk(const PipeBufs& b, hipStream_t s) {
+  k_pk<<<bls_grid_for(b.n_sets), BLS_BLOCK, 0, s>>>(b);
+  return hipGetLastError();
+}
+hipError_t launch_k_aggregate(const PipeBufs& b, uint8_t* out96, hipStream_t s) {
+  k_aggregate<<<bls_grid_for(b.n_sets), BLS_BLOCK, 0, s>>>(b, out96);
+  return hipGetLastError();
+}
+hipError_t launch_k_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, G1A* out, int32_t* codes,
+                                 hipStream_t s) {
+  k_load_pubkeys<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(pks, n, pk_len, out, codes);
+  return hipGetLastError();
+}
+hipError_t launch_k_status(const PipeBufs& b, hipStream_t s) {
+  k_status<<<bls_grid_for(b.n_reqs), BLS_BLOCK, 0, s>>>(b);
+  return hipGetLastError();
+}

@@ -1,0 +1,26 @@
+// Host-side launchers, one per kernel translation unit (lodestar_amd/csrc/kernels/*.hip).
+// Each heavy kernel lives in its own TU so the build compiles them in parallel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "bls/pipeline.hpp"
+
+#define BLS_BLOCK 64
+
+static inline unsigned bls_grid_for(uint32_t n) { return (n + BLS_BLOCK - 1) / BLS_BLOCK; }
+
+hipError_t launch_k_pk(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_aggregate(const bls::PipeBufs& b, uint8_t* out96, hipStream_t s);
+hipError_t launch_k_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, bls::G1A* out, int32_t* codes,
+                                 hipStream_t s);
+hipError_t launch_k_status(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_sig(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_h2c(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_hash_to_g2(const uint8_t* msgs, uint32_t n, uint8_t* out192, hipStream_t s);
+hipError_t launch_k_scale(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_miller(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_chunk(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_indiv(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_sk_to_pk(const uint8_t* sks, uint32_t n, uint8_t* out48, hipStream_t s);
+hipError_t launch_k_sign(const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t s);

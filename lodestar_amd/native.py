@@ -1,0 +1,203 @@
+"""Thin Python handle over the C-ABI (include/lodestar_bls.h) for one GPU.
+
+`GpuContext` owns one `bls_gpu_ctx` (one device, one HIP stream, the device
+pubkey table).  Buffers are numpy arrays handed over as raw pointers; the
+library copies them into pinned staging, so nothing is retained after a call.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._abi import BlsBatch, BlsStats, load_library
+
+
+def _ptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u8(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8)
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+@dataclass
+class PackedBatch:
+    """SoA form of one verifyManySignatureSets call (bls_batch)."""
+
+    req_set_offsets: np.ndarray  # uint32[n_reqs + 1]
+    req_batchable: np.ndarray  # uint8[n_reqs]
+    messages: np.ndarray  # uint8[n_sets * 32]
+    signatures: np.ndarray  # uint8[n_sets * 96]
+    pubkeys: np.ndarray | None = None  # uint8[n_sets * 96]
+    set_pk_offsets: np.ndarray | None = None  # uint32[n_sets + 1]
+    pk_indices: np.ndarray | None = None  # uint32[...]
+    signature_lens: np.ndarray | None = None  # uint32[n_sets]
+    seed: bytes | None = None
+
+    @property
+    def n_sets(self) -> int:
+        return int(self.req_set_offsets[-1])
+
+    @property
+    def n_reqs(self) -> int:
+        return len(self.req_set_offsets) - 1
+
+
+def pack_requests(requests, seed: bytes | None = None) -> PackedBatch:
+    """requests: list of (batchable: bool, sets) where each set is (pk, msg32, sig).
+
+    pk is either 96 raw bytes (uncompressed affine) or a list/tuple of device
+    pubkey-table indices (all sets of one batch must use the same form).  sig may
+    have any length (a length other than 96 yields BLST_INVALID_SIZE)."""
+    offs = [0]
+    batchable = []
+    msgs, sigs, lens = [], [], []
+    raw_pks, idx_offs, idx = [], [0], []
+    table_mode = None
+    for is_b, sets in requests:
+        batchable.append(1 if is_b else 0)
+        for pk, msg, sig in sets:
+            this_table = not isinstance(pk, (bytes, bytearray, memoryview, np.ndarray))
+            if table_mode is None:
+                table_mode = this_table
+            if table_mode != this_table:
+                raise ValueError("mixed raw / table pubkeys in one batch")
+            if table_mode:
+                idx.extend(int(i) for i in pk)
+                idx_offs.append(len(idx))
+            else:
+                raw_pks.append(bytes(pk))
+            if len(msg) != 32:
+                raise ValueError("signing roots are 32 bytes")
+            msgs.append(bytes(msg))
+            sb = bytes(sig)
+            lens.append(len(sb))
+            sigs.append(sb[:96].ljust(96, b"\0"))
+        offs.append(len(msgs))
+    n = len(msgs)
+    pb = PackedBatch(
+        req_set_offsets=np.array(offs, dtype=np.uint32),
+        req_batchable=np.array(batchable, dtype=np.uint8),
+        messages=np.frombuffer(b"".join(msgs), dtype=np.uint8).copy() if n else np.zeros(1, np.uint8),
+        signatures=np.frombuffer(b"".join(sigs), dtype=np.uint8).copy() if n else np.zeros(1, np.uint8),
+        seed=seed,
+    )
+    if any(L != 96 for L in lens):
+        pb.signature_lens = np.array(lens, dtype=np.uint32)
+    if table_mode:
+        pb.set_pk_offsets = np.array(idx_offs, dtype=np.uint32)
+        pb.pk_indices = np.array(idx if idx else [0], dtype=np.uint32)
+    else:
+        pb.pubkeys = np.frombuffer(b"".join(raw_pks), dtype=np.uint8).copy() if n else np.zeros(96, np.uint8)
+    return pb
+
+
+class GpuContext:
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        ndev = self.lib.bls_gpu_device_count()
+        if ndev <= device:
+            raise NativeError(f"no HIP device {device} (visible: {ndev}); the verifier has no CPU fallback")
+        h = ctypes.c_void_p()
+        if self.lib.bls_gpu_init(device, ctypes.byref(h)) != 0:
+            raise NativeError(f"bls_gpu_init({device}) failed")
+        self._h = h
+        self.device = device
+
+    # -- lifecycle ------------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            self.lib.bls_gpu_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc < 0:
+            msg = self.lib.bls_gpu_last_error(self._h)
+            raise NativeError(f"{what}: {msg.decode() if msg else rc}")
+
+    # -- pubkey table ---------------------------------------------------------
+    def load_pubkeys(self, pks: bytes | np.ndarray, pk_len: int = 48) -> np.ndarray:
+        arr = _u8(pks)
+        n = arr.size // pk_len
+        codes = np.zeros(max(n, 1), dtype=np.int32)
+        rc = self.lib.bls_gpu_load_pubkeys(self._h, _ptr(arr), n, pk_len, _ptr(codes))
+        self._check(rc, "bls_gpu_load_pubkeys")
+        return codes[:n]
+
+    # -- verification -------------------------------------------------------------
+    def verify_packed(self, pb: PackedBatch) -> tuple[np.ndarray, BlsStats]:
+        keep = []
+        b = BlsBatch()
+        b.n_sets = pb.n_sets
+        b.n_reqs = pb.n_reqs
+        for field in ("req_set_offsets", "req_batchable", "messages", "signatures", "pubkeys", "set_pk_offsets",
+                      "pk_indices", "signature_lens"):
+            a = getattr(pb, field)
+            if a is not None:
+                a = np.ascontiguousarray(a)
+                keep.append(a)
+            setattr(b, field, _ptr(a))
+        seed_buf = None
+        if pb.seed is not None:
+            seed_buf = ctypes.create_string_buffer(bytes(pb.seed), 32)
+            b.seed = ctypes.cast(seed_buf, ctypes.c_void_p)
+        verdicts = np.zeros(max(pb.n_reqs, 1), dtype=np.int32)
+        stats = BlsStats()
+        rc = self.lib.bls_gpu_verify(self._h, ctypes.byref(b), _ptr(verdicts), ctypes.byref(stats))
+        self._check(rc, "bls_gpu_verify")
+        return verdicts[: pb.n_reqs], stats
+
+    # -- standalone primitives (parity tests, fixtures) ---------------------------
+    def aggregate_pubkeys(self, index_lists) -> tuple[list[bytes], np.ndarray]:
+        offs = [0]
+        idx = []
+        for lst in index_lists:
+            idx.extend(int(i) for i in lst)
+            offs.append(len(idx))
+        n = len(index_lists)
+        o = np.array(offs, dtype=np.uint32)
+        ix = np.array(idx if idx else [0], dtype=np.uint32)
+        out = np.zeros(96 * max(n, 1), dtype=np.uint8)
+        codes = np.zeros(max(n, 1), dtype=np.int32)
+        rc = self.lib.bls_gpu_aggregate_pubkeys(self._h, _ptr(o), _ptr(ix), n, _ptr(out), _ptr(codes))
+        self._check(rc, "bls_gpu_aggregate_pubkeys")
+        raw = out.tobytes()
+        return [raw[96 * i: 96 * i + 96] for i in range(n)], codes[:n]
+
+    def hash_to_g2(self, msgs: bytes | np.ndarray) -> np.ndarray:
+        m = _u8(msgs)
+        n = m.size // 32
+        out = np.zeros(192 * max(n, 1), dtype=np.uint8)
+        self._check(self.lib.bls_gpu_hash_to_g2(self._h, _ptr(m), n, _ptr(out)), "bls_gpu_hash_to_g2")
+        return out[: 192 * n].reshape(n, 192)
+
+    def sk_to_pk(self, sks: bytes | np.ndarray) -> np.ndarray:
+        s = _u8(sks)
+        n = s.size // 32
+        out = np.zeros(48 * max(n, 1), dtype=np.uint8)
+        self._check(self.lib.bls_gpu_sk_to_pk(self._h, _ptr(s), n, _ptr(out)), "bls_gpu_sk_to_pk")
+        return out[: 48 * n].reshape(n, 48)
+
+    def sign(self, sks: bytes | np.ndarray, msgs: bytes | np.ndarray) -> np.ndarray:
+        s, m = _u8(sks), _u8(msgs)
+        n = s.size // 32
+        out = np.zeros(96 * max(n, 1), dtype=np.uint8)
+        self._check(self.lib.bls_gpu_sign(self._h, _ptr(s), _ptr(m), n, _ptr(out)), "bls_gpu_sign")
+        return out[: 96 * n].reshape(n, 96)

@@ -1,0 +1,296 @@
+// TEST INFRASTRUCTURE ONLY -- never linked into the product library.
+//
+// Compiles the HIP kernels' __host__ __device__ math (lodestar_amd/csrc/bls/*.hpp)
+// for the CPU so tests/ can check every device routine against the Python
+// oracle (oracle/bls_oracle.py) without a GPU, and count Fp multiplications per
+// stage (the algorithmic work model behind bench.py's roofline figure).
+//
+// All byte interfaces use canonical big-endian encodings:
+//   Fp = 48 B; Fp2 = c0 || c1 (96 B); Fp12 = w-basis coefficients k = 0..5, each Fp2 (576 B);
+//   G1 = 96 B uncompressed (x || y); G2 = 192 B uncompressed (ZCash order x.c1 x.c0 y.c1 y.c0).
+#include <string.h>
+
+#include "bls/pairing.hpp"
+#include "bls/hash_to_curve.hpp"
+#include "bls/pipeline.hpp"
+
+unsigned long long bls_fpm_counter = 0;
+
+using namespace bls;
+
+static Fp rd_fp(const uint8_t* b) { return fp_to_mont(fp_from_be48(b)); }
+static void wr_fp(const Fp& a, uint8_t* b) { fp_to_be48(fp_from_mont(a), b); }
+static Fp2 rd_fp2(const uint8_t* b) { return Fp2{rd_fp(b), rd_fp(b + 48)}; }
+static void wr_fp2(const Fp2& a, uint8_t* b) {
+  wr_fp(a.c0, b);
+  wr_fp(a.c1, b + 48);
+}
+static Fp2* coef(Fp12& f, int k) {
+  switch (k) {
+    case 0: return &f.c0.c0;
+    case 1: return &f.c1.c0;
+    case 2: return &f.c0.c1;
+    case 3: return &f.c1.c1;
+    case 4: return &f.c0.c2;
+    default: return &f.c1.c2;
+  }
+}
+static Fp12 rd_fp12(const uint8_t* b) {
+  Fp12 f;
+  for (int k = 0; k < 6; ++k) *coef(f, k) = rd_fp2(b + 96 * k);
+  return f;
+}
+static void wr_fp12(Fp12 f, uint8_t* b) {
+  for (int k = 0; k < 6; ++k) wr_fp2(*coef(f, k), b + 96 * k);
+}
+static G1A rd_g1(const uint8_t* b) {
+  G1A a;
+  a.inf = (b[0] & 0x40) != 0;
+  if (a.inf) {
+    a.x = fp_zero();
+    a.y = fp_zero();
+  } else {
+    a.x = rd_fp(b);
+    a.y = rd_fp(b + 48);
+  }
+  return a;
+}
+static G2A rd_g2(const uint8_t* b) {
+  G2A a;
+  a.inf = (b[0] & 0x40) != 0;
+  if (a.inf) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  } else {
+    a.x = Fp2{rd_fp(b + 48), rd_fp(b)};
+    a.y = Fp2{rd_fp(b + 144), rd_fp(b + 96)};
+  }
+  return a;
+}
+
+extern "C" {
+
+unsigned long long hs_fpm_count(void) { return bls_fpm_counter; }
+void hs_fpm_reset(void) { bls_fpm_counter = 0; }
+
+void hs_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_mul(rd_fp(a), rd_fp(b)), out); }
+void hs_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_add(rd_fp(a), rd_fp(b)), out); }
+void hs_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_sub(rd_fp(a), rd_fp(b)), out); }
+void hs_fp_half(const uint8_t* a, uint8_t* out) { wr_fp(fp_half(rd_fp(a)), out); }
+void hs_fp_inv(const uint8_t* a, uint8_t* out) { wr_fp(fp_inv(rd_fp(a)), out); }
+int hs_fp_sqrt(const uint8_t* a, uint8_t* out) {
+  Fp r;
+  bool ok = fp_sqrt(rd_fp(a), r);
+  wr_fp(r, out);
+  return ok;
+}
+
+void hs_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp2(fp2_mul(rd_fp2(a), rd_fp2(b)), out); }
+void hs_fp2_sqr(const uint8_t* a, uint8_t* out) { wr_fp2(fp2_sqr(rd_fp2(a)), out); }
+void hs_fp2_inv(const uint8_t* a, uint8_t* out) { wr_fp2(fp2_inv(rd_fp2(a)), out); }
+int hs_fp2_sqrt(const uint8_t* a, uint8_t* out) {
+  Fp2 r = fp2_zero();
+  bool ok = fp2_sqrt(rd_fp2(a), r);
+  wr_fp2(r, out);
+  return ok;
+}
+int hs_fp2_sgn0(const uint8_t* a) { return (int)fp2_sgn0(rd_fp2(a)); }
+
+void hs_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp12(fp12_mul(rd_fp12(a), rd_fp12(b)), out); }
+void hs_fp12_sqr(const uint8_t* a, uint8_t* out) { wr_fp12(fp12_sqr(rd_fp12(a)), out); }
+void hs_fp12_cyclotomic_sqr(const uint8_t* a, uint8_t* out) { wr_fp12(fp12_cyclotomic_sqr(rd_fp12(a)), out); }
+void hs_fp12_inv(const uint8_t* a, uint8_t* out) { wr_fp12(fp12_inv(rd_fp12(a)), out); }
+void hs_fp12_frob(const uint8_t* a, uint8_t* out) { wr_fp12(fp12_frob(rd_fp12(a)), out); }
+void hs_fp12_frob2(const uint8_t* a, uint8_t* out) { wr_fp12(fp12_frob2(rd_fp12(a)), out); }
+void hs_fp12_mul_line(const uint8_t* f, const uint8_t* l0, const uint8_t* l2, const uint8_t* l3, uint8_t* out) {
+  wr_fp12(fp12_mul_line(rd_fp12(f), rd_fp2(l0), rd_fp2(l2), rd_fp2(l3)), out);
+}
+void hs_final_exp(const uint8_t* a, uint8_t* out) { wr_fp12(final_exponentiation(rd_fp12(a)), out); }
+
+void hs_miller_loop(const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
+  wr_fp12(miller_loop(g1_eval_from_aff(rd_g1(g1)), rd_g2(g2)), out);
+}
+// Miller loop with the G1 point given in Jacobian form (x z^2, y z^3, z) for a scaling z
+void hs_miller_loop_jac(const uint8_t* g1, const uint8_t* z48, const uint8_t* g2, uint8_t* out) {
+  G1A a = rd_g1(g1);
+  Fp z = rd_fp(z48);
+  G1J j;
+  Fp z2 = fp_sqr(z);
+  j.x = fp_mul(a.x, z2);
+  j.y = fp_mul(a.y, fp_mul(z2, z));
+  j.z = z;
+  wr_fp12(miller_loop(g1_eval_from_jac(j), rd_g2(g2)), out);
+}
+void hs_pairing(const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
+  wr_fp12(final_exponentiation(miller_loop(g1_eval_from_aff(rd_g1(g1)), rd_g2(g2))), out);
+}
+
+void hs_hash_to_g2(const uint8_t* msg32, uint8_t* out192) {
+  uint32_t w[8];
+  msg_words_from_bytes(msg32, w);
+  g2_serialize192(hash_to_g2(w), out192);
+}
+void hs_map_to_curve_sswu(const uint8_t* u96, uint8_t* out192) {
+  G2A r = map_to_curve_sswu(rd_fp2(u96));
+  wr_fp2(r.x, out192);
+  wr_fp2(r.y, out192 + 96);
+}
+void hs_hash_to_field(const uint8_t* msg32, uint8_t* out384) {
+  uint32_t w[8];
+  msg_words_from_bytes(msg32, w);
+  Fp2 u0, u1;
+  hash_to_field_fp2_x2(w, u0, u1);
+  wr_fp2(u0, out384);
+  wr_fp2(u1, out384 + 96);
+}
+void hs_expand_message_xmd(const uint8_t* msg32, uint8_t* out256) {
+  uint32_t w[8], o[64];
+  msg_words_from_bytes(msg32, w);
+  expand_message_xmd_32(w, o);
+  for (int i = 0; i < 64; ++i) {
+    out256[4 * i] = (uint8_t)(o[i] >> 24);
+    out256[4 * i + 1] = (uint8_t)(o[i] >> 16);
+    out256[4 * i + 2] = (uint8_t)(o[i] >> 8);
+    out256[4 * i + 3] = (uint8_t)o[i];
+  }
+}
+
+int hs_g2_decompress(const uint8_t* sig96, uint8_t* out192) {
+  G2A a;
+  int32_t code = g2_decompress96(sig96, a);
+  if (code == BLS_OK) g2_serialize192(a, out192);
+  return code;
+}
+int hs_g2_in_subgroup(const uint8_t* g2) { return g2_in_subgroup(rd_g2(g2)); }
+int hs_g1_decompress(const uint8_t* pk48, uint8_t* out96) {
+  G1A a;
+  int32_t code = g1_decompress48(pk48, a);
+  if (code == BLS_OK) g1_serialize96(a, out96);
+  return code;
+}
+void hs_g2_compress(const uint8_t* g2, uint8_t* out96) { g2_compress96(rd_g2(g2), out96); }
+void hs_g1_compress(const uint8_t* g1, uint8_t* out48) { g1_compress48(rd_g1(g1), out48); }
+void hs_g2_clear_cofactor(const uint8_t* g2, uint8_t* out192) {
+  g2_serialize192(jac_to_aff(g2_clear_cofactor(jac_from_aff(rd_g2(g2)))), out192);
+}
+void hs_g1_mul_u64(const uint8_t* g1, uint64_t k, uint8_t* out96) {
+  g1_serialize96(jac_to_aff(aff_mul_u64(rd_g1(g1), k)), out96);
+}
+void hs_g2_mul_u64(const uint8_t* g2, uint64_t k, uint8_t* out192) {
+  g2_serialize192(jac_to_aff(aff_mul_u64(rd_g2(g2), k)), out192);
+}
+void hs_g1_add(const uint8_t* a, const uint8_t* b, uint8_t* out96) {
+  g1_serialize96(jac_to_aff(jac_add(jac_from_aff(rd_g1(a)), jac_from_aff(rd_g1(b)))), out96);
+}
+void hs_g2_add(const uint8_t* a, const uint8_t* b, uint8_t* out192) {
+  g2_serialize192(jac_to_aff(jac_add(jac_from_aff(rd_g2(a)), jac_from_aff(rd_g2(b)))), out192);
+}
+void hs_g2_dbl(const uint8_t* a, uint8_t* out192) {
+  g2_serialize192(jac_to_aff(jac_dbl(jac_from_aff(rd_g2(a)))), out192);
+}
+
+// sk: 32 bytes big-endian
+void hs_sk_to_pk(const uint8_t* sk, uint8_t* out48) {
+  uint32_t k[8];
+  scalar_words_from_be32(sk, k);
+  g1_compress48(jac_to_aff(aff_mul_u256(g1_generator(), k)), out48);
+}
+void hs_sign(const uint8_t* sk, const uint8_t* msg32, uint8_t* out96) {
+  uint32_t k[8], w[8];
+  scalar_words_from_be32(sk, k);
+  msg_words_from_bytes(msg32, w);
+  g2_compress96(jac_to_aff(aff_mul_u256(hash_to_g2(w), k)), out96);
+}
+
+}  // extern "C"
+
+#include <vector>
+
+static std::vector<G1A> g_table;
+
+extern "C" {
+
+// Pubkey table for the host pipeline (mirrors bls_gpu_load_pubkeys)
+long long hs_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes) {
+  for (uint32_t i = 0; i < n; ++i) {
+    G1A a;
+    int32_t c = pk_len == 48 ? g1_decompress48(pks + 48ull * i, a) : g1_deserialize96(pks + 96ull * i, a);
+    if (codes) codes[i] = c;
+    if (c != BLS_OK) {
+      a.inf = true;
+      a.x = fp_zero();
+      a.y = fp_zero();
+    }
+    g_table.push_back(a);
+  }
+  return (long long)g_table.size();
+}
+void hs_clear_pubkeys(void) { g_table.clear(); }
+
+// Full verify pipeline on the CPU: the GPU kernels' stage bodies (pipeline.hpp) looped
+// over "lanes", planned and assembled by the same host code as bls_gpu_verify.
+int hs_verify_batch(const bls_batch* in, int32_t* verdicts, bls_stats* stats) {
+  BatchPlan plan;
+  plan_batch(in, plan);
+  uint32_t n = in->n_sets, R = in->n_reqs;
+  std::vector<G2A> sig(n), H(n);
+  std::vector<G1J> pk(n), rpk(n);
+  std::vector<G2J> rsig(n);
+  std::vector<Fp12> f(n);
+  std::vector<int32_t> sig_status(n), pk_status(n), req_status(R);
+  uint32_t n_chunks = (uint32_t)plan.chunk_off.size() - 1;
+  std::vector<int32_t> chunk_ok(n_chunks + 1);
+  uint32_t seed[8];
+  if (in->seed) {
+    scalar_words_from_be32(in->seed, seed);
+  } else {
+    for (int k = 0; k < 8; ++k) seed[k] = 0x9e3779b9u * (k + 1);
+  }
+  PipeBufs b;
+  memset(&b, 0, sizeof(b));
+  b.n_sets = n;
+  b.n_reqs = R;
+  b.n_chunks = n_chunks;
+  b.req_off = in->req_set_offsets;
+  b.pubkeys = in->pubkeys;
+  b.set_pk_off = in->set_pk_offsets;
+  b.pk_idx = in->pk_indices;
+  b.pk_table = g_table.data();
+  b.pk_table_n = (uint32_t)g_table.size();
+  b.msgs = in->messages;
+  b.sigs = in->signatures;
+  b.sig_lens = in->signature_lens;
+  b.seed = seed;
+  b.chunk_off = plan.chunk_off.data();
+  b.chunk_reqs = plan.chunk_reqs.data();
+  b.sig = sig.data();
+  b.sig_status = sig_status.data();
+  b.pk = pk.data();
+  b.pk_status = pk_status.data();
+  b.H = H.data();
+  b.rpk = rpk.data();
+  b.rsig = rsig.data();
+  b.f = f.data();
+  b.req_status = req_status.data();
+  b.chunk_ok = chunk_ok.data();
+  for (uint32_t i = 0; i < n; ++i) stage_pk(b, i);
+  for (uint32_t i = 0; i < n; ++i) stage_sig(b, i);
+  for (uint32_t i = 0; i < n; ++i) stage_h2c(b, i);
+  for (uint32_t i = 0; i < n; ++i) stage_scale(b, i);
+  for (uint32_t i = 0; i < n; ++i) stage_miller_set(b, i);
+  for (uint32_t r = 0; r < R; ++r) stage_req_status(b, r);
+  for (uint32_t c = 0; c < n_chunks; ++c) stage_chunk(b, c);
+  std::vector<uint32_t> indiv = plan.nonbatch_reqs;
+  for (uint32_t c = 0; c < n_chunks; ++c)
+    if (chunk_ok[c] != 1)
+      for (uint32_t k = plan.chunk_off[c]; k < plan.chunk_off[c + 1]; ++k) indiv.push_back(plan.chunk_reqs[k]);
+  std::vector<int32_t> indiv_verdict(indiv.size() + 1);
+  b.indiv_reqs = indiv.data();
+  b.n_indiv = (uint32_t)indiv.size();
+  b.indiv_verdict = indiv_verdict.data();
+  for (uint32_t t = 0; t < b.n_indiv; ++t) stage_indiv(b, t);
+  assemble_verdicts(in, plan, chunk_ok.data(), indiv, indiv_verdict.data(), verdicts, stats);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+"""GPU parity tests: every entry point of the C-ABI on cuda:0 against the golden
+fixtures (tests/golden/golden.json, produced by the CPU oracle and pinned by the
+reference's own known-answer data) and the reference's verdict semantics.
+
+Bar: bit-exact for every byte output (hash_to_G2, aggregate pubkeys, pk, signatures);
+exact verdict / error-code equality for verification.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from lodestar_amd._abi import (
+    CODE_BAD_ENCODING,
+    CODE_EMPTY_AGGREGATE,
+    CODE_EMPTY_SET,
+    CODE_INVALID_SIZE,
+    CODE_PK_IS_INFINITY,
+    CODE_ZERO_SIGNATURE,
+)
+from lodestar_amd.native import pack_requests
+
+pytestmark = pytest.mark.gpu
+
+
+def _h(b: bytes) -> bytes:
+    return hashlib.sha256(b).digest()
+
+
+def test_hash_to_g2_bit_exact(gpu, golden):
+    vecs = golden["hash_to_g2"]
+    msgs = b"".join(bytes.fromhex(v["msg"]) for v in vecs)
+    out = gpu.hash_to_g2(msgs)
+    for row, v in zip(out, vecs):
+        assert row.tobytes().hex() == v["point"]
+
+
+def test_sk_to_pk_interop_kat(gpu, golden, oracle):
+    sks = b"".join(oracle.interop_secret_key(i).to_bytes(32, "big") for i in range(100))
+    pks = gpu.sk_to_pk(sks)
+    assert [p.tobytes().hex() for p in pks] == golden["kat2_interop_pubkeys"]
+    assert pks[0].tobytes().hex() == golden["kat1"]["pubkey"]
+
+
+def test_sign_kat_and_golden(gpu, golden):
+    k = golden["kat1"]
+    sig = gpu.sign(bytes.fromhex(k["sk"]), bytes.fromhex(k["signing_root"]))
+    assert sig[0].tobytes().hex() == k["signature"]
+    sv = golden["signatures"]
+    sks = b"".join(bytes.fromhex(s["sk"]) for s in sv)
+    msgs = b"".join(bytes.fromhex(s["msg"]) for s in sv)
+    out = gpu.sign(sks, msgs)
+    assert [o.tobytes().hex() for o in out] == [s["sig"] for s in sv]
+
+
+@pytest.fixture(scope="module")
+def table(gpu, golden):
+    """Device pubkey table: the 100 interop keys (KAT-2), compressed, loaded once."""
+    pks = b"".join(bytes.fromhex(h) for h in golden["kat2_interop_pubkeys"])
+    base = gpu.load_pubkeys(b"", 48)  # current size probe
+    codes = gpu.load_pubkeys(pks, 48)
+    assert (codes == 0).all()
+    return 0 if base.size == 0 else None
+
+
+def test_aggregate_pubkeys_bit_exact(gpu, golden, table):
+    agg = golden["aggregate"]
+    out, codes = gpu.aggregate_pubkeys(agg["lists"])
+    assert list(codes) == [0] * len(agg["lists"])
+    assert [o.hex() for o in out] == agg["expected"]
+    _, codes = gpu.aggregate_pubkeys([[]])
+    assert codes[0] == CODE_EMPTY_AGGREGATE
+
+
+# ---------------------------------------------------------------------------
+# verification semantics (worker.ts:32-108, maybeBatch.ts:16-39, multithread.test.ts)
+# ---------------------------------------------------------------------------
+def _keys(oracle, n):
+    return [oracle.interop_secret_key(i).to_bytes(32, "big") for i in range(n)]
+
+
+def _sets(gpu, oracle, n, tag=b"m"):
+    sks = _keys(oracle, n)
+    msgs = [_h(tag + b"%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks), b"".join(msgs))
+    return [([i], msgs[i], sigs[i].tobytes()) for i in range(n)]
+
+
+def test_verify_valid_single_and_batched(gpu, oracle, table):
+    sets = _sets(gpu, oracle, 3)
+    # 1 request of 3 sets (non-batchable), 8 copies batchable (multithread.test.ts:52-87)
+    reqs = [(False, sets)] + [(True, sets)] * 8 + [(False, sets[:1])]
+    v, st = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [1] * 10
+    assert st.batch_retries == 0 and st.batch_sigs_success == 24
+
+
+def test_verify_invalid_size_isolated(gpu, oracle, table):
+    # multithread.test.ts:89-106: a 32-byte signature rejects with BLST_INVALID_SIZE,
+    # 8 concurrent valid requests still resolve true
+    sets = _sets(gpu, oracle, 3)
+    bad = [(sets[0][0], sets[0][1], bytes(32))]
+    reqs = [(True, bad)] + [(True, sets)] * 8
+    v, st = gpu.verify_packed(pack_requests(reqs))
+    assert v[0] == -CODE_INVALID_SIZE
+    assert list(v[1:]) == [1] * 8
+    assert st.batch_retries == 0 or st.batch_retries == st.n_chunks
+
+
+def test_verify_wrong_message_and_key(gpu, oracle, table):
+    sets = _sets(gpu, oracle, 4)
+    wrong_msg = [(sets[0][0], _h(b"other"), sets[0][2])]
+    wrong_key = [([1], sets[0][1], sets[0][2])]
+    reqs = [(False, wrong_msg), (False, wrong_key), (False, sets), (False, sets[:3] + wrong_msg)]
+    v, _ = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [0, 0, 1, 0]
+    # the same requests batchable: the batch fails and the fallback isolates them
+    v2, st = gpu.verify_packed(pack_requests([(True, r[1]) for r in reqs]))
+    assert list(v2) == [0, 0, 1, 0]
+    assert st.batch_retries >= 1
+
+
+def test_verify_decode_error_codes(gpu, oracle, golden, table):
+    sets = _sets(gpu, oracle, 2)
+    reqs, expect = [], []
+    for case in golden["sig_decode"]:
+        raw = bytes.fromhex(case["bytes"])
+        reqs.append((False, [(sets[0][0], sets[0][1], raw)]))
+        if case["code"] != 0:
+            expect.append(-case["code"])
+        elif case["name"] == "infinity":
+            expect.append(-CODE_ZERO_SIGNATURE)  # 1-set path rejects the infinity signature
+        else:
+            expect.append(0)  # a valid G2 point, but not the signature of this message
+    v, _ = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == expect
+
+
+def test_verify_edge_cases(gpu, oracle, table):
+    sets = _sets(gpu, oracle, 3)
+    inf_sig = bytes([0xC0]) + bytes(95)
+    reqs = [
+        (False, []),                                       # empty -> "Empty signature set"
+        (False, [sets[0], (sets[1][0], sets[1][1], inf_sig)]),  # n >= 2 with an infinity sig -> false
+        (False, [([], sets[0][1], sets[0][2])]),           # empty aggregate
+        (False, [([0, 1], sets[0][1], sets[0][2])]),       # aggregate of 2 keys, sig of key 0 -> false
+        (True, sets),
+    ]
+    v, _ = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [-CODE_EMPTY_SET, 0, -CODE_EMPTY_AGGREGATE, 0, 1]
+
+
+def test_verify_aggregate_sets(gpu, oracle, table):
+    # fast-aggregate style sets: the same message signed by k keys, aggregated G2 signature
+    k = 5
+    msg = _h(b"committee")
+    sks = _keys(oracle, k)
+    sigs = gpu.sign(b"".join(sks), msg * k)
+    pts = [oracle.signature_from_bytes(s.tobytes()) for s in sigs]
+    agg = None
+    for p_ in pts:
+        agg = oracle.E2.add(agg, p_)
+    agg_sig = oracle.g2_compress(agg)
+    reqs = [(False, [(list(range(k)), msg, agg_sig)]), (False, [(list(range(k - 1)), msg, agg_sig)])]
+    v, _ = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [1, 0]
+
+
+def test_verify_raw_pubkeys(gpu, oracle, golden):
+    # raw 96-byte uncompressed keys (what index.ts:160 sends the worker)
+    sks = _keys(oracle, 3)
+    msgs = [_h(b"raw%d" % i) for i in range(3)]
+    sigs = gpu.sign(b"".join(sks), b"".join(msgs))
+    raw = [oracle.g1_serialize(oracle.sk_to_pk(int.from_bytes(s, "big"))) for s in sks]
+    sets = [(raw[i], msgs[i], sigs[i].tobytes()) for i in range(3)]
+    bad_pk = bytes([0x80]) + raw[0][1:]
+    reqs = [(False, sets), (True, sets[:1]), (True, sets[1:]), (False, [(bad_pk, msgs[0], sigs[0].tobytes())])]
+    v, _ = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [1, 1, 1, -CODE_BAD_ENCODING]
+
+
+def test_verify_batch_with_injected_invalid(gpu, oracle, table):
+    """64 single-set batchable requests, 3 invalid: chunks of 16 requests; the chunks
+    holding an invalid set fail and are re-verified per request."""
+    n = 64
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"batch%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    bad = {5, 17, 40}
+    reqs = []
+    for i in range(n):
+        m = msgs[i] if i not in bad else _h(b"tampered%d" % i)
+        reqs.append((True, [([i % 16], m, sigs[i].tobytes())]))
+    v, st = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [0 if i in bad else 1 for i in range(n)]
+    assert st.n_chunks == 4 and st.batch_retries == 3
+    assert st.batch_sigs_success == 16
+
+
+def test_verify_pk_infinity(gpu, oracle):
+    inf_pk = bytes([0x40]) + bytes(95)
+    sets = [(inf_pk, _h(b"x"), bytes.fromhex("c0" + "00" * 95))]
+    v, _ = gpu.verify_packed(pack_requests([(False, sets)]))
+    assert v[0] == -CODE_ZERO_SIGNATURE
+    sk = _keys(oracle, 1)[0]
+    sig = gpu.sign(sk, _h(b"x"))[0].tobytes()
+    v, _ = gpu.verify_packed(pack_requests([(False, [(inf_pk, _h(b"x"), sig)])]))
+    assert v[0] == -CODE_PK_IS_INFINITY
