@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X BLS signature-set verifier (BASELINE.json metric:
+"BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch").
+
+Workload per step (BASELINE.json configs[1], cfg2): one verifyManySignatureSets call of
+1024 gossip-attestation sets, each its own batchable single-pubkey request (as
+multithread/index.ts:260-275 buffers them), pubkeys resident in the device table
+(index2pubkey, pubkeyCache.ts:56-77), random-scalar batch verification in chunks of
+16 requests (worker.ts:17,56) -- every stage (decompress + subgroup check,
+hash_to_G2, scalar muls, Miller loops, final exponentiations) runs inside the timed
+step.  Inputs are synthetic: interop keys sk_i = LE(sha256(LE32(i))) mod r
+(state-transition/src/util/interop.ts:19-22), messages sha256(LE64(j) || "LODE"),
+signatures made on the GPU before timing.
+
+Multi-GPU (torchrun, one process per GPU): each rank verifies its own 1024 sets (shard
+by request, no data-path collective: scaling "weak"); value = all ranks' sets / max
+over ranks of the timed region.
+
+Also reported: p50 latency of one non-batchable 128-set call (cfg1 shape), the
+roofline of the dominant kernel against the measured v_mad_u64_u32 peak, and the CPU
+baseline (the oracle, rank 0, N = 1 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+STAGE_NAMES = ["h2d", "k_pk", "k_sig", "k_h2c", "k_scale", "k_miller", "k_status+k_chunk", "k_indiv"]
+STAGE_WORK = {"k_sig": "sig", "k_h2c": "h2c", "k_scale": "scale", "k_miller": "miller"}
+
+
+def interop_sk(i: int) -> bytes:
+    v = int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R_ORDER
+    return v.to_bytes(32, "big")
+
+
+def make_workload(gpu, n_sets: int, rank: int):
+    from lodestar_amd.native import pack_requests
+
+    n_keys = n_sets
+    sks = b"".join(interop_sk(i) for i in range(n_keys))
+    pks = gpu.sk_to_pk(sks)
+    codes = gpu.load_pubkeys(pks.tobytes(), 48)
+    assert (codes == 0).all()
+    msgs = [hashlib.sha256((rank * n_sets + j).to_bytes(8, "little") + b"LODE").digest() for j in range(n_sets)]
+    sigs = gpu.sign(b"".join(interop_sk(j % n_keys) for j in range(n_sets)), b"".join(msgs))
+    sets = [([j % n_keys], msgs[j], sigs[j].tobytes()) for j in range(n_sets)]
+    batch = pack_requests([(True, [s]) for s in sets])
+    call128 = pack_requests([(False, sets[:128])])
+    return batch, call128, sets
+
+
+def cpu_baseline(sample_sets: int = 24) -> dict:
+    """Oracle (pure-Python restatement, oracle/bls_oracle.py) timed on one host core
+    over a bounded sample: verifySignatureSetsMaybeBatch on `sample_sets` sets."""
+    from oracle import bls_oracle as O
+
+    sks = [int.from_bytes(interop_sk(i), "big") for i in range(sample_sets)]
+    msgs = [hashlib.sha256(j.to_bytes(8, "little") + b"LODE").digest() for j in range(sample_sets)]
+    sigs = [O.g2_compress(O.sign(s, m)) for s, m in zip(sks, msgs)]
+    pks = [O.sk_to_pk(s) for s in sks]
+    t0 = time.perf_counter()
+    ok = O.verify_signature_sets_maybe_batch(list(zip(pks, msgs, sigs)))
+    dt = time.perf_counter() - t0
+    assert ok
+    return {"value": round(sample_sets / dt, 3), "unit": "sets/s", "cores": 1, "kind": "port",
+            "sample": f"{sample_sets} single-pubkey sets in one random-scalar batch "
+                      f"(verifySignatureSetsMaybeBatch), {dt:.1f} s, pure-Python oracle"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sets", type=int, default=1024)
+    ap.add_argument("--latency-runs", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    from lodestar_amd.native import GpuContext
+
+    gpu = GpuContext(local_rank)
+    batch, call128, _ = make_workload(gpu, args.sets, rank)
+
+    for _ in range(args.warmup):
+        v, _ = gpu.verify_packed(batch)
+        assert (v == 1).all(), "warm-up verification failed"
+
+    stage_sum = np.zeros(8)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        v, st = gpu.verify_packed(batch)
+        if not (v == 1).all():
+            raise SystemExit("verification failed inside the timed region")
+        stage_sum += np.array(st.stage_ms[:])
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # p50 latency of one 128-set non-batchable call (cfg1 shape)
+    lat = []
+    for _ in range(args.latency_runs):
+        t1 = time.perf_counter()
+        v, _ = gpu.verify_packed(call128)
+        lat.append((time.perf_counter() - t1) * 1e3)
+        assert v[0] == 1
+
+    # roofline of the dominant kernel (VALU integer multiply-add bound)
+    wm = json.loads((ROOT / "lodestar_amd" / "work_model.json").read_text())
+    stage_ms = stage_sum / args.steps
+    dom = max(STAGE_WORK, key=lambda k: stage_ms[STAGE_NAMES.index(k)])
+    dom_ms = stage_ms[STAGE_NAMES.index(dom)]
+    mads = wm["fpm_per_set"][STAGE_WORK[dom]] * wm["mads_per_fpm"] * args.sets
+    achieved = mads / (dom_ms * 1e-3) / 1e12
+    peak_rate, _ = gpu.mad_peak()
+    peak = peak_rate / 1e12
+
+    total_sets = args.sets * args.steps * world
+    value = total_sets / elapsed
+    if rank == 0:
+        out = {
+            "metric": "BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch",
+            "value": round(value, 2),
+            "unit": "sets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (381-bit Fp, 12x32-bit Montgomery limbs)",
+            "data": "synthetic: interop keys, sha256 messages, GPU-made signatures",
+            "config": {"workload": "cfg2: 1024 single-pubkey gossip sets per GPU, batchable requests, "
+                                   "random-scalar batch in chunks of 16 requests",
+                       "sets_per_step_per_gpu": args.sets, "parallelism": f"shard-by-request x{world}"},
+            "p50_latency_ms_128": round(statistics.median(lat), 3),
+            "stage_ms": {k: round(float(x), 3) for k, x in zip(STAGE_NAMES, stage_ms)},
+            "roofline": {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
+                         "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5), "traffic": None,
+                         "work": f"{wm['fpm_per_set'][STAGE_WORK[dom]]:.0f} Fp products/set x "
+                                 f"{wm['mads_per_fpm']} MAD x {args.sets} sets per launch"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    gpu.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

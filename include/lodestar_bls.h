@@ -65,6 +65,7 @@ typedef struct bls_stats {
   uint32_t n_chunks;           /* batchable chunks (chunkifyMaximizeChunkSize(reqs, 16)) */
   uint32_t n_individual;       /* requests verified on their own */
   double device_ms;            /* device time of the call (HIP events) */
+  double stage_ms[8];          /* per stage: h2d, pk, sig, h2c, scale, miller, status+chunk, individual */
 } bls_stats;
 
 typedef struct bls_gpu_ctx bls_gpu_ctx;
@@ -112,6 +113,10 @@ int bls_gpu_hash_to_g2(bls_gpu_ctx* ctx, const uint8_t* msgs, uint32_t n, uint8_
  * sks: n * 32 bytes big-endian scalars. */
 int bls_gpu_sk_to_pk(bls_gpu_ctx* ctx, const uint8_t* sks, uint32_t n, uint8_t* out48);
 int bls_gpu_sign(bls_gpu_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96);
+
+/* Roofline probe: measured rate of v_mad_u64_u32 (32x32+64 multiply-add, the unit of
+ * every Fp Montgomery product) on this device, with every CU at 8 waves/SIMD. */
+int bls_gpu_mad_peak(bls_gpu_ctx* ctx, double* mads_per_s, double* ms);
 
 #ifdef __cplusplus
 }

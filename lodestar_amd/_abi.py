@@ -46,6 +46,7 @@ SYMBOLS = (
     "bls_gpu_hash_to_g2",
     "bls_gpu_sk_to_pk",
     "bls_gpu_sign",
+    "bls_gpu_mad_peak",
 )
 
 
@@ -72,6 +73,7 @@ class BlsStats(ctypes.Structure):
         ("n_chunks", ctypes.c_uint32),
         ("n_individual", ctypes.c_uint32),
         ("device_ms", ctypes.c_double),
+        ("stage_ms", ctypes.c_double * 8),
     ]
 
 
@@ -98,6 +100,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_sk_to_pk.restype = i32
         lib.bls_gpu_sign.argtypes = [vp, vp, vp, u32, vp]
         lib.bls_gpu_sign.restype = i32
+        lib.bls_gpu_mad_peak.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        lib.bls_gpu_mad_peak.restype = i32
     return lib
 
 

@@ -31,6 +31,7 @@ struct bls_gpu_ctx {
   int device;
   hipStream_t stream;
   hipEvent_t ev0, ev1;
+  hipEvent_t ev[9];  // stage boundaries of the last verify call
   char err[512];
   // device pubkey table (affine, Montgomery)
   G1A* table;
@@ -127,6 +128,12 @@ int bls_gpu_init(int device, bls_gpu_ctx** out) {
     delete ctx;
     return -1;
   }
+  for (int i = 0; i < 9; ++i) {
+    if (hipEventCreate(&ctx->ev[i]) != hipSuccess) {
+      delete ctx;
+      return -1;
+    }
+  }
   *out = ctx;
   return 0;
 }
@@ -140,6 +147,7 @@ void bls_gpu_close(bls_gpu_ctx* ctx) {
   if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
+  for (int i = 0; i < 9; ++i) (void)hipEventDestroy(ctx->ev[i]);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -280,15 +288,24 @@ int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls
   hipStream_t s = ctx->stream;
   HIPC(ctx, hipEventRecord(ctx->ev0, s));
   HIPC(ctx, hipMemcpyAsync(ctx->dev_ws, ctx->host_stage, input_end, hipMemcpyHostToDevice, s));
+  HIPC(ctx, hipEventRecord(ctx->ev[0], s));
   if (n > 0) {
     HIPC(ctx, launch_k_pk(b, s));
+    HIPC(ctx, hipEventRecord(ctx->ev[1], s));
     HIPC(ctx, launch_k_sig(b, s));
+    HIPC(ctx, hipEventRecord(ctx->ev[2], s));
     HIPC(ctx, launch_k_h2c(b, s));
+    HIPC(ctx, hipEventRecord(ctx->ev[3], s));
     HIPC(ctx, launch_k_scale(b, s));
+    HIPC(ctx, hipEventRecord(ctx->ev[4], s));
     HIPC(ctx, launch_k_miller(b, s));
+    HIPC(ctx, hipEventRecord(ctx->ev[5], s));
+  } else {
+    for (int i = 1; i <= 5; ++i) HIPC(ctx, hipEventRecord(ctx->ev[i], s));
   }
   HIPC(ctx, launch_k_status(b, s));
   if (n_chunks > 0) HIPC(ctx, launch_k_chunk(b, s));
+  HIPC(ctx, hipEventRecord(ctx->ev[6], s));
 
   std::vector<int32_t> chunk_ok(n_chunks + 1, 0);
   if (n_chunks > 0)
@@ -304,7 +321,9 @@ int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls
     b.n_indiv = (uint32_t)indiv.size();
     HIPC(ctx, hipMemcpyAsync((void*)b.indiv_reqs, indiv.data(), sizeof(uint32_t) * indiv.size(),
                              hipMemcpyHostToDevice, s));
+    HIPC(ctx, hipEventRecord(ctx->ev[7], s));
     HIPC(ctx, launch_k_indiv(b, s));
+    HIPC(ctx, hipEventRecord(ctx->ev[8], s));
     HIPC(ctx, hipMemcpyAsync(indiv_verdict.data(), b.indiv_verdict, sizeof(int32_t) * indiv.size(),
                              hipMemcpyDeviceToHost, s));
   }
@@ -315,6 +334,18 @@ int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     stats->device_ms = ms;
+    // stage_ms: h2d, pk, sig, h2c, scale, miller, status+chunk, indiv
+    (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev[0]);
+    stats->stage_ms[0] = ms;
+    for (int i = 1; i <= 6; ++i) {
+      (void)hipEventElapsedTime(&ms, ctx->ev[i - 1], ctx->ev[i]);
+      stats->stage_ms[i] = ms;
+    }
+    stats->stage_ms[7] = 0.0;
+    if (!indiv.empty()) {
+      (void)hipEventElapsedTime(&ms, ctx->ev[7], ctx->ev[8]);
+      stats->stage_ms[7] = ms;
+    }
   }
   return 0;
 }
@@ -391,3 +422,24 @@ int bls_gpu_sign(bls_gpu_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, uint
 }
 
 }  // extern "C"
+
+extern "C" int bls_gpu_mad_peak(bls_gpu_ctx* ctx, double* mads_per_s, double* ms_out) {
+  HIPC(ctx, hipSetDevice(ctx->device));
+  int cus = 0;
+  HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  const uint32_t blocks = (uint32_t)cus * 8, iters = 1024;
+  if (ensure_dev(ctx, sizeof(uint64_t) * blocks)) return -1;
+  uint64_t* d = (uint64_t*)ctx->dev_ws;
+  hipStream_t s = ctx->stream;
+  HIPC(ctx, launch_k_mad_peak(d, blocks, iters, s));  // warm-up (clocks, code load)
+  HIPC(ctx, hipEventRecord(ctx->ev0, s));
+  HIPC(ctx, launch_k_mad_peak(d, blocks, iters, s));
+  HIPC(ctx, hipEventRecord(ctx->ev1, s));
+  HIPC(ctx, hipStreamSynchronize(s));
+  float ms = 0.f;
+  HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  double mads = (double)blocks * 256.0 * iters * 16.0 * 8.0;
+  *mads_per_s = mads / (ms * 1e-3);
+  if (ms_out) *ms_out = ms;
+  return 0;
+}

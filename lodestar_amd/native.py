@@ -195,6 +195,12 @@ class GpuContext:
         self._check(self.lib.bls_gpu_sk_to_pk(self._h, _ptr(s), n, _ptr(out)), "bls_gpu_sk_to_pk")
         return out[: 48 * n].reshape(n, 48)
 
+    def mad_peak(self) -> tuple[float, float]:
+        """Measured v_mad_u64_u32 rate (MAD/s) and the probe's duration (ms)."""
+        rate, ms = ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.bls_gpu_mad_peak(self._h, ctypes.byref(rate), ctypes.byref(ms)), "bls_gpu_mad_peak")
+        return rate.value, ms.value
+
     def sign(self, sks: bytes | np.ndarray, msgs: bytes | np.ndarray) -> np.ndarray:
         s, m = _u8(sks), _u8(msgs)
         n = s.size // 32

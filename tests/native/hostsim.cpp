@@ -207,8 +207,13 @@ void hs_sign(const uint8_t* sk, const uint8_t* msg32, uint8_t* out96) {
 #include <vector>
 
 static std::vector<G1A> g_table;
+// Fp multiplications per stage of the last hs_verify_batch:
+// pk, sig, h2c, scale, miller, status+chunk, individual
+static unsigned long long g_stage_fpm[7];
 
 extern "C" {
+
+unsigned long long hs_stage_fpm(int k) { return (k >= 0 && k < 7) ? g_stage_fpm[k] : 0ull; }
 
 // Pubkey table for the host pipeline (mirrors bls_gpu_load_pubkeys)
 long long hs_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes) {
@@ -273,13 +278,24 @@ int hs_verify_batch(const bls_batch* in, int32_t* verdicts, bls_stats* stats) {
   b.f = f.data();
   b.req_status = req_status.data();
   b.chunk_ok = chunk_ok.data();
+  unsigned long long c0 = bls_fpm_counter;
+  auto mark = [&](int k) {
+    g_stage_fpm[k] = bls_fpm_counter - c0;
+    c0 = bls_fpm_counter;
+  };
   for (uint32_t i = 0; i < n; ++i) stage_pk(b, i);
+  mark(0);
   for (uint32_t i = 0; i < n; ++i) stage_sig(b, i);
+  mark(1);
   for (uint32_t i = 0; i < n; ++i) stage_h2c(b, i);
+  mark(2);
   for (uint32_t i = 0; i < n; ++i) stage_scale(b, i);
+  mark(3);
   for (uint32_t i = 0; i < n; ++i) stage_miller_set(b, i);
+  mark(4);
   for (uint32_t r = 0; r < R; ++r) stage_req_status(b, r);
   for (uint32_t c = 0; c < n_chunks; ++c) stage_chunk(b, c);
+  mark(5);
   std::vector<uint32_t> indiv = plan.nonbatch_reqs;
   for (uint32_t c = 0; c < n_chunks; ++c)
     if (chunk_ok[c] != 1)
@@ -289,6 +305,7 @@ int hs_verify_batch(const bls_batch* in, int32_t* verdicts, bls_stats* stats) {
   b.n_indiv = (uint32_t)indiv.size();
   b.indiv_verdict = indiv_verdict.data();
   for (uint32_t t = 0; t < b.n_indiv; ++t) stage_indiv(b, t);
+  mark(6);
   assemble_verdicts(in, plan, chunk_ok.data(), indiv, indiv_verdict.data(), verdicts, stats);
   return 0;
 }
