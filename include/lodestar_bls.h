@@ -118,6 +118,13 @@ int bls_gpu_sign(bls_gpu_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, uint
  * every Fp Montgomery product) on this device, with every CU at 8 waves/SIMD. */
 int bls_gpu_mad_peak(bls_gpu_ctx* ctx, double* mads_per_s, double* ms);
 
+/* Field self-test: out = a * b mod p for n pairs of canonical 48-byte big-endian
+ * elements (exercises to/from Montgomery and the device Montgomery product). */
+int bls_gpu_fp_mul_test(bls_gpu_ctx* ctx, const uint8_t* a48, const uint8_t* b48, uint32_t n, uint8_t* out48);
+
+/* Probe: `lanes` lanes each run `iters` dependent Montgomery products. */
+int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iters, double* ns_per_fpm, double* fpm_per_s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,6 +47,8 @@ SYMBOLS = (
     "bls_gpu_sk_to_pk",
     "bls_gpu_sign",
     "bls_gpu_mad_peak",
+    "bls_gpu_fp_mul_test",
+    "bls_gpu_fpm_bench",
 )
 
 
@@ -102,6 +104,11 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_sign.restype = i32
         lib.bls_gpu_mad_peak.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         lib.bls_gpu_mad_peak.restype = i32
+        lib.bls_gpu_fp_mul_test.argtypes = [vp, vp, vp, u32, vp]
+        lib.bls_gpu_fp_mul_test.restype = i32
+        dp = ctypes.POINTER(ctypes.c_double)
+        lib.bls_gpu_fpm_bench.argtypes = [vp, u32, u32, dp, dp]
+        lib.bls_gpu_fpm_bench.restype = i32
     return lib
 
 

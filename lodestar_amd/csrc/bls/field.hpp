@@ -174,8 +174,72 @@ BLS_HD Fp fp_half(const Fp& a) {
   return r;
 }
 
-// Montgomery product a*b/R mod p, CIOS with the no-carry optimisation
-// (valid because p's top limb 0x1a0111ea < 2^31 - 1).  Inputs < p, output < p.
+#if defined(__HIP_DEVICE_COMPILE__)
+// gfx950: product-scanning (FIPS) Montgomery product.  Each 32x32 product is one
+// v_mad_u64_u32 into a 64-bit column accumulator whose carry-out (VOP3B sdst) feeds
+// a v_addc_co_u32 into the third accumulator word: 2 instructions per product,
+// 288 products.  a*b and m*p products go to two accumulators (two dependency
+// chains per column), merged once per column.
+__device__ __forceinline__ void bls_mac(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
+      "v_addc_co_u32 %1, %2, 0, %1, %2"
+      : "+v"(lo), "+v"(hi), "=&s"(cc)
+      : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void bls_mac_s(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
+      "v_addc_co_u32 %1, %2, 0, %1, %2"
+      : "+v"(lo), "+v"(hi), "=&s"(cc)
+      : "v"(a), "s"(b));
+}
+
+BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
+  uint32_t m[12];
+  Fp u;
+  uint64_t lo = 0, lo2 = 0;
+  uint32_t hi = 0, hi2 = 0;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+#pragma unroll
+    for (int i = 0; i < k; ++i) {
+      bls_mac(lo, hi, a.l[i], b.l[k - i]);
+      bls_mac_s(lo2, hi2, m[i], p_limb(k - i));
+    }
+    bls_mac(lo, hi, a.l[k], b.l[0]);
+    uint64_t s = lo + lo2;
+    hi = hi + hi2 + (s < lo ? 1u : 0u);
+    lo = s;
+    lo2 = 0;
+    hi2 = 0;
+    m[k] = (uint32_t)lo * BLS_NP0;
+    bls_mac_s(lo, hi, m[k], p_limb(0));
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int k = 12; k < 23; ++k) {
+#pragma unroll
+    for (int i = k - 11; i < 12; ++i) {
+      bls_mac(lo, hi, a.l[i], b.l[k - i]);
+      bls_mac_s(lo2, hi2, m[i], p_limb(k - i));
+    }
+    uint64_t s = lo + lo2;
+    hi = hi + hi2 + (s < lo ? 1u : 0u);
+    lo = s;
+    lo2 = 0;
+    hi2 = 0;
+    u.l[k - 12] = (uint32_t)lo;
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  u.l[11] = (uint32_t)lo;
+  return fp_reduce_once(u);
+}
+#else
+// Host build (test harness): Montgomery product a*b/R mod p, CIOS with the no-carry
+// optimisation (valid because p's top limb 0x1a0111ea < 2^31 - 1).  Inputs < p, output < p.
 BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
   BLS_COUNT_FPM();
   uint32_t t[12];
@@ -204,6 +268,7 @@ BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
   for (int j = 0; j < 12; ++j) r.l[j] = t[j];
   return fp_reduce_once(r);
 }
+#endif
 
 BLS_HD Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }
 

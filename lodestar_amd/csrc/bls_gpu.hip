@@ -443,3 +443,41 @@ extern "C" int bls_gpu_mad_peak(bls_gpu_ctx* ctx, double* mads_per_s, double* ms
   if (ms_out) *ms_out = ms;
   return 0;
 }
+
+extern "C" int bls_gpu_fp_mul_test(bls_gpu_ctx* ctx, const uint8_t* a48, const uint8_t* b48, uint32_t n,
+                                   uint8_t* out48) {
+  HIPC(ctx, hipSetDevice(ctx->device));
+  if (n == 0) return 0;
+  size_t sz = 48ull * n, al = (sz + 255) & ~(size_t)255;
+  if (ensure_dev(ctx, 3 * al)) return -1;
+  uint8_t *da = ctx->dev_ws, *db = da + al, *dout = db + al;
+  hipStream_t s = ctx->stream;
+  HIPC(ctx, hipMemcpyAsync(da, a48, sz, hipMemcpyHostToDevice, s));
+  HIPC(ctx, hipMemcpyAsync(db, b48, sz, hipMemcpyHostToDevice, s));
+  HIPC(ctx, launch_k_fp_mul_test(da, db, n, dout, s));
+  HIPC(ctx, hipMemcpyAsync(out48, dout, sz, hipMemcpyDeviceToHost, s));
+  HIPC(ctx, hipStreamSynchronize(s));
+  return 0;
+}
+
+// Dependent Montgomery-product chain: `lanes` lanes (multiple of 64) x `iters` products.
+// ns_per_fpm = wall time / iters (per-lane latency); fpm_per_s = lanes * iters / time.
+extern "C" int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iters, double* ns_per_fpm,
+                                 double* fpm_per_s) {
+  HIPC(ctx, hipSetDevice(ctx->device));
+  lanes = (lanes + 63) / 64 * 64;
+  if (ensure_dev(ctx, sizeof(Fp) * 2 * lanes)) return -1;
+  Fp* io = (Fp*)ctx->dev_ws;
+  hipStream_t s = ctx->stream;
+  HIPC(ctx, hipMemsetAsync(io, 0x11, sizeof(Fp) * 2 * lanes, s));
+  HIPC(ctx, launch_k_fpm_chain(io, lanes, 8, s));
+  HIPC(ctx, hipEventRecord(ctx->ev0, s));
+  HIPC(ctx, launch_k_fpm_chain(io, lanes, iters, s));
+  HIPC(ctx, hipEventRecord(ctx->ev1, s));
+  HIPC(ctx, hipStreamSynchronize(s));
+  float ms = 0.f;
+  HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  *ns_per_fpm = ms * 1e6 / iters;
+  *fpm_per_s = (double)lanes * iters / (ms * 1e-3);
+  return 0;
+}

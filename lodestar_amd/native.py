@@ -201,6 +201,18 @@ class GpuContext:
         self._check(self.lib.bls_gpu_mad_peak(self._h, ctypes.byref(rate), ctypes.byref(ms)), "bls_gpu_mad_peak")
         return rate.value, ms.value
 
+    def fp_mul_test(self, a: bytes, b: bytes) -> bytes:
+        n = len(a) // 48
+        out = ctypes.create_string_buffer(48 * max(n, 1))
+        self._check(self.lib.bls_gpu_fp_mul_test(self._h, a, b, n, out), "bls_gpu_fp_mul_test")
+        return out.raw[: 48 * n]
+
+    def fpm_bench(self, lanes: int, iters: int) -> tuple[float, float]:
+        ns, rate = ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.bls_gpu_fpm_bench(self._h, lanes, iters, ctypes.byref(ns), ctypes.byref(rate)),
+                    "bls_gpu_fpm_bench")
+        return ns.value, rate.value
+
     def sign(self, sks: bytes | np.ndarray, msgs: bytes | np.ndarray) -> np.ndarray:
         s, m = _u8(sks), _u8(msgs)
         n = s.size // 32

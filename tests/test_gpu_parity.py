@@ -208,3 +208,19 @@ def test_verify_pk_infinity(gpu, oracle):
     sig = gpu.sign(sk, _h(b"x"))[0].tobytes()
     v, _ = gpu.verify_packed(pack_requests([(False, [(inf_pk, _h(b"x"), sig)])]))
     assert v[0] == -CODE_PK_IS_INFINITY
+
+
+def test_fp_mul_device_vs_bigint(gpu):
+    """The device Montgomery product (inline-asm product scanning on gfx950) against
+    Python big integers: random operands plus the edges 0, 1, p-1, 2^381 region."""
+    import random
+
+    from oracle.bls_oracle import P
+
+    rng = random.Random(7)
+    vals = [0, 1, 2, P - 1, P - 2, (1 << 380), (1 << 381) % P, P // 2, P // 2 + 1]
+    a = vals + [rng.randrange(P) for _ in range(500)]
+    b = list(reversed(vals)) + [rng.randrange(P) for _ in range(500)]
+    out = gpu.fp_mul_test(b"".join(x.to_bytes(48, "big") for x in a), b"".join(x.to_bytes(48, "big") for x in b))
+    got = [int.from_bytes(out[48 * i: 48 * i + 48], "big") for i in range(len(a))]
+    assert got == [(x * y) % P for x, y in zip(a, b)]

@@ -1,0 +1,151 @@
+"""The HIP kernels' math compiled for the CPU (tests/native/hostsim.cpp) against the
+oracle and the golden fixtures -- runs without a GPU.  The device build differs only
+in fp_mul (inline-asm product scanning), which tests/test_gpu_parity.py pins."""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import random
+
+import numpy as np
+
+from tests._codec import P, b48, bf2, bf12, bg2, f2b, f12b, fp, g1b, g2b
+
+
+def _buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+def test_fp_ops(hostsim):
+    rng = random.Random(1)
+    o = _buf(48)
+    for _ in range(100):
+        a, b = rng.randrange(P), rng.randrange(P)
+        hostsim.hs_fp_mul(b48(a), b48(b), o)
+        assert fp(o.raw) == a * b % P
+        hostsim.hs_fp_sub(b48(a), b48(b), o)
+        assert fp(o.raw) == (a - b) % P
+    hostsim.hs_fp_inv(b48(12345), o)
+    assert fp(o.raw) * 12345 % P == 1
+
+
+def test_fp2_sqrt(hostsim, oracle):
+    rng = random.Random(2)
+    o = _buf(96)
+    for _ in range(20):
+        x = (rng.randrange(P), rng.randrange(P))
+        ok = hostsim.hs_fp2_sqrt(f2b(x), o)
+        assert bool(ok) == (oracle.f2_sqrt(x) is not None)
+        if ok:
+            assert oracle.f2_mul(bf2(o.raw), bf2(o.raw)) == x
+    for x in ((5, 0), (P - 5, 0), (0, 7)):  # the a1 == 0 branch and a0 == 0
+        s = oracle.f2_mul(x, x)
+        assert hostsim.hs_fp2_sqrt(f2b(s), o) == 1
+        assert oracle.f2_mul(bf2(o.raw), bf2(o.raw)) == s
+
+
+def test_fp12_tower(hostsim, oracle):
+    rng = random.Random(3)
+    a = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+    b = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+    o = _buf(576)
+    hostsim.hs_fp12_mul(f12b(a), f12b(b), o)
+    assert bf12(o.raw) == oracle.f12_mul(a, b)
+    hostsim.hs_fp12_sqr(f12b(a), o)
+    assert bf12(o.raw) == oracle.f12_mul(a, a)
+    hostsim.hs_fp12_frob(f12b(a), o)
+    assert bf12(o.raw) == oracle.f12_frob(a)
+    t = oracle.f12_mul(oracle.f12_conj(a), oracle.f12_inv(a))
+    t = oracle.f12_mul(oracle.f12_frob(oracle.f12_frob(t)), t)
+    hostsim.hs_fp12_cyclotomic_sqr(f12b(t), o)
+    assert bf12(o.raw) == oracle.f12_mul(t, t)
+
+
+def test_hash_to_g2_golden(hostsim, golden):
+    o = _buf(192)
+    for v in golden["hash_to_g2"]:
+        hostsim.hs_hash_to_g2(bytes.fromhex(v["msg"]), o)
+        assert o.raw.hex() == v["point"]
+
+
+def test_pairing_matches_oracle_cubed(hostsim, oracle):
+    Pp = oracle.E1.mul(oracle.G1, 99)
+    Qq = oracle.E2.mul(oracle.G2, 7)
+    o = _buf(576)
+    hostsim.hs_pairing(g1b(Pp), g2b(Qq), o)
+    assert bf12(o.raw) == oracle.final_exponentiation(oracle.miller_loop(Pp, Qq), hard_multiple=3)
+
+
+def test_sig_decode_cases(hostsim, golden):
+    o = _buf(192)
+    for case in golden["sig_decode"]:
+        raw = bytes.fromhex(case["bytes"])
+        code = hostsim.hs_g2_decompress(raw, o)
+        if code == 0 and not (raw[0] & 0x40):
+            code = 0 if hostsim.hs_g2_in_subgroup(o.raw) else 3
+        assert code == case["code"], case["name"]
+
+
+def test_kat_points(hostsim, golden):
+    o = _buf(192)
+    for p in golden["kat3_g2_points"]:
+        assert hostsim.hs_g2_decompress(bytes.fromhex(p["compressed"]), o) == 0
+        assert o.raw.hex() == p["uncompressed"]
+        assert hostsim.hs_g2_in_subgroup(o.raw) == 1
+    o48 = _buf(48)
+    hostsim.hs_sk_to_pk(bytes.fromhex(golden["kat1"]["sk"]), o48)
+    assert o48.raw.hex() == golden["kat1"]["pubkey"]
+    o96 = _buf(96)
+    hostsim.hs_sign(bytes.fromhex(golden["kat1"]["sk"]), bytes.fromhex(golden["kat1"]["signing_root"]), o96)
+    assert o96.raw.hex() == golden["kat1"]["signature"]
+
+
+def _hs_verify(hostsim, reqs, seed=b"\x07" * 32):
+    from lodestar_amd._abi import BlsBatch, BlsStats
+    from lodestar_amd.native import _ptr, pack_requests
+
+    pb = pack_requests(reqs, seed=seed)
+    b = BlsBatch()
+    b.n_sets, b.n_reqs = pb.n_sets, pb.n_reqs
+    keep = []
+    for f in ("req_set_offsets", "req_batchable", "messages", "signatures", "pubkeys", "set_pk_offsets",
+              "pk_indices", "signature_lens"):
+        a = getattr(pb, f)
+        keep.append(a)
+        setattr(b, f, _ptr(a))
+    s = ctypes.create_string_buffer(seed, 32)
+    b.seed = ctypes.cast(s, ctypes.c_void_p)
+    v = np.zeros(max(pb.n_reqs, 1), dtype=np.int32)
+    st = BlsStats()
+    hostsim.hs_verify_batch(ctypes.byref(b), _ptr(v), ctypes.byref(st))
+    return list(v[: pb.n_reqs]), st
+
+
+def test_pipeline_semantics(hostsim, oracle):
+    """The kernels' stage bodies, planned and assembled by the same host code as
+    bls_gpu_verify, against the reference worker semantics (worker.ts:32-108)."""
+    n = 20
+    sks = [oracle.interop_secret_key(i) for i in range(n)]
+    pks = b""
+    for sk in sks:
+        o = _buf(48)
+        hostsim.hs_sk_to_pk(sk.to_bytes(32, "big"), o)
+        pks += o.raw
+    hostsim.hs_clear_pubkeys()
+    assert hostsim.hs_load_pubkeys(pks, n, 48, None) == n
+    msgs = [hashlib.sha256(b"hs%d" % i).digest() for i in range(n)]
+    sigs = []
+    for sk, m in zip(sks, msgs):
+        o = _buf(96)
+        hostsim.hs_sign(sk.to_bytes(32, "big"), m, o)
+        sigs.append(o.raw)
+    sets = [([i], msgs[i], sigs[i]) for i in range(n)]
+    reqs = [(True, [s]) for s in sets]
+    v, st = _hs_verify(hostsim, reqs)
+    assert v == [1] * n and st.n_chunks == 1 and st.batch_retries == 0
+    bad = list(reqs)
+    bad[3] = (True, [([3], msgs[4], sigs[3])])
+    bad[7] = (True, [([7], msgs[7], bytes(32))])
+    v, st = _hs_verify(hostsim, bad + [(False, sets[:4]), (False, [])])
+    assert v == [1, 1, 1, 0, 1, 1, 1, -8] + [1] * 12 + [1, -10]
+    assert st.batch_retries == 1 and st.n_individual == n + 2
