@@ -50,9 +50,26 @@ def _compile(src: Path, hdr: str, verbose: bool) -> Path:
     return obj
 
 
+def build_coop_tables(verbose: bool = True) -> Path:
+    """Cooperative-kernel program tables (tools/gen_coop.py), regenerated when the
+    generator sources change."""
+    tools = ROOT / "tools"
+    out = OUT_DIR / "coop_tables.bin"
+    key = hashlib.sha256((tools / "gen_coop.py").read_bytes() + (tools / "circuits.py").read_bytes()).hexdigest()
+    stamp = OUT_DIR / ".coop_stamp"
+    if out.exists() and stamp.exists() and stamp.read_text() == key:
+        return out
+    if verbose:
+        print("[build] tools/gen_coop.py ->", out, flush=True)
+    subprocess.run([sys.executable, str(tools / "gen_coop.py"), str(out)], check=True)
+    stamp.write_text(key)
+    return out
+
+
 def build(jobs: int | None = None, verbose: bool = True) -> Path:
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    build_coop_tables(verbose)
     hdr = _headers_digest()
     srcs = sources()
     jobs = jobs or min(len(srcs), os.cpu_count() or 4)

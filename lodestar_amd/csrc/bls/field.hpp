@@ -194,6 +194,18 @@ __device__ __forceinline__ void bls_mac_s(uint64_t& lo, uint32_t& hi, uint32_t a
       : "+v"(lo), "+v"(hi), "=&s"(cc)
       : "v"(a), "s"(b));
 }
+// one a*b product on chain 1 and one m*p product on chain 2, interleaved in one
+// block (fewer inline-asm boundaries, two independent carry chains in flight)
+__device__ __forceinline__ void bls_mac2(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b, uint64_t& lo2,
+                                         uint32_t& hi2, uint32_t m, uint32_t p) {
+  uint64_t c1, c2;
+  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
+      "v_addc_co_u32 %1, %4, 0, %1, %4\n\t"
+      "v_addc_co_u32 %3, %5, 0, %3, %5"
+      : "+v"(lo), "+v"(hi), "+v"(lo2), "+v"(hi2), "=&s"(c1), "=&s"(c2)
+      : "v"(a), "v"(b), "v"(m), "s"(p));
+}
 
 BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
   uint32_t m[12];
@@ -204,8 +216,7 @@ BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
   for (int k = 0; k < 12; ++k) {
 #pragma unroll
     for (int i = 0; i < k; ++i) {
-      bls_mac(lo, hi, a.l[i], b.l[k - i]);
-      bls_mac_s(lo2, hi2, m[i], p_limb(k - i));
+      bls_mac2(lo, hi, a.l[i], b.l[k - i], lo2, hi2, m[i], p_limb(k - i));
     }
     bls_mac(lo, hi, a.l[k], b.l[0]);
     uint64_t s = lo + lo2;
@@ -222,8 +233,7 @@ BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
   for (int k = 12; k < 23; ++k) {
 #pragma unroll
     for (int i = k - 11; i < 12; ++i) {
-      bls_mac(lo, hi, a.l[i], b.l[k - i]);
-      bls_mac_s(lo2, hi2, m[i], p_limb(k - i));
+      bls_mac2(lo, hi, a.l[i], b.l[k - i], lo2, hi2, m[i], p_limb(k - i));
     }
     uint64_t s = lo + lo2;
     hi = hi + hi2 + (s < lo ? 1u : 0u);

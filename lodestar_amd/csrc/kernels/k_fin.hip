@@ -1,0 +1,110 @@
+// Cooperative finalisation (one 64-lane wavefront per task; programs from
+// tools/gen_coop.py, interpreter in bls/coop.hpp):
+//   k_chunk_coop  one task per chunk of >= 16 batchable requests
+//                 (worker.ts:56-88: random-scalar batch over the chunk's sets)
+//   k_indiv_coop  one task per request verified on its own
+//                 (failed chunks' requests and non-batchable requests, worker.ts:91-98)
+// Task: F = prod f_i, S = sum r_i sig_i (Jacobian, exceptional cases exact),
+//       F *= ML(-g1, S), verdict = (FE(F) == 1).
+#include "../launchers.hpp"
+#include "../bls/coop.hpp"
+
+using namespace bls;
+
+struct FinShared {
+  Fp frame[COOP_FRAME];
+  uint32_t flag;
+};
+
+__device__ __forceinline__ bool g2j_is_inf_global(const G2J& p) { return fp2_is_zero(p.z); }
+
+__device__ void fin_accumulate_set(const PipeBufs& b, const CoopEnv& env, FinShared& sh, uint32_t i, bool& s_inf) {
+  coop_load(sh.frame, FIN_G, reinterpret_cast<const Fp*>(&b.f[i]), 12);
+  coop_run(env, env.fin_fmul, sh.frame, &sh.flag);
+  const G2J& rs = b.rsig[i];
+  if (g2j_is_inf_global(rs)) return;
+  if (s_inf) {
+    coop_load(sh.frame, FIN_S, reinterpret_cast<const Fp*>(&rs), 6);
+    s_inf = false;
+    return;
+  }
+  coop_load(sh.frame, FIN_R, reinterpret_cast<const Fp*>(&rs), 6);
+  if (threadIdx.x == 0) sh.flag = 0;
+  __syncthreads();
+  coop_run(env, env.fin_g2add, sh.frame, &sh.flag);
+  if (sh.flag) {  // H may be zero: exact test (S == R -> doubling, S == -R -> infinity)
+    if (coop_is_zero(sh.frame, FIN_HR, 2)) {
+      if (coop_is_zero(sh.frame, FIN_HR + 2, 2)) {
+        coop_run(env, env.fin_g2dbl, sh.frame, &sh.flag);
+      } else {
+        s_inf = true;
+      }
+    }
+  }
+}
+
+__device__ bool fin_finish(const CoopEnv& env, FinShared& sh, bool s_inf) {
+  if (!s_inf) {
+    coop_run(env, env.fin_normz, sh.frame, &sh.flag);
+    coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
+    coop_run(env, env.fin_affine, sh.frame, &sh.flag);
+    coop_run(env, env.fin_ml_neg_g1, sh.frame, &sh.flag);
+  }
+  coop_run(env, env.fin_fe1, sh.frame, &sh.flag);
+  coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
+  coop_run(env, env.fin_fe2, sh.frame, &sh.flag);
+  bool one = fp_eq(lds_load_fp(sh.frame, FIN_F), c_one());
+  for (int k = 1; k < 12; ++k) one = one && fp_is_zero(lds_load_fp(sh.frame, FIN_F + k));
+  return one;
+}
+
+__device__ void fin_init(FinShared& sh) {
+  if (threadIdx.x < 12) lds_store_fp(sh.frame, FIN_F + threadIdx.x, threadIdx.x == 0 ? c_one() : fp_zero());
+  if (threadIdx.x == 0) sh.flag = 0;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv env) {
+  __shared__ FinShared sh;
+  const uint32_t c = blockIdx.x;
+  const uint32_t beg = b.chunk_off[c], end = b.chunk_off[c + 1];
+  for (uint32_t k = beg; k < end; ++k) {
+    if (b.req_status[b.chunk_reqs[k]] != BLS_OK) {
+      if (threadIdx.x == 0) b.chunk_ok[c] = 0;  // the batch would throw -> retry (worker.ts:81-87)
+      return;
+    }
+  }
+  fin_init(sh);
+  bool s_inf = true;
+  for (uint32_t k = beg; k < end; ++k) {
+    const uint32_t r = b.chunk_reqs[k];
+    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, s_inf);
+  }
+  bool ok = fin_finish(env, sh, s_inf);
+  if (threadIdx.x == 0) b.chunk_ok[c] = ok ? 1 : 0;
+}
+
+__global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv env) {
+  __shared__ FinShared sh;
+  const uint32_t t = blockIdx.x;
+  const uint32_t r = b.indiv_reqs[t];
+  const int32_t code = b.req_status[r];
+  if (code != BLS_OK) {
+    if (threadIdx.x == 0) b.indiv_verdict[t] = -code;
+    return;
+  }
+  fin_init(sh);
+  bool s_inf = true;
+  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, s_inf);
+  bool ok = fin_finish(env, sh, s_inf);
+  if (threadIdx.x == 0) b.indiv_verdict[t] = ok ? 1 : 0;
+}
+
+hipError_t launch_k_chunk_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
+  k_chunk_coop<<<b.n_chunks, COOP_LANES, 0, s>>>(b, env);
+  return hipGetLastError();
+}
+hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
+  k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env);
+  return hipGetLastError();
+}

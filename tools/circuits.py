@@ -1,0 +1,306 @@
+"""Circuit compiler for the cooperative (one wavefront per task) kernels.
+
+The tower / curve formulas are written once, in Python, as arithmetic over Fp:
+multiplications are nodes, additions / subtractions / small-integer scalings are
+kept symbolic as linear combinations (Lin) and folded into the operands of the
+multiplications that consume them.  The scheduler levels the DAG (a product's
+level = 1 + the deepest product it depends on), packs each level's products into
+steps of at most LANES lanes, materialises operands whose linear combination is
+too long, allocates frame slots with liveness, and emits the table the device
+interpreter (lodestar_amd/csrc/bls/coop.hpp) walks: one 64-byte op per lane per
+step.  Step semantics: every lane gathers its operands, the wave synchronises,
+every lane writes its result -- so a step may overwrite a slot it also reads.
+
+`simulate()` runs a program on Python integers with exactly those semantics; the
+tests check every program against the oracle's math (tests/test_circuits.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+LANES = 64
+KMAX = 8          # terms per operand linear combination
+CMAX = 32767      # |coefficient| of a term (int16)
+OP_NOP, OP_MUL, OP_LIN = 0, 1, 2
+ZCHECK = -1       # output "slot" of a zero-check op: ORs is_zero(value) into the task flag
+
+
+# ----------------------------------------------------------------------------
+# symbolic values
+# ----------------------------------------------------------------------------
+class Lin:
+    """sum coef * ref; ref = ('in', slot) | ('n', node_id) | ('c', const_index)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, terms=None):
+        self.t = {}
+        if terms:
+            for r, c in terms.items():
+                if c % P:
+                    self.t[r] = c
+
+    def __add__(self, o):
+        r = Lin(self.t)
+        for k, c in o.t.items():
+            r.t[k] = r.t.get(k, 0) + c
+            if r.t[k] == 0:
+                del r.t[k]
+        return r
+
+    def __neg__(self):
+        return Lin({k: -c for k, c in self.t.items()})
+
+    def __sub__(self, o):
+        return self + (-o)
+
+    def scale(self, s: int):
+        return Lin({k: c * s for k, c in self.t.items()})
+
+    def __mul__(self, s: int):
+        return self.scale(s)
+
+    __rmul__ = __mul__
+
+    def is_zero(self):
+        return not self.t
+
+
+@dataclass
+class Node:
+    a: Lin
+    b: Lin
+    id: int
+    kind: int = OP_MUL
+    level: int = 0
+    depth: int = 0   # LIN nodes: chain depth among LIN nodes of the same level
+
+
+class ConstBank:
+    """Fp constants shared by every program (plain integers; the emitter converts
+    them to Montgomery form).  Index 0 is 1."""
+
+    def __init__(self):
+        self.vals = [1]
+        self._idx = {1: 0}
+
+    def index(self, v: int) -> int:
+        v %= P
+        if v not in self._idx:
+            self._idx[v] = len(self.vals)
+            self.vals.append(v)
+        return self._idx[v]
+
+
+class Circuit:
+    def __init__(self, name: str, consts: ConstBank):
+        self.name = name
+        self.nodes: list[Node] = []
+        self.consts = consts
+        self.outputs: list[tuple[int, Lin]] = []
+        self.zchecks: list[Lin] = []
+
+    @staticmethod
+    def inp(slot: int) -> Lin:
+        return Lin({("in", slot): 1})
+
+    def const(self, value: int) -> Lin:
+        return Lin({("c", self.consts.index(value)): 1})
+
+    def one(self) -> Lin:
+        return self.const(1)
+
+    def mul(self, a: Lin, b: Lin) -> Lin:
+        if a.is_zero() or b.is_zero():
+            return Lin()
+        n = Node(a, b, len(self.nodes), OP_MUL)
+        self.nodes.append(n)
+        return Lin({("n", n.id): 1})
+
+    def mat(self, a: Lin) -> Lin:
+        """Materialise a linear combination (a LIN node) so consumers see one term."""
+        if len(a.t) <= 1 and all(c == 1 for c in a.t.values()):
+            return a
+        n = Node(a, Lin(), len(self.nodes), OP_LIN)
+        self.nodes.append(n)
+        return Lin({("n", n.id): 1})
+
+    def out(self, slot: int, v: Lin):
+        self.outputs.append((slot, v))
+
+    def zcheck(self, v: Lin):
+        self.zchecks.append(v)
+
+
+# ----------------------------------------------------------------------------
+# scheduled program
+# ----------------------------------------------------------------------------
+@dataclass
+class Op:
+    kind: int
+    out: int
+    a: list  # [(ref, coef)]; ref = slot int or ('c', idx)
+    b: list = field(default_factory=list)
+
+
+@dataclass
+class Program:
+    name: str
+    steps: list          # list[list[Op]]
+    n_slots: int
+    out_slots: list
+    n_mul_steps: int = 0
+
+
+def _refs(l: Lin):
+    return [k for k in l.t if k[0] == "n"]
+
+
+def schedule(c: Circuit, frame_slots: int, reserved: set, lanes: int = LANES) -> Program:
+    """Level-schedule circuit `c` into steps of <= `lanes` ops over a frame of
+    `frame_slots` slots.  `reserved` slots (the caller's live registers) are never
+    used for temporaries.  Products of level L run in phase (L, 0); linear
+    combinations whose deepest reference has level L run in phases (L, 1, depth)."""
+    nodes = c.nodes
+
+    def level_of(n: Node):
+        lv, dep = 0, 0
+        for l in (n.a, n.b):
+            for r in _refs(l):
+                m = nodes[r[1]]
+                lv = max(lv, m.level)
+        if n.kind == OP_MUL:
+            return lv + 1, 0
+        for r in _refs(n.a):
+            m = nodes[r[1]]
+            if m.kind == OP_LIN and m.level == lv:
+                dep = max(dep, m.depth + 1)
+        return lv, dep
+
+    def fit(l: Lin) -> Lin:
+        for cf in l.t.values():
+            if abs(cf) > CMAX:
+                raise ValueError(f"{c.name}: coefficient {cf} out of range")
+        if len(l.t) <= KMAX:
+            return l
+        items = list(l.t.items())
+        groups = [items[i: i + KMAX] for i in range(0, len(items), KMAX)]
+        res = {}
+        for g in groups:
+            if len(g) == 1:
+                res[g[0][0]] = g[0][1]
+                continue
+            ln = Node(Lin(dict(g)), Lin(), len(nodes), OP_LIN)
+            ln.level, ln.depth = level_of(ln)
+            nodes.append(ln)
+            res[("n", ln.id)] = 1
+        return fit(Lin(res))
+
+    i = 0
+    while i < len(nodes):   # nodes appended by fit() are already fitted and levelled
+        n = nodes[i]
+        if n.level == 0 and n.depth == 0 and not getattr(n, "_done", False):
+            n.a = fit(n.a)
+            n.b = fit(n.b)
+            n.level, n.depth = level_of(n)
+            n._done = True
+        i += 1
+    outs = [(slot, fit(v)) for slot, v in c.outputs]
+    zchecks = [fit(z) for z in c.zchecks]
+
+    def phase(n: Node):
+        return (n.level, 0, 0) if n.kind == OP_MUL else (n.level, 1, n.depth)
+
+    phases: dict = {}
+    for n in nodes:
+        phases.setdefault(phase(n), []).append(n)
+    order = sorted(phases)
+    rank = {ph: k for k, ph in enumerate(order)}
+    tail_rank = len(order)
+    last_use = {}
+
+    def note(l: Lin, r):
+        for x in _refs(l):
+            last_use[x[1]] = max(last_use.get(x[1], -1), r)
+
+    for ph, ns in phases.items():
+        for n in ns:
+            note(n.a, rank[ph])
+            note(n.b, rank[ph])
+    for _, v in outs:
+        note(v, tail_rank)
+    for z in zchecks:
+        note(z, tail_rank)
+
+    free = [s for s in range(frame_slots) if s not in reserved]
+    slot_of = {}
+    busy_until = {}
+    steps = []
+    n_mul = 0
+    for ph in order:
+        r = rank[ph]
+        for s, until in list(busy_until.items()):
+            if until < r:
+                del busy_until[s]
+                free.append(s)
+        free.sort()
+        ns = phases[ph]
+        for k in range(0, len(ns), lanes):
+            ops = []
+            for n in ns[k: k + lanes]:
+                if not free:
+                    raise RuntimeError(f"{c.name}: out of frame slots ({frame_slots})")
+                s = free.pop(0)
+                slot_of[n.id] = s
+                busy_until[s] = last_use.get(n.id, r)
+                ops.append(Op(n.kind, s, _emit(n.a, slot_of), _emit(n.b, slot_of)))
+            steps.append(ops)
+            if ph[1] == 0:
+                n_mul += 1
+    tail = [Op(OP_LIN, slot, _emit(v, slot_of)) for slot, v in outs]
+    tail += [Op(OP_LIN, ZCHECK, _emit(z, slot_of)) for z in zchecks]
+    for k in range(0, len(tail), lanes):
+        if k > 0:
+            raise RuntimeError(f"{c.name}: {len(tail)} outputs exceed one step")
+        steps.append(tail[k: k + lanes])
+    return Program(c.name, steps, frame_slots, [s for s, _ in outs], n_mul)
+
+
+def _emit(l: Lin, slot_of) -> list:
+    res = []
+    for k, cf in l.t.items():
+        if k[0] == "in":
+            res.append((k[1], cf))
+        elif k[0] == "c":
+            res.append((("c", k[1]), cf))
+        else:
+            res.append((slot_of[k[1]], cf))
+    return res
+
+
+# ----------------------------------------------------------------------------
+# simulation (exact device semantics)
+# ----------------------------------------------------------------------------
+def simulate(prog: Program, frame: list, consts: ConstBank) -> bool:
+    """Run `prog` in place on `frame` (list of ints mod P); returns the zero-check flag."""
+    flag = False
+
+    def val(terms):
+        s = 0
+        for ref, cf in terms:
+            v = consts.vals[ref[1]] if isinstance(ref, tuple) else frame[ref]
+            s += cf * v
+        return s % P
+
+    for step in prog.steps:
+        res = []
+        for op in step:
+            a = val(op.a)
+            res.append((op, a * val(op.b) % P if op.kind == OP_MUL else a))
+        for op, r in res:
+            if op.out == ZCHECK:
+                flag = flag or r == 0
+            else:
+                frame[op.out] = r
+    return flag
