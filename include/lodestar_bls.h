@@ -125,6 +125,11 @@ int bls_gpu_fp_mul_test(bls_gpu_ctx* ctx, const uint8_t* a48, const uint8_t* b48
 /* Probe: `lanes` lanes each run `iters` dependent Montgomery products. */
 int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iters, double* ns_per_fpm, double* fpm_per_s);
 
+/* Probe: time the cooperative (one wavefront per task) program `name` on `blocks`
+ * tasks, `reps` runs each; us_per_step = run time / step count. */
+int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint32_t reps, double* us_per_step,
+                       double* ms_total);
+
 #ifdef __cplusplus
 }
 #endif

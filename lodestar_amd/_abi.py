@@ -49,6 +49,7 @@ SYMBOLS = (
     "bls_gpu_mad_peak",
     "bls_gpu_fp_mul_test",
     "bls_gpu_fpm_bench",
+    "bls_gpu_coop_probe",
 )
 
 
@@ -109,6 +110,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         dp = ctypes.POINTER(ctypes.c_double)
         lib.bls_gpu_fpm_bench.argtypes = [vp, u32, u32, dp, dp]
         lib.bls_gpu_fpm_bench.restype = i32
+        lib.bls_gpu_coop_probe.argtypes = [vp, ctypes.c_char_p, u32, u32, dp, dp]
+        lib.bls_gpu_coop_probe.restype = i32
     return lib
 
 

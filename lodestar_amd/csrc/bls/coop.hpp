@@ -23,6 +23,7 @@ namespace bls {
 #define COOP_FRAME 256
 #define COOP_OUT_ZCHECK 0xFFFFu
 #define COOP_OUT_NONE 0xFFFEu
+#define COOP_MAX_CONSTS 64
 
 struct CoopOp {  // 80 bytes, one per lane per step (tools/gen_coop.py:emit)
   uint16_t out;
@@ -42,6 +43,7 @@ struct CoopProg {
 struct CoopEnv {
   const CoopOp* ops;
   const Fp* consts;
+  uint32_t n_consts;
   CoopProg fin_fmul, fin_g2add, fin_g2dbl, fin_normz, fin_affine, fin_ml_neg_g1, fin_fe1, fin_fe2;
 };
 
@@ -89,21 +91,89 @@ __device__ __forceinline__ void lds_store_fp(Fp* frame, uint32_t slot, const Fp&
   p[2] = make_uint4(v.l[8], v.l[9], v.l[10], v.l[11]);
 }
 
-__device__ __forceinline__ Fp coop_term(uint16_t ref, const Fp* frame, const Fp* consts) {
-  return (ref & 0x8000u) ? consts[ref & 0x7fffu] : lds_load_fp(frame, ref);
+// frame slot or (bit 15) constant-bank entry; both live in LDS
+__device__ __forceinline__ Fp coop_term(uint16_t ref, const Fp* frame, const Fp* cbank) {
+  return (ref & 0x8000u) ? lds_load_fp(cbank, ref & 0x7fffu) : lds_load_fp(frame, ref);
+}
+
+// Lazy linear combination: terms accumulate unreduced in a 13-limb two's-complement
+// accumulator (|sum| < 8 * 2^15 * p < 2^399); one reduction at the end.
+struct Acc13 {
+  uint32_t l[13];
+};
+
+__device__ __forceinline__ void acc_add(Acc13& a, const Fp& x) { asm_acc_add12(a.l, x.l); }
+
+__device__ __forceinline__ void acc_sub(Acc13& a, const Fp& x) { asm_acc_sub12(a.l, x.l); }
+
+// a += c * x for a small signed c
+__device__ __forceinline__ void acc_add_small(Acc13& a, const Fp& x, int c) {
+  const uint32_t m = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
+  uint32_t t[13], carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t v = (uint64_t)x.l[i] * m + carry;
+    t[i] = (uint32_t)v;
+    carry = (uint32_t)(v >> 32);
+  }
+  t[12] = carry;
+  if (c < 0) asm_acc_sub13(a.l, t);
+  else asm_acc_add13(a.l, t);
+}
+
+__device__ __forceinline__ uint32_t k20p_limb(int i) {  // 2^20 * p, 13 limbs
+  const uint32_t t[13] = {0xaab00000u, 0xfffffffau, 0xfffb9fefu, 0xffeb153fu, 0x6241eabfu, 0x2a0f6b0fu, 0x2bf6730du,
+                          0xb84f3851u, 0xcd764774u, 0x7b6434bau, 0x69a4b1bau, 0x1ea397feu, 0x0001a011u};
+  return t[i];
+}
+
+// canonical (sum mod p) of the accumulator
+__device__ __forceinline__ Fp acc_reduce(Acc13 a) {
+  uint32_t k20p[13];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) k20p[i] = k20p_limb(i);
+  asm_acc_add13(a.l, k20p);  // now 0 <= a < 2^21 p
+  // q ~ a / p from the top 96 bits in double precision (error < 1)
+  double d = (double)a.l[12] * 18446744073709551616.0 + (double)a.l[11] * 4294967296.0 + (double)a.l[10];
+  uint32_t q = (uint32_t)(d * 0x1.3b06ba5e7993dp-61);
+  uint32_t qp[13], carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t v = (uint64_t)p_limb(i) * q + carry;
+    qp[i] = (uint32_t)v;
+    carry = (uint32_t)(v >> 32);
+  }
+  qp[12] = carry;
+  asm_acc_sub13(a.l, qp);  // a - q p in [-p, 2p)
+  // a < 0 -> + p ; a >= p -> - p
+  const uint32_t pl[12] = {BLS_P_LIMBS};
+  Fp lo, up, dn;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) lo.l[i] = a.l[i];
+  const bool negative = (int32_t)a.l[12] < 0;
+  asm_add12(up.l, lo.l, pl);
+  const uint32_t bb = asm_sub12(dn.l, lo.l, pl);
+  const bool ge_p = !negative && bb == 0;
+  return negative ? up : (ge_p ? dn : lo);
 }
 
 __device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n,
-                                       const Fp* frame, const Fp* consts) {
-  Fp acc = fp_zero();
+                                       const Fp* frame, const Fp* cbank) {
+  if (n == 1 && cf[0] == 1) return coop_term(refs[0], frame, cbank);
+  Acc13 acc;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) acc.l[i] = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     if (k < n) {
-      Fp t = fp_mul_small(coop_term(refs[k], frame, consts), cf[k]);
-      acc = k == 0 ? t : fp_add(acc, t);
+      const Fp x = coop_term(refs[k], frame, cbank);
+      const int c = cf[k];
+      if (c == 1) acc_add(acc, x);
+      else if (c == -1) acc_sub(acc, x);
+      else acc_add_small(acc, x, c);
     }
   }
-  return acc;
+  return acc_reduce(acc);
 }
 
 union CoopOpWords {
@@ -111,21 +181,29 @@ union CoopOpWords {
   CoopOp op;
 };
 
-// Run one program on this block's frame.  *flag (LDS) is set when a zero-check op
-// sees zero.
-__device__ __noinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, uint32_t* flag) {
+__device__ __forceinline__ void coop_fetch(CoopOpWords& u, const uint4* base, uint32_t step, int lane) {
+  const uint4* src = base + ((size_t)step * COOP_LANES + lane) * 5;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) u.w[k] = src[k];
+}
+
+// Run one program on this block's frame.  cbank: the constant bank staged in LDS
+// (coop_stage_consts).  *flag (LDS) is set when a zero-check op sees zero.  The
+// next step's ops are fetched while the current step computes.
+__device__ __noinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
+                                      uint32_t* flag) {
   const int lane = threadIdx.x;
   const uint4* base = reinterpret_cast<const uint4*>(env.ops);
+  if (pg.n == 0) return;
+  CoopOpWords cur, nxt;
+  coop_fetch(cur, base, pg.first, lane);
   for (uint32_t s = 0; s < pg.n; ++s) {
-    CoopOpWords u;
-    const uint4* src = base + ((size_t)(pg.first + s) * COOP_LANES + lane) * 5;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) u.w[k] = src[k];
-    const CoopOp& op = u.op;
+    if (s + 1 < pg.n) coop_fetch(nxt, base, pg.first + s + 1, lane);
+    const CoopOp& op = cur.op;
     Fp r = fp_zero();
     if (op.kind != 0) {
-      r = coop_lin(op.a, op.ca, op.na, frame, env.consts);
-      if (op.kind == 1) r = fp_mul(r, coop_lin(op.b, op.cb, op.nb, frame, env.consts));
+      r = coop_lin(op.a, op.ca, op.na, frame, cbank);
+      if (op.kind == 1) r = fp_mul(r, coop_lin(op.b, op.cb, op.nb, frame, cbank));
     }
     __syncthreads();
     if (op.kind != 0) {
@@ -136,7 +214,14 @@ __device__ __noinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame
       }
     }
     __syncthreads();
+    cur = nxt;
   }
+}
+
+// copy the constant bank into LDS (once per block)
+__device__ __forceinline__ void coop_stage_consts(const CoopEnv& env, Fp* cbank) {
+  for (uint32_t k = threadIdx.x; k < env.n_consts; k += COOP_LANES) lds_store_fp(cbank, k, env.consts[k]);
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------

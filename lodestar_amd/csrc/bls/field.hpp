@@ -66,6 +66,35 @@ BLS_HD uint32_t p_limb(int i) {
   return t[i];
 }
 
+// 32-bit add / subtract with carry.  With clang (hipcc, device and host) these are
+// the carry builtins, which lower to v_add_co_u32 / v_addc_co_u32 / v_subb_co_u32
+// chains on gfx950; the g++ build of the test harness uses 64-bit arithmetic.
+#if defined(__clang__)
+BLS_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  unsigned co;
+  unsigned r = __builtin_addc(a, b, cin, &co);
+  *cout = co;
+  return r;
+}
+BLS_HD uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  unsigned bo;
+  unsigned r = __builtin_subc(a, b, bin, &bo);
+  *bout = bo;
+  return r;
+}
+#else
+BLS_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  uint64_t t = (uint64_t)a + b + cin;
+  *cout = (uint32_t)(t >> 32);
+  return (uint32_t)t;
+}
+BLS_HD uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  uint64_t t = (uint64_t)a - b - bin;
+  *bout = (uint32_t)(t >> 63);
+  return (uint32_t)t;
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Fp
 // ---------------------------------------------------------------------------
@@ -101,14 +130,39 @@ BLS_HD Fp fp_select(bool c, const Fp& a, const Fp& b) {
 BLS_HD uint32_t fp_sub_p(const Fp& a, Fp& d) {
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)a.l[i] - p_limb(i) - borrow;
-    d.l[i] = (uint32_t)t;
-    borrow = (uint32_t)(t >> 63);
-  }
+  for (int i = 0; i < 12; ++i) d.l[i] = subc32(a.l[i], p_limb(i), borrow, &borrow);
   return borrow;
 }
 
+#if defined(__HIPCC__)
+}  // namespace bls
+#include "carry_asm.hpp"
+namespace bls {
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// gfx950: each chain is one inline-asm block (tools/gen_carry_asm.py)
+BLS_HD Fp fp_reduce_once(const Fp& s) {
+  const uint32_t pl[12] = {BLS_P_LIMBS};
+  Fp r;
+  asm_reduce12(r.l, s.l, pl);
+  return r;
+}
+
+BLS_HD Fp fp_add(const Fp& a, const Fp& b) {
+  Fp s;
+  asm_add12(s.l, a.l, b.l);  // a + b < 2p < 2^382: no carry out
+  return fp_reduce_once(s);
+}
+
+BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
+  const uint32_t pl[12] = {BLS_P_LIMBS};
+  Fp d, r;
+  uint32_t borrow = asm_sub12(d.l, a.l, b.l);
+  asm_add12_masked(r.l, d.l, pl, 0u - borrow);  // a < b: add p back
+  return r;
+}
+#else
 // Reduce a value < 2p to [0, p).
 BLS_HD Fp fp_reduce_once(const Fp& s) {
   Fp d;
@@ -118,38 +172,27 @@ BLS_HD Fp fp_reduce_once(const Fp& s) {
 
 BLS_HD Fp fp_add(const Fp& a, const Fp& b) {
   Fp s;
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    c += (uint64_t)a.l[i] + b.l[i];
-    s.l[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  for (int i = 0; i < 12; ++i) s.l[i] = addc32(a.l[i], b.l[i], c, &c);
   return fp_reduce_once(s);  // a + b < 2p < 2^382: no carry out
 }
-
-BLS_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
 BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
   Fp d;
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)a.l[i] - b.l[i] - borrow;
-    d.l[i] = (uint32_t)t;
-    borrow = (uint32_t)(t >> 63);
-  }
+  for (int i = 0; i < 12; ++i) d.l[i] = subc32(a.l[i], b.l[i], borrow, &borrow);
   // if a < b add p back
   uint32_t mask = 0u - borrow;
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    c += (uint64_t)d.l[i] + (p_limb(i) & mask);
-    d.l[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  for (int i = 0; i < 12; ++i) d.l[i] = addc32(d.l[i], p_limb(i) & mask, c, &c);
   return d;
 }
+#endif
+
+BLS_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
 BLS_HD Fp fp_neg(const Fp& a) {
   Fp z = fp_zero();
@@ -160,13 +203,9 @@ BLS_HD Fp fp_neg(const Fp& a) {
 BLS_HD Fp fp_half(const Fp& a) {
   uint32_t mask = 0u - (a.l[0] & 1u);
   Fp s;
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    c += (uint64_t)a.l[i] + (p_limb(i) & mask);
-    s.l[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  for (int i = 0; i < 12; ++i) s.l[i] = addc32(a.l[i], p_limb(i) & mask, c, &c);
   Fp r;
 #pragma unroll
   for (int i = 0; i < 11; ++i) r.l[i] = (s.l[i] >> 1) | (s.l[i + 1] << 31);

@@ -13,6 +13,7 @@ using namespace bls;
 
 struct FinShared {
   Fp frame[COOP_FRAME];
+  Fp cbank[COOP_MAX_CONSTS];
   uint32_t flag;
 };
 
@@ -20,7 +21,7 @@ __device__ __forceinline__ bool g2j_is_inf_global(const G2J& p) { return fp2_is_
 
 __device__ void fin_accumulate_set(const PipeBufs& b, const CoopEnv& env, FinShared& sh, uint32_t i, bool& s_inf) {
   coop_load(sh.frame, FIN_G, reinterpret_cast<const Fp*>(&b.f[i]), 12);
-  coop_run(env, env.fin_fmul, sh.frame, &sh.flag);
+  coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
   const G2J& rs = b.rsig[i];
   if (g2j_is_inf_global(rs)) return;
   if (s_inf) {
@@ -31,11 +32,11 @@ __device__ void fin_accumulate_set(const PipeBufs& b, const CoopEnv& env, FinSha
   coop_load(sh.frame, FIN_R, reinterpret_cast<const Fp*>(&rs), 6);
   if (threadIdx.x == 0) sh.flag = 0;
   __syncthreads();
-  coop_run(env, env.fin_g2add, sh.frame, &sh.flag);
+  coop_run(env, env.fin_g2add, sh.frame, sh.cbank, &sh.flag);
   if (sh.flag) {  // H may be zero: exact test (S == R -> doubling, S == -R -> infinity)
     if (coop_is_zero(sh.frame, FIN_HR, 2)) {
       if (coop_is_zero(sh.frame, FIN_HR + 2, 2)) {
-        coop_run(env, env.fin_g2dbl, sh.frame, &sh.flag);
+        coop_run(env, env.fin_g2dbl, sh.frame, sh.cbank, &sh.flag);
       } else {
         s_inf = true;
       }
@@ -45,20 +46,21 @@ __device__ void fin_accumulate_set(const PipeBufs& b, const CoopEnv& env, FinSha
 
 __device__ bool fin_finish(const CoopEnv& env, FinShared& sh, bool s_inf) {
   if (!s_inf) {
-    coop_run(env, env.fin_normz, sh.frame, &sh.flag);
+    coop_run(env, env.fin_normz, sh.frame, sh.cbank, &sh.flag);
     coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
-    coop_run(env, env.fin_affine, sh.frame, &sh.flag);
-    coop_run(env, env.fin_ml_neg_g1, sh.frame, &sh.flag);
+    coop_run(env, env.fin_affine, sh.frame, sh.cbank, &sh.flag);
+    coop_run(env, env.fin_ml_neg_g1, sh.frame, sh.cbank, &sh.flag);
   }
-  coop_run(env, env.fin_fe1, sh.frame, &sh.flag);
+  coop_run(env, env.fin_fe1, sh.frame, sh.cbank, &sh.flag);
   coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
-  coop_run(env, env.fin_fe2, sh.frame, &sh.flag);
+  coop_run(env, env.fin_fe2, sh.frame, sh.cbank, &sh.flag);
   bool one = fp_eq(lds_load_fp(sh.frame, FIN_F), c_one());
   for (int k = 1; k < 12; ++k) one = one && fp_is_zero(lds_load_fp(sh.frame, FIN_F + k));
   return one;
 }
 
-__device__ void fin_init(FinShared& sh) {
+__device__ void fin_init(const CoopEnv& env, FinShared& sh) {
+  coop_stage_consts(env, sh.cbank);
   if (threadIdx.x < 12) lds_store_fp(sh.frame, FIN_F + threadIdx.x, threadIdx.x == 0 ? c_one() : fp_zero());
   if (threadIdx.x == 0) sh.flag = 0;
   __syncthreads();
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv e
       return;
     }
   }
-  fin_init(sh);
+  fin_init(env, sh);
   bool s_inf = true;
   for (uint32_t k = beg; k < end; ++k) {
     const uint32_t r = b.chunk_reqs[k];
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
     if (threadIdx.x == 0) b.indiv_verdict[t] = -code;
     return;
   }
-  fin_init(sh);
+  fin_init(env, sh);
   bool s_inf = true;
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, s_inf);
   bool ok = fin_finish(env, sh, s_inf);
@@ -106,5 +108,27 @@ hipError_t launch_k_chunk_coop(const PipeBufs& b, const CoopEnv& env, hipStream_
 }
 hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
   k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env);
+  return hipGetLastError();
+}
+
+// Probe: run program `pg` `reps` times on a block-private frame of pseudo-random
+// field elements (timing of the interpreter; results discarded).
+__global__ __launch_bounds__(COOP_LANES) void k_coop_probe(CoopEnv env, CoopProg pg, uint32_t reps, uint32_t* sink) {
+  __shared__ FinShared sh;
+  coop_stage_consts(env, sh.cbank);
+  for (int k = threadIdx.x; k < COOP_FRAME; k += COOP_LANES) {
+    Fp v = fp_zero();
+    for (int i = 0; i < 11; ++i) v.l[i] = (uint32_t)(k * 2654435761u + i * 40503u + blockIdx.x);
+    lds_store_fp(sh.frame, k, v);
+  }
+  if (threadIdx.x == 0) sh.flag = 0;
+  __syncthreads();
+  for (uint32_t r = 0; r < reps; ++r) coop_run(env, pg, sh.frame, sh.cbank, &sh.flag);
+  if (threadIdx.x == 0 && sh.frame[0].l[0] == 0x12345678u) sink[blockIdx.x] = sh.flag;
+}
+
+hipError_t launch_k_coop_probe(const CoopEnv& env, CoopProg pg, uint32_t blocks, uint32_t reps, uint32_t* sink,
+                               hipStream_t s) {
+  k_coop_probe<<<blocks, COOP_LANES, 0, s>>>(env, pg, reps, sink);
   return hipGetLastError();
 }

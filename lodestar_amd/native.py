@@ -213,6 +213,12 @@ class GpuContext:
                     "bls_gpu_fpm_bench")
         return ns.value, rate.value
 
+    def coop_probe(self, name: str, blocks: int, reps: int) -> tuple[float, float]:
+        us, ms = ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.bls_gpu_coop_probe(self._h, name.encode(), blocks, reps, ctypes.byref(us),
+                                                ctypes.byref(ms)), "bls_gpu_coop_probe")
+        return us.value, ms.value
+
     def sign(self, sks: bytes | np.ndarray, msgs: bytes | np.ndarray) -> np.ndarray:
         s, m = _u8(sks), _u8(msgs)
         n = s.size // 32
