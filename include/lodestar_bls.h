@@ -128,7 +128,7 @@ int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iters, double* 
 /* Probe: time the cooperative (one wavefront per task) program `name` on `blocks`
  * tasks, `reps` runs each; us_per_step = run time / step count. */
 int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint32_t reps, double* us_per_step,
-                       double* ms_total);
+                       double* ms_total, uint64_t* step_stamps /* nullable, n_steps + 1 s_memtime stamps */);
 
 #ifdef __cplusplus
 }

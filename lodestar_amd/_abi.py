@@ -110,7 +110,7 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         dp = ctypes.POINTER(ctypes.c_double)
         lib.bls_gpu_fpm_bench.argtypes = [vp, u32, u32, dp, dp]
         lib.bls_gpu_fpm_bench.restype = i32
-        lib.bls_gpu_coop_probe.argtypes = [vp, ctypes.c_char_p, u32, u32, dp, dp]
+        lib.bls_gpu_coop_probe.argtypes = [vp, ctypes.c_char_p, u32, u32, dp, dp, vp]
         lib.bls_gpu_coop_probe.restype = i32
     return lib
 

@@ -45,6 +45,7 @@ struct CoopEnv {
   const Fp* consts;
   uint32_t n_consts;
   CoopProg fin_fmul, fin_g2add, fin_g2dbl, fin_normz, fin_affine, fin_ml_neg_g1, fin_fe1, fin_fe2;
+  CoopProg set_ml;
 };
 
 // fin frame registers
@@ -190,14 +191,16 @@ __device__ __forceinline__ void coop_fetch(CoopOpWords& u, const uint4* base, ui
 // Run one program on this block's frame.  cbank: the constant bank staged in LDS
 // (coop_stage_consts).  *flag (LDS) is set when a zero-check op sees zero.  The
 // next step's ops are fetched while the current step computes.
-__device__ __noinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
-                                      uint32_t* flag) {
+template <bool TIMED>
+__device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
+                                        uint32_t* flag, uint64_t* stamps) {
   const int lane = threadIdx.x;
   const uint4* base = reinterpret_cast<const uint4*>(env.ops);
   if (pg.n == 0) return;
   CoopOpWords cur, nxt;
   coop_fetch(cur, base, pg.first, lane);
   for (uint32_t s = 0; s < pg.n; ++s) {
+    if (TIMED && lane == 0) stamps[s] = __builtin_amdgcn_s_memtime();
     if (s + 1 < pg.n) coop_fetch(nxt, base, pg.first + s + 1, lane);
     const CoopOp& op = cur.op;
     Fp r = fp_zero();
@@ -216,6 +219,12 @@ __device__ __noinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame
     __syncthreads();
     cur = nxt;
   }
+  if (TIMED && lane == 0) stamps[pg.n] = __builtin_amdgcn_s_memtime();
+}
+
+__device__ __forceinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
+                                         uint32_t* flag) {
+  coop_run_t<false>(env, pg, frame, cbank, flag, nullptr);
 }
 
 // copy the constant bank into LDS (once per block)

@@ -113,7 +113,8 @@ hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, hipStream_
 
 // Probe: run program `pg` `reps` times on a block-private frame of pseudo-random
 // field elements (timing of the interpreter; results discarded).
-__global__ __launch_bounds__(COOP_LANES) void k_coop_probe(CoopEnv env, CoopProg pg, uint32_t reps, uint32_t* sink) {
+__global__ __launch_bounds__(COOP_LANES) void k_coop_probe(CoopEnv env, CoopProg pg, uint32_t reps, uint32_t* sink,
+                                                          uint64_t* stamps) {
   __shared__ FinShared sh;
   coop_stage_consts(env, sh.cbank);
   for (int k = threadIdx.x; k < COOP_FRAME; k += COOP_LANES) {
@@ -125,10 +126,11 @@ __global__ __launch_bounds__(COOP_LANES) void k_coop_probe(CoopEnv env, CoopProg
   __syncthreads();
   for (uint32_t r = 0; r < reps; ++r) coop_run(env, pg, sh.frame, sh.cbank, &sh.flag);
   if (threadIdx.x == 0 && sh.frame[0].l[0] == 0x12345678u) sink[blockIdx.x] = sh.flag;
+  if (stamps && blockIdx.x == 0) coop_run_t<true>(env, pg, sh.frame, sh.cbank, &sh.flag, stamps);
 }
 
 hipError_t launch_k_coop_probe(const CoopEnv& env, CoopProg pg, uint32_t blocks, uint32_t reps, uint32_t* sink,
-                               hipStream_t s) {
-  k_coop_probe<<<blocks, COOP_LANES, 0, s>>>(env, pg, reps, sink);
+                               uint64_t* stamps, hipStream_t s) {
+  k_coop_probe<<<blocks, COOP_LANES, 0, s>>>(env, pg, reps, sink, stamps);
   return hipGetLastError();
 }

@@ -213,10 +213,14 @@ class GpuContext:
                     "bls_gpu_fpm_bench")
         return ns.value, rate.value
 
-    def coop_probe(self, name: str, blocks: int, reps: int) -> tuple[float, float]:
+    def coop_probe(self, name: str, blocks: int, reps: int, n_stamps: int = 0):
+        """(us per step, ms total[, per-step s_memtime stamps of one run])"""
         us, ms = ctypes.c_double(), ctypes.c_double()
+        stamps = np.zeros(n_stamps, dtype=np.uint64) if n_stamps else None
         self._check(self.lib.bls_gpu_coop_probe(self._h, name.encode(), blocks, reps, ctypes.byref(us),
-                                                ctypes.byref(ms)), "bls_gpu_coop_probe")
+                                                ctypes.byref(ms), _ptr(stamps)), "bls_gpu_coop_probe")
+        if stamps is not None:
+            return us.value, ms.value, stamps
         return us.value, ms.value
 
     def sign(self, sks: bytes | np.ndarray, msgs: bytes | np.ndarray) -> np.ndarray:

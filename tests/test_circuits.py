@@ -116,3 +116,19 @@ def test_fin_g2dbl(progs, oracle):
     fr[GC.INV_OUT] = pow(fr[GC.INV_IN], P - 2, P)
     simulate(pg["fin_affine"], fr, consts)
     assert ((fr[GC.Q], fr[GC.Q + 1]), (fr[GC.Q + 2], fr[GC.Q + 3])) == oracle.E2.dbl(p1)
+
+
+def test_set_ml_jacobian_p(progs, oracle):
+    """Per-set Miller loop with the G1 point in Jacobian form (line scaled by Z^3)."""
+    pg, consts = progs
+    rng = random.Random(5)
+    q = oracle.E2.mul(oracle.G2, rng.randrange(1, 1 << 64))
+    pp = oracle.E1.mul(oracle.G1, rng.randrange(1, 1 << 64))
+    z = rng.randrange(1, P)
+    fr = [0] * GC.FRAME
+    fr[GC.SQ:GC.SQ + 4] = [q[0][0], q[0][1], q[1][0], q[1][1]]
+    fr[GC.SP:GC.SP + 3] = [pp[0] * z * z % P, pp[1] * z * z * z % P, z]
+    simulate(pg["set_ml"], fr, consts)
+    got = get12(fr, GC.SF)
+    want = oracle.miller_loop(pp, q)
+    assert oracle.final_exponentiation(got, 3) == oracle.final_exponentiation(want, 3)

@@ -1,16 +1,31 @@
 #!/usr/bin/env python3
-"""Time the cooperative programs on cuda:0 (interpreter cost per step)."""
+"""Time the cooperative programs on cuda:0: us per step at 1 / 64 / 1024 tasks, and
+per-step s_memtime stamps of one run split by step kind (product steps vs
+linear-combination steps)."""
 import json
 import sys
 from pathlib import Path
 
+import numpy as np
+
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+import gen_coop  # noqa: E402
 from lodestar_amd.native import GpuContext  # noqa: E402
 
+progs, _ = gen_coop.build_all()
+kinds = {p.name: [any(op.kind == 1 for op in st) for st in p.steps] for p in progs}
 with GpuContext(0) as g:
     out = {}
-    for name, reps in (("fin_fmul", 200), ("fin_g2add", 100), ("fin_ml_neg_g1", 3), ("fin_fe2", 2)):
+    for name, reps in (("fin_fmul", 200), ("fin_g2add", 100), ("set_ml", 3), ("fin_fe2", 2)):
         for blocks in (1, 64, 1024):
             us, ms = g.coop_probe(name, blocks, reps)
             out[f"{name}@{blocks}"] = {"us_per_step": round(us, 3), "ms_per_run": round(ms / reps, 3)}
+        k = kinds[name]
+        _, _, st = g.coop_probe(name, 1, 1, len(k) + 1)
+        d = np.diff(st.astype(np.int64))  # s_memtime ticks (100 MHz constant clock on gfx9)
+        mul = d[np.array(k)]
+        lin = d[~np.array(k)]
+        out[f"{name}:stamps"] = {"mul_steps": int(len(mul)), "mul_ticks_mean": float(mul.mean()) if len(mul) else 0,
+                                 "lin_steps": int(len(lin)), "lin_ticks_mean": float(lin.mean()) if len(lin) else 0}
     print(json.dumps(out, indent=1))

@@ -37,6 +37,9 @@ INV_IN, INV_OUT = 40, 41
 E = 42
 HR = 50   # H (2 slots) and S2 - S1 (2 slots) of the last G2 addition
 
+# "set" frame registers
+SQ, SP, SF = 0, 4, 8
+
 
 # ----------------------------------------------------------------------------
 # tower over Lin (same formulas as field.hpp)
@@ -494,9 +497,27 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
     path.write_bytes(header + cbin + bytes(table) + bytes(steps_bin))
 
 
+def build_set(consts: ConstBank) -> list[Program]:
+    """Per-set programs ("set" frame):
+         SQ 0..3   H(m) affine (G2)           SP 4..6   r*pk Jacobian (G1)
+         SF 8..19  Miller-loop output f_i     temporaries 24..FRAME-1"""
+    progs = []
+    regs = set(range(0, 24))
+    c = Circuit("set_ml", consts)
+    t = T(c)
+    X, Y, Z = (Circuit.inp(SP + k) for k in range(3))
+    z2 = c.mul(Z, Z)
+    pz3 = c.mat(c.mul(z2, Z))
+    pxz = c.mat(c.mul(X, Z))
+    ml = miller_loop(t, t.f2(SQ), t.f2(SQ + 2), pxz, Y, pz3)
+    out12(c, SF, ml)
+    progs.append(schedule(c, FRAME, regs))
+    return progs
+
+
 def build_all():
     consts = ConstBank()
-    progs = build_fin(consts)
+    progs = build_fin(consts) + build_set(consts)
     return progs, consts
 
 
