@@ -37,8 +37,23 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-STAGE_NAMES = ["h2d", "k_pk", "k_sig", "k_h2c", "k_scale", "k_miller", "k_status+k_chunk", "k_indiv"]
-STAGE_WORK = {"k_sig": "sig", "k_h2c": "h2c", "k_scale": "scale", "k_miller": "miller"}
+STAGE_NAMES = ["h2d", "k_pk", "k_pre", "k_pset", "k_exact", "-", "k_status+k_chunk", "k_indiv"]
+X_ABS = 0xD201000000010000
+MADS_PER_FPM = 288   # 12x12 limb products + 12x12 reduction products per Montgomery product
+
+
+def pset_products_per_set() -> float:
+    """Expected Fp products k_pset executes per set (program MUL ops from
+    lodestar_amd/_native/coop_programs.json; r's bits are uniform)."""
+    pg = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
+    m = {k: v["mul_ops"] for k, v in pg.items()}
+    n = m["pset_prep"] + m["pset_dbl_r"] + 0.5 * m["pset_add_r"] + 63 * m["pset_dbl_all"]
+    for i in range(62, -1, -1):
+        if (X_ABS >> i) & 1:
+            n += 0.5 * m["pset_add_xr"] + 0.5 * m["pset_add_x"]
+        else:
+            n += 0.5 * m["pset_add_r"]
+    return n + m["pset_phase2"] + m["pset_norm2"] + m["pset_affine2"] + m["pset_ml2"]
 
 
 def interop_sk(i: int) -> bytes:
@@ -142,12 +157,12 @@ def main() -> None:
         lat.append((time.perf_counter() - t1) * 1e3)
         assert v[0] == 1
 
-    # roofline of the dominant kernel (VALU integer multiply-add bound)
-    wm = json.loads((ROOT / "lodestar_amd" / "work_model.json").read_text())
+    # roofline of the dominant kernel, k_pset (VALU integer multiply-add bound)
     stage_ms = stage_sum / args.steps
-    dom = max(STAGE_WORK, key=lambda k: stage_ms[STAGE_NAMES.index(k)])
+    dom = "k_pset"
     dom_ms = stage_ms[STAGE_NAMES.index(dom)]
-    mads = wm["fpm_per_set"][STAGE_WORK[dom]] * wm["mads_per_fpm"] * args.sets
+    fpm_set = pset_products_per_set()
+    mads = fpm_set * MADS_PER_FPM * args.sets
     achieved = mads / (dom_ms * 1e-3) / 1e12
     peak_rate, _ = gpu.mad_peak()
     peak = peak_rate / 1e12
@@ -175,8 +190,8 @@ def main() -> None:
             "stage_ms": {k: round(float(x), 3) for k, x in zip(STAGE_NAMES, stage_ms)},
             "roofline": {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
                          "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5), "traffic": None,
-                         "work": f"{wm['fpm_per_set'][STAGE_WORK[dom]]:.0f} Fp products/set x "
-                                 f"{wm['mads_per_fpm']} MAD x {args.sets} sets per launch"},
+                         "work": f"{fpm_set:.0f} Fp products/set x {MADS_PER_FPM} MAD x {args.sets} sets "
+                                 f"per launch, {dom_ms:.3f} ms/launch (HIP events)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()

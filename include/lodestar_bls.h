@@ -65,7 +65,7 @@ typedef struct bls_stats {
   uint32_t n_chunks;           /* batchable chunks (chunkifyMaximizeChunkSize(reqs, 16)) */
   uint32_t n_individual;       /* requests verified on their own */
   double device_ms;            /* device time of the call (HIP events) */
-  double stage_ms[8];          /* per stage: h2d, pk, sig, h2c, scale, miller, status+chunk, individual */
+  double stage_ms[8];          /* per stage: h2d, pk, pre (SSWU + sig decode), pset, exact, -, status+chunk, individual */
 } bls_stats;
 
 typedef struct bls_gpu_ctx bls_gpu_ctx;
@@ -129,6 +129,11 @@ int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iters, double* 
  * tasks, `reps` runs each; us_per_step = run time / step count. */
 int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint32_t reps, double* us_per_step,
                        double* ms_total, uint64_t* step_stamps /* nullable, n_steps + 1 s_memtime stamps */);
+
+/* Test hook: BLS_DEBUG_FORCE_EXACT routes every set through the exact single-lane
+ * path (k_exact) instead of the cooperative kernel, so parity tests cover both. */
+#define BLS_DEBUG_FORCE_EXACT 1u
+int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus
 }

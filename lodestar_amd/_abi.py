@@ -50,7 +50,9 @@ SYMBOLS = (
     "bls_gpu_fp_mul_test",
     "bls_gpu_fpm_bench",
     "bls_gpu_coop_probe",
+    "bls_gpu_set_debug_flags",
 )
+DEBUG_FORCE_EXACT = 1
 
 
 class BlsBatch(ctypes.Structure):
@@ -112,6 +114,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_fpm_bench.restype = i32
         lib.bls_gpu_coop_probe.argtypes = [vp, ctypes.c_char_p, u32, u32, dp, dp, vp]
         lib.bls_gpu_coop_probe.restype = i32
+        lib.bls_gpu_set_debug_flags.argtypes = [vp, u32]
+        lib.bls_gpu_set_debug_flags.restype = i32
     return lib
 
 

@@ -55,9 +55,10 @@ def build_coop_tables(verbose: bool = True) -> Path:
     generator sources change."""
     tools = ROOT / "tools"
     out = OUT_DIR / "coop_tables.bin"
-    key = hashlib.sha256((tools / "gen_coop.py").read_bytes() + (tools / "circuits.py").read_bytes()).hexdigest()
+    key = hashlib.sha256(b"".join((tools / f).read_bytes()
+                                  for f in ("gen_coop.py", "gen_pset.py", "circuits.py", "gen_constants.py"))).hexdigest()
     stamp = OUT_DIR / ".coop_stamp"
-    if out.exists() and stamp.exists() and stamp.read_text() == key:
+    if out.exists() and out.with_name("coop_programs.json").exists() and stamp.exists() and stamp.read_text() == key:
         return out
     if verbose:
         print("[build] tools/gen_coop.py ->", out, flush=True)
@@ -95,7 +96,7 @@ def build_hostsim(verbose: bool = True) -> Path:
     hdr = _headers_digest()
     key = hashlib.sha256(hdr.encode() + src.read_bytes()).hexdigest()[:16]
     stamp = out.with_suffix(".stamp")
-    if out.exists() and stamp.exists() and stamp.read_text() == key:
+    if out.exists() and out.with_name("coop_programs.json").exists() and stamp.exists() and stamp.read_text() == key:
         return out
     cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-DBLS_COUNT_OPS", "-I", str(CSRC), "-I",
            str(ROOT / "include"), "-o", str(out), str(src)]

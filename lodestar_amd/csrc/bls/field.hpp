@@ -342,6 +342,74 @@ BLS_HD Fp fp_pow_const(const Fp& a) {
 
 BLS_HD Fp fp_inv(const Fp& a) { return fp_pow_const<e_p_minus_2, E_P_MINUS_2_BITS>(a); }
 
+// ---------------------------------------------------------------------------
+// Fp inversion by the binary extended Euclidean algorithm (variable time: all
+// inputs are public).  ~2 log2(p) shift steps of 12-limb words instead of the
+// ~450 dependent Montgomery products of Fermat's a^(p-2).
+// In: a in Montgomery form (aR).  Out: a^-1 in Montgomery form (a^-1 R); 0 -> 0.
+// ---------------------------------------------------------------------------
+BLS_HD bool big_is_one(const Fp& a) {
+  uint32_t acc = a.l[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 12; ++i) acc |= a.l[i];
+  return acc == 0;
+}
+
+BLS_HD void big_shr1(Fp& a) {
+#pragma unroll
+  for (int i = 0; i < 11; ++i) a.l[i] = (a.l[i] >> 1) | (a.l[i + 1] << 31);
+  a.l[11] >>= 1;
+}
+
+// a >= b (plain 384-bit)
+BLS_HD bool big_geq(const Fp& a, const Fp& b) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.l[i] - b.l[i] - borrow;
+    borrow = (uint32_t)(t >> 63);
+  }
+  return borrow == 0;
+}
+
+BLS_HD void big_sub(Fp& a, const Fp& b) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.l[i] - b.l[i] - borrow;
+    a.l[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+}
+
+BLS_NOINLINE Fp fp_inv_gcd(Fp a) {
+  if (fp_is_zero(a)) return fp_zero();
+  Fp u = a, v, x1 = fp_zero(), x2 = fp_zero();
+#pragma unroll
+  for (int i = 0; i < 12; ++i) v.l[i] = p_limb(i);
+  x1.l[0] = 1;
+  while (!big_is_one(u) && !big_is_one(v)) {
+    while (!(u.l[0] & 1u)) {
+      big_shr1(u);
+      x1 = fp_half(x1);
+    }
+    while (!(v.l[0] & 1u)) {
+      big_shr1(v);
+      x2 = fp_half(x2);
+    }
+    if (big_geq(u, v)) {
+      big_sub(u, v);
+      x1 = fp_sub(x1, x2);
+    } else {
+      big_sub(v, u);
+      x2 = fp_sub(x2, x1);
+    }
+  }
+  Fp inv = big_is_one(u) ? x1 : x2;   // (aR)^-1 mod p
+  return fp_mul(inv, c_r3());          // (aR)^-1 R^3 / R = a^-1 R
+}
+
+
 // Is the (plain, non-Montgomery) value a > (p-1)/2 ?  (ZCash "lexicographically largest")
 BLS_HD bool fp_plain_gt_half(const Fp& a) {
   const uint32_t h[12] = {BLS_HALF_P_LIMBS};

@@ -171,6 +171,49 @@ BLS_HD G2A map_to_curve_sswu(const Fp2& u) {
   return r;
 }
 
+// Simplified SWU with two Fp exponentiations whichever branch is taken (the
+// verify pipeline's stage_pre_sswu).  Same output as map_to_curve_sswu:
+//   * 1/den by one Fp inversion of the norm (binary GCD);
+//   * g(x1) is a square in Fp2 iff N(g(x1)) is a square in Fp, decided by
+//     gamma = N(g(x1))^((p+1)/4): gamma^2 == N  ->  x = x1, sqrt(N) = gamma;
+//     otherwise gamma^2 == -N and, g(x2) = Z^3 u^6 g(x1) with N(Z) = 5,
+//     sqrt(N(g(x2))) = N(u)^3 sqrt(-125) gamma  (no second Legendre exponentiation);
+//   * the Fp2 root from sqrt(N) as in fp2_sqrt (one (p-3)/4 exponentiation); the
+//     sign of sqrt(N) does not matter since y is normalised by sgn0(u).
+// Returns false (the caller falls back to the exact routine) when den == 0, when
+// g(x).c1 == 0 (fp2_sqrt's special case) or if the root does not verify.
+BLS_HD bool map_to_curve_sswu_fast(const Fp2& u, Fp2& xo, Fp2& yo) {
+  const Fp2 A = c_sswu_a(), B = c_sswu_b(), Z = c_sswu_z();
+  Fp2 u2 = fp2_sqr(u);
+  Fp2 zu2 = fp2_mul(Z, u2);
+  Fp2 den = fp2_add(fp2_sqr(zu2), zu2);
+  if (fp2_is_zero(den)) return false;
+  Fp nd = fp_add(fp_sqr(den.c0), fp_sqr(den.c1));
+  Fp ndi = fp_inv_gcd(nd);
+  Fp2 deninv = Fp2{fp_mul(den.c0, ndi), fp_neg(fp_mul(den.c1, ndi))};
+  Fp2 x = fp2_mul(c_sswu_mb_over_a(), fp2_add(fp2_one(), deninv));
+  Fp2 gx = fp2_add(fp2_mul(fp2_add(fp2_sqr(x), A), x), B);
+  Fp n1 = fp_add(fp_sqr(gx.c0), fp_sqr(gx.c1));
+  Fp gamma = fp_pow_const<e_p_plus_1_div_4, E_P_PLUS_1_DIV_4_BITS>(n1);
+  if (!fp_eq(fp_sqr(gamma), n1)) {
+    x = fp2_mul(zu2, x);
+    gx = fp2_add(fp2_mul(fp2_add(fp2_sqr(x), A), x), B);
+    Fp nu = fp_add(fp_sqr(u.c0), fp_sqr(u.c1));
+    gamma = fp_mul(fp_mul(fp_mul(fp_sqr(nu), nu), c_sqrt_m125()), gamma);
+  }
+  if (fp_is_zero(gx.c1)) return false;
+  Fp d = fp_half(fp_add(gx.c0, gamma));
+  Fp t = fp_pow_const<e_p_minus_3_div_4, E_P_MINUS_3_DIV_4_BITS>(d);
+  Fp dt = fp_mul(d, t);
+  Fp a1t2 = fp_half(fp_mul(gx.c1, t));
+  Fp2 y = fp_eq(fp_sqr(dt), d) ? Fp2{dt, a1t2} : Fp2{a1t2, fp_neg(dt)};
+  if (!fp2_eq(fp2_sqr(y), gx)) return false;
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  xo = x;
+  yo = y;
+  return true;
+}
+
 // 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3), affine
 BLS_HD G2A iso_map_g2(const G2A& p) {
   const Fp2 x = p.x;

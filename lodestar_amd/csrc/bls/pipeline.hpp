@@ -8,10 +8,19 @@
 //   stage_sig         Signature.fromBytes(sig, affine, true)    (maybeBatch.ts:23,36)
 //   stage_h2c         hash_to_G2(signingRoot)                   ([ext] blst)
 //   stage_scale       r_i * pk_i, r_i * sig_i, 64-bit r_i       ([ext] verifyMultipleSignatures)
-//   stage_miller_set  f_i = ML(r_i pk_i, H(m_i))
+//   stage_pair_set    f_i = ML(r_i pk_i, H(m_i)) * ML(-g1, r_i sig_i)
 //   stage_req_status  per-request error precedence              (worker.ts:45, maybeBatch.ts:16-39)
-//   stage_chunk       prod f_i * ML(-g1, sum r_i sig_i) -> FE == 1 per chunk of >= 16 requests
+//   stage_chunk       FE(prod f_i) == 1 per chunk of >= 16 requests
 //   stage_indiv       the same per request (fallback / non-batchable, worker.ts:76-98)
+// The check prod e(r_i pk_i, H_i) * e(-g1, sum r_i sig_i) == 1 of the reference is
+// evaluated with the -g1 pairing split per set (bilinearity: identical verdict), so
+// every set's pairing work is independent and no cross-set point sum is needed.
+//
+// The GPU verify path (bls_gpu.hip) runs the per-set part as
+//   stage_pre (single lane: SSWU points, signature decoding)  ->  k_pset (one
+//   wavefront per set, kernels/k_pset.hip)  ->  stage_exact_set for the rare sets
+//   k_pset flags (exceptional point additions, infinity signatures);
+// the host harness runs the straight stages above, which compute the same values.
 #pragma once
 
 #include "../../../include/lodestar_bls.h"
@@ -46,6 +55,8 @@ struct PipeBufs {
   G2J* rsig;
   Fp12* f;
   int32_t* req_status;
+  Fp* q;               // n_sets * 8: the two SSWU points on E2' (x.c0, x.c1, y.c0, y.c1) per set
+  uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
   // outputs
   int32_t* chunk_ok;       // n_chunks: 1 ok, 0 failed (retry)
   int32_t* indiv_verdict;  // n_indiv: 1 / 0 / -code
@@ -134,13 +145,86 @@ BLS_HD void stage_scale(const PipeBufs& b, uint32_t i) {
   }
 }
 
-BLS_HD void stage_miller_set(const PipeBufs& b, uint32_t i) {
+BLS_HD G1Eval neg_g1_eval() {
+  G1Eval ng1;
+  ng1.xz = c_g1_x();
+  ng1.y = c_g1_negy();
+  ng1.z3 = c_one();
+  return ng1;
+}
+
+// f_i = ML(r pk, H) * ML(-g1, r sig) (1 when the set's request errors anyway)
+BLS_HD Fp12 pair_set(const G1J& rpk, const G2A& H, const G2J& rsig, bool sig_inf) {
+  Fp12 f = miller_loop(g1_eval_from_jac(rpk), H);
+  if (!sig_inf) f = fp12_mul(f, miller_loop(neg_g1_eval(), jac_to_aff(rsig)));
+  return f;
+}
+
+BLS_HD void stage_pair_set(const PipeBufs& b, uint32_t i) {
   if (i >= b.n_sets) return;
   if (b.pk_status[i] == BLS_OK && b.sig_status[i] == BLS_OK && !jac_is_inf(b.rpk[i])) {
-    b.f[i] = miller_loop(g1_eval_from_jac(b.rpk[i]), b.H[i]);
+    b.f[i] = pair_set(b.rpk[i], b.H[i], b.rsig[i], b.sig[i].inf);
   } else {
     b.f[i] = fp12_one();
   }
+}
+
+// GPU pre-stage, one lane per task t in [0, 3 n_sets):
+//   t < 2n:  SSWU point q_{t%2} of set t/2 (map_to_curve_sswu_fast; on its rare
+//            false return the set is flagged for the exact path)
+//   t >= 2n: decode signature t - 2n (on-curve, no subgroup test: k_pset does it)
+BLS_HD void stage_pre(const PipeBufs& b, uint32_t t) {
+  const uint32_t n = b.n_sets;
+  if (t < 2 * n) {
+    const uint32_t i = t >> 1;
+    uint32_t w[8];
+    msg_words_from_bytes(b.msgs + 32ull * i, w);
+    Fp2 u0, u1;
+    hash_to_field_fp2_x2(w, u0, u1);
+    Fp2 x, y;
+    Fp* q = b.q + 8ull * i + 4 * (t & 1);
+    if (map_to_curve_sswu_fast((t & 1) ? u1 : u0, x, y)) {
+      q[0] = x.c0;
+      q[1] = x.c1;
+      q[2] = y.c0;
+      q[3] = y.c1;
+    } else {
+      b.set_flag[i] = 1u;
+    }
+    return;
+  }
+  if (t >= 3 * n) return;
+  const uint32_t i = t - 2 * n;
+  G2A s;
+  s.inf = true;
+  s.x = fp2_zero();
+  s.y = fp2_zero();
+  int32_t code = (b.sig_lens && b.sig_lens[i] != 96) ? BLS_INVALID_SIZE : g2_decompress96(b.sigs + 96ull * i, s);
+  b.sig[i] = s;
+  b.sig_status[i] = code;
+}
+
+// Exact per-set path for sets k_pset flagged: subgroup test, H(m), r pk, r sig and
+// f_i with the complete (exception-handling) formulas of curve.hpp.
+BLS_HD void stage_exact_set(const PipeBufs& b, uint32_t i) {
+  if (i >= b.n_sets || !b.set_flag[i]) return;
+  if (b.pk_status[i] != BLS_OK || b.sig_status[i] != BLS_OK || jac_is_inf(b.pk[i])) {
+    b.f[i] = fp12_one();
+    return;
+  }
+  const G2A sig = b.sig[i];
+  if (!sig.inf && !g2_in_subgroup(sig)) {
+    b.sig_status[i] = BLS_POINT_NOT_IN_GROUP;
+    b.f[i] = fp12_one();
+    return;
+  }
+  uint32_t w[8];
+  msg_words_from_bytes(b.msgs + 32ull * i, w);
+  const G2A H = hash_to_g2(w);
+  const uint64_t r = set_scalar(b.seed, i);
+  const G1J rpk = jac_mul_u64(b.pk[i], r);
+  const G2J rsig = sig.inf ? jac_infinity<Fp2>() : aff_mul_u64(sig, r);
+  b.f[i] = pair_set(rpk, H, rsig, sig.inf);
 }
 
 // Error precedence per request (r): pk decode / aggregation errors (deserializeSet
@@ -168,17 +252,6 @@ BLS_HD void stage_req_status(const PipeBufs& b, uint32_t r) {
   b.req_status[r] = code;
 }
 
-// prod_{i in sets} f_i * ML(-g1, sum r_i sig_i), final exponentiation, == 1
-BLS_HD bool check_sets(const PipeBufs& b, Fp12 F, const G2J& S) {
-  G1Eval ng1;
-  ng1.xz = c_g1_x();
-  ng1.y = c_g1_negy();
-  ng1.z3 = c_one();
-  G2A Sa = jac_to_aff(S);
-  F = fp12_mul(F, miller_loop(ng1, Sa));
-  return fp12_is_one(final_exponentiation(F));
-}
-
 BLS_HD void stage_chunk(const PipeBufs& b, uint32_t c) {
   if (c >= b.n_chunks) return;
   uint32_t beg = b.chunk_off[c], end = b.chunk_off[c + 1];
@@ -189,15 +262,11 @@ BLS_HD void stage_chunk(const PipeBufs& b, uint32_t c) {
     }
   }
   Fp12 F = fp12_one();
-  G2J S = jac_infinity<Fp2>();
   for (uint32_t k = beg; k < end; ++k) {
     uint32_t r = b.chunk_reqs[k];
-    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) {
-      F = fp12_mul(F, b.f[i]);
-      S = jac_add(S, b.rsig[i]);
-    }
+    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) F = fp12_mul(F, b.f[i]);
   }
-  b.chunk_ok[c] = check_sets(b, F, S) ? 1 : 0;
+  b.chunk_ok[c] = fp12_is_one(final_exponentiation(F)) ? 1 : 0;
 }
 
 BLS_HD void stage_indiv(const PipeBufs& b, uint32_t t) {
@@ -209,12 +278,8 @@ BLS_HD void stage_indiv(const PipeBufs& b, uint32_t t) {
     return;
   }
   Fp12 F = fp12_one();
-  G2J S = jac_infinity<Fp2>();
-  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) {
-    F = fp12_mul(F, b.f[i]);
-    S = jac_add(S, b.rsig[i]);
-  }
-  b.indiv_verdict[t] = check_sets(b, F, S) ? 1 : 0;
+  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) F = fp12_mul(F, b.f[i]);
+  b.indiv_verdict[t] = fp12_is_one(final_exponentiation(F)) ? 1 : 0;
 }
 
 }  // namespace bls

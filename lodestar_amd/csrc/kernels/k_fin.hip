@@ -4,8 +4,8 @@
 //                 (worker.ts:56-88: random-scalar batch over the chunk's sets)
 //   k_indiv_coop  one task per request verified on its own
 //                 (failed chunks' requests and non-batchable requests, worker.ts:91-98)
-// Task: F = prod f_i, S = sum r_i sig_i (Jacobian, exceptional cases exact),
-//       F *= ML(-g1, S), verdict = (FE(F) == 1).
+// Task: F = prod f_i (each f_i already holds both pairings of its set, k_pset),
+//       verdict = (FE(F) == 1).
 #include "../launchers.hpp"
 #include "../bls/coop.hpp"
 
@@ -17,40 +17,17 @@ struct FinShared {
   uint32_t flag;
 };
 
-__device__ __forceinline__ bool g2j_is_inf_global(const G2J& p) { return fp2_is_zero(p.z); }
-
-__device__ void fin_accumulate_set(const PipeBufs& b, const CoopEnv& env, FinShared& sh, uint32_t i, bool& s_inf) {
-  coop_load(sh.frame, FIN_G, reinterpret_cast<const Fp*>(&b.f[i]), 12);
-  coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
-  const G2J& rs = b.rsig[i];
-  if (g2j_is_inf_global(rs)) return;
-  if (s_inf) {
-    coop_load(sh.frame, FIN_S, reinterpret_cast<const Fp*>(&rs), 6);
-    s_inf = false;
+__device__ void fin_accumulate_set(const PipeBufs& b, const CoopEnv& env, FinShared& sh, uint32_t i, bool& first) {
+  if (first) {
+    coop_load(sh.frame, FIN_F, reinterpret_cast<const Fp*>(&b.f[i]), 12);
+    first = false;
     return;
   }
-  coop_load(sh.frame, FIN_R, reinterpret_cast<const Fp*>(&rs), 6);
-  if (threadIdx.x == 0) sh.flag = 0;
-  __syncthreads();
-  coop_run(env, env.fin_g2add, sh.frame, sh.cbank, &sh.flag);
-  if (sh.flag) {  // H may be zero: exact test (S == R -> doubling, S == -R -> infinity)
-    if (coop_is_zero(sh.frame, FIN_HR, 2)) {
-      if (coop_is_zero(sh.frame, FIN_HR + 2, 2)) {
-        coop_run(env, env.fin_g2dbl, sh.frame, sh.cbank, &sh.flag);
-      } else {
-        s_inf = true;
-      }
-    }
-  }
+  coop_load(sh.frame, FIN_G, reinterpret_cast<const Fp*>(&b.f[i]), 12);
+  coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
 }
 
-__device__ bool fin_finish(const CoopEnv& env, FinShared& sh, bool s_inf) {
-  if (!s_inf) {
-    coop_run(env, env.fin_normz, sh.frame, sh.cbank, &sh.flag);
-    coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
-    coop_run(env, env.fin_affine, sh.frame, sh.cbank, &sh.flag);
-    coop_run(env, env.fin_ml_neg_g1, sh.frame, sh.cbank, &sh.flag);
-  }
+__device__ bool fin_finish(const CoopEnv& env, FinShared& sh) {
   coop_run(env, env.fin_fe1, sh.frame, sh.cbank, &sh.flag);
   coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
   coop_run(env, env.fin_fe2, sh.frame, sh.cbank, &sh.flag);
@@ -77,12 +54,12 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv e
     }
   }
   fin_init(env, sh);
-  bool s_inf = true;
+  bool first = true;
   for (uint32_t k = beg; k < end; ++k) {
     const uint32_t r = b.chunk_reqs[k];
-    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, s_inf);
+    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, first);
   }
-  bool ok = fin_finish(env, sh, s_inf);
+  bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.chunk_ok[c] = ok ? 1 : 0;
 }
 
@@ -96,9 +73,9 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
     return;
   }
   fin_init(env, sh);
-  bool s_inf = true;
-  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, s_inf);
-  bool ok = fin_finish(env, sh, s_inf);
+  bool first = true;
+  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, first);
+  bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.indiv_verdict[t] = ok ? 1 : 0;
 }
 

@@ -1,0 +1,14 @@
+// Single-lane pre-stage of the verify path (pipeline.hpp stage_pre): for every set
+// the two SSWU points on E2' (expand_message_xmd + hash_to_field + SSWU, two Fp
+// exponentiations each) and the signature decompression.  Lanes [0, 2n) map,
+// lanes [2n, 3n) decode, so each wavefront runs one kind of work.
+#include "../launchers.hpp"
+
+using namespace bls;
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_pre(PipeBufs b) { stage_pre(b, blockIdx.x * BLS_BLOCK + threadIdx.x); }
+
+hipError_t launch_k_pre(const PipeBufs& b, hipStream_t s) {
+  k_pre<<<bls_grid_for(3 * b.n_sets), BLS_BLOCK, 0, s>>>(b);
+  return hipGetLastError();
+}

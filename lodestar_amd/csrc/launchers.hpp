@@ -15,10 +15,9 @@ hipError_t launch_k_aggregate(const bls::PipeBufs& b, uint8_t* out96, hipStream_
 hipError_t launch_k_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, bls::G1A* out, int32_t* codes,
                                  hipStream_t s);
 hipError_t launch_k_status(const bls::PipeBufs& b, hipStream_t s);
-hipError_t launch_k_sig(const bls::PipeBufs& b, hipStream_t s);
-hipError_t launch_k_h2c(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_pre(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_exact(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_hash_to_g2(const uint8_t* msgs, uint32_t n, uint8_t* out192, hipStream_t s);
-hipError_t launch_k_scale(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_sk_to_pk(const uint8_t* sks, uint32_t n, uint8_t* out48, hipStream_t s);
 hipError_t launch_k_sign(const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t s);
 hipError_t launch_k_mad_peak(uint64_t* out, uint32_t blocks, uint32_t iters, hipStream_t s);
@@ -29,4 +28,4 @@ hipError_t launch_k_chunk_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, 
 hipError_t launch_k_indiv_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_coop_probe(const bls::CoopEnv& env, bls::CoopProg pg, uint32_t blocks, uint32_t reps,
                                uint32_t* sink, uint64_t* stamps, hipStream_t s);
-hipError_t launch_k_miller_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
+hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);

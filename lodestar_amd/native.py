@@ -195,6 +195,9 @@ class GpuContext:
         self._check(self.lib.bls_gpu_sk_to_pk(self._h, _ptr(s), n, _ptr(out)), "bls_gpu_sk_to_pk")
         return out[: 48 * n].reshape(n, 48)
 
+    def set_debug_flags(self, flags: int) -> None:
+        self._check(self.lib.bls_gpu_set_debug_flags(self._h, flags), "bls_gpu_set_debug_flags")
+
     def mad_peak(self) -> tuple[float, float]:
         """Measured v_mad_u64_u32 rate (MAD/s) and the probe's duration (ms)."""
         rate, ms = ctypes.c_double(), ctypes.c_double()

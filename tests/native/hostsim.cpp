@@ -78,6 +78,7 @@ void hs_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_add(
 void hs_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_sub(rd_fp(a), rd_fp(b)), out); }
 void hs_fp_half(const uint8_t* a, uint8_t* out) { wr_fp(fp_half(rd_fp(a)), out); }
 void hs_fp_inv(const uint8_t* a, uint8_t* out) { wr_fp(fp_inv(rd_fp(a)), out); }
+void hs_fp_inv_gcd(const uint8_t* a, uint8_t* out) { wr_fp(fp_inv_gcd(rd_fp(a)), out); }
 int hs_fp_sqrt(const uint8_t* a, uint8_t* out) {
   Fp r;
   bool ok = fp_sqrt(rd_fp(a), r);
@@ -134,6 +135,13 @@ void hs_map_to_curve_sswu(const uint8_t* u96, uint8_t* out192) {
   G2A r = map_to_curve_sswu(rd_fp2(u96));
   wr_fp2(r.x, out192);
   wr_fp2(r.y, out192 + 96);
+}
+int hs_map_to_curve_sswu_fast(const uint8_t* u96, uint8_t* out192) {
+  Fp2 x, y;
+  if (!map_to_curve_sswu_fast(rd_fp2(u96), x, y)) return 0;
+  wr_fp2(x, out192);
+  wr_fp2(y, out192 + 96);
+  return 1;
 }
 void hs_hash_to_field(const uint8_t* msg32, uint8_t* out384) {
   uint32_t w[8];
@@ -291,7 +299,7 @@ int hs_verify_batch(const bls_batch* in, int32_t* verdicts, bls_stats* stats) {
   mark(2);
   for (uint32_t i = 0; i < n; ++i) stage_scale(b, i);
   mark(3);
-  for (uint32_t i = 0; i < n; ++i) stage_miller_set(b, i);
+  for (uint32_t i = 0; i < n; ++i) stage_pair_set(b, i);
   mark(4);
   for (uint32_t r = 0; r < R; ++r) stage_req_status(b, r);
   for (uint32_t c = 0; c < n_chunks; ++c) stage_chunk(b, c);

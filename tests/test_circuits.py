@@ -58,77 +58,15 @@ def test_fin_fmul(progs, oracle):
     assert get12(fr, GC.F) == oracle.f12_mul(a, b)
 
 
-def test_fin_g2add_and_affine(progs, oracle):
-    pg, consts = progs
-    rng = random.Random(2)
-    p1 = oracle.E2.mul(oracle.G2, rng.randrange(1, 1 << 64))
-    p2 = oracle.E2.mul(oracle.G2, rng.randrange(1, 1 << 64))
-    fr = [0] * GC.FRAME
-    z1 = (rng.randrange(P), rng.randrange(P))
-    z2 = (rng.randrange(P), rng.randrange(P))
-    for base, pt, z in ((GC.S, p1, z1), (GC.R, p2, z2)):
-        X, Y, Z = to_jac(pt, z)
-        fr[base:base + 6] = [X[0], X[1], Y[0], Y[1], Z[0], Z[1]]
-    flag = simulate(pg["fin_g2add"], fr, consts)
-    assert not flag
-    simulate(pg["fin_normz"], fr, consts)
-    fr[GC.INV_OUT] = pow(fr[GC.INV_IN], P - 2, P)
-    simulate(pg["fin_affine"], fr, consts)
-    assert ((fr[GC.Q], fr[GC.Q + 1]), (fr[GC.Q + 2], fr[GC.Q + 3])) == oracle.E2.add(p1, p2)
-    # H == 0 (P + P) raises the zero-check flag
-    X, Y, Z = to_jac(p1, z1)
-    fr[GC.S:GC.S + 6] = [X[0], X[1], Y[0], Y[1], Z[0], Z[1]]
-    X, Y, Z = to_jac(p1, z2)
-    fr[GC.R:GC.R + 6] = [X[0], X[1], Y[0], Y[1], Z[0], Z[1]]
-    assert simulate(pg["fin_g2add"], fr, consts)
-
-
-def test_fin_ml_and_final_exponentiation(progs, oracle):
+def test_fin_final_exponentiation(progs, oracle):
     pg, consts = progs
     rng = random.Random(3)
     q = oracle.E2.mul(oracle.G2, rng.randrange(1, 1 << 64))
-    f0 = rand12(rng)
+    pp = oracle.E1.mul(oracle.G1, rng.randrange(1, 1 << 64))
+    f0 = oracle.f12_mul(rand12(rng), oracle.miller_loop(pp, q))
     fr = [0] * GC.FRAME
     put12(fr, GC.F, f0)
-    fr[GC.Q:GC.Q + 4] = [q[0][0], q[0][1], q[1][0], q[1][1]]
-    simulate(pg["fin_ml_neg_g1"], fr, consts)
-    got_ml = get12(fr, GC.F)
     simulate(pg["fin_fe1"], fr, consts)
     fr[GC.INV_OUT] = pow(fr[GC.INV_IN], P - 2, P)
     simulate(pg["fin_fe2"], fr, consts)
-    got = get12(fr, GC.F)
-    want = oracle.final_exponentiation(oracle.f12_mul(f0, oracle.miller_loop(oracle.E1.neg(oracle.G1), q)),
-                                       hard_multiple=3)
-    assert got == want
-    # the program's FE alone equals the oracle's FE (x3) on the Miller output
-    assert oracle.final_exponentiation(got_ml, hard_multiple=3) == want
-
-
-def test_fin_g2dbl(progs, oracle):
-    pg, consts = progs
-    rng = random.Random(4)
-    p1 = oracle.E2.mul(oracle.G2, rng.randrange(1, 1 << 64))
-    fr = [0] * GC.FRAME
-    X, Y, Z = to_jac(p1, (rng.randrange(P), rng.randrange(P)))
-    fr[GC.R:GC.R + 6] = [X[0], X[1], Y[0], Y[1], Z[0], Z[1]]
-    simulate(pg["fin_g2dbl"], fr, consts)
-    simulate(pg["fin_normz"], fr, consts)
-    fr[GC.INV_OUT] = pow(fr[GC.INV_IN], P - 2, P)
-    simulate(pg["fin_affine"], fr, consts)
-    assert ((fr[GC.Q], fr[GC.Q + 1]), (fr[GC.Q + 2], fr[GC.Q + 3])) == oracle.E2.dbl(p1)
-
-
-def test_set_ml_jacobian_p(progs, oracle):
-    """Per-set Miller loop with the G1 point in Jacobian form (line scaled by Z^3)."""
-    pg, consts = progs
-    rng = random.Random(5)
-    q = oracle.E2.mul(oracle.G2, rng.randrange(1, 1 << 64))
-    pp = oracle.E1.mul(oracle.G1, rng.randrange(1, 1 << 64))
-    z = rng.randrange(1, P)
-    fr = [0] * GC.FRAME
-    fr[GC.SQ:GC.SQ + 4] = [q[0][0], q[0][1], q[1][0], q[1][1]]
-    fr[GC.SP:GC.SP + 3] = [pp[0] * z * z % P, pp[1] * z * z * z % P, z]
-    simulate(pg["set_ml"], fr, consts)
-    got = get12(fr, GC.SF)
-    want = oracle.miller_loop(pp, q)
-    assert oracle.final_exponentiation(got, 3) == oracle.final_exponentiation(want, 3)
+    assert get12(fr, GC.F) == oracle.final_exponentiation(f0, hard_multiple=3)

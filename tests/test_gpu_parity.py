@@ -224,3 +224,23 @@ def test_fp_mul_device_vs_bigint(gpu):
     out = gpu.fp_mul_test(b"".join(x.to_bytes(48, "big") for x in a), b"".join(x.to_bytes(48, "big") for x in b))
     got = [int.from_bytes(out[48 * i: 48 * i + 48], "big") for i in range(len(a))]
     assert got == [(x * y) % P for x, y in zip(a, b)]
+
+
+@pytest.mark.gpu
+def test_exact_path_matches_cooperative_path(gpu, oracle, golden, table):
+    """The same calls with every set forced through k_exact (complete single-lane
+    formulas) give the verdicts of the cooperative k_pset path."""
+    sets = _sets(gpu, oracle, 4, tag=b"exact")
+    reqs = [(True, [s]) for s in sets] + [(False, sets)]
+    reqs.append((True, [(sets[0][0], _h(b"other"), sets[0][2])]))          # wrong message
+    for case in golden["sig_decode"]:                                       # decode / subgroup codes
+        reqs.append((False, [(sets[0][0], sets[0][1], bytes.fromhex(case["bytes"]))]))
+    pb = pack_requests(reqs)
+    v0, _ = gpu.verify_packed(pb)
+    try:
+        gpu.set_debug_flags(1)
+        v1, _ = gpu.verify_packed(pb)
+    finally:
+        gpu.set_debug_flags(0)
+    assert list(v0) == list(v1)
+    assert list(v0[:5]) == [1] * 5 and v0[5] == 0

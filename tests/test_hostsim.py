@@ -29,6 +29,43 @@ def test_fp_ops(hostsim):
     assert fp(o.raw) * 12345 % P == 1
 
 
+def test_fp_inv_gcd(hostsim):
+    rng = random.Random(7)
+    o = _buf(48)
+    for a in [1, 2, P - 1, P - 2, 3] + [rng.randrange(1, P) for _ in range(50)]:
+        hostsim.hs_fp_inv_gcd(b48(a), o)
+        assert fp(o.raw) * a % P == 1
+    hostsim.hs_fp_inv_gcd(b48(0), o)
+    assert fp(o.raw) == 0
+
+
+def test_sswu_fast_matches_oracle(hostsim, oracle):
+    """map_to_curve_sswu_fast (norm-based branch choice, one Legendre exponentiation)
+    equals RFC 9380's map on both branches."""
+    rng = random.Random(8)
+    o = _buf(192)
+    branches = set()
+    for k in range(40):
+        u = (rng.randrange(P), rng.randrange(P))
+        assert hostsim.hs_map_to_curve_sswu_fast(f2b(u), o) == 1
+        want = oracle.map_to_curve_sswu(u)
+        assert (bf2(o.raw[:96]), bf2(o.raw[96:])) == want
+        gx1_square = oracle.f2_is_square(_gx1(oracle, u))
+        branches.add(gx1_square)
+    assert branches == {True, False}
+    # u = 0: den == 0 -> exact-path fallback
+    assert hostsim.hs_map_to_curve_sswu_fast(f2b((0, 0)), o) == 0
+
+
+def _gx1(oracle, u):
+    Z = oracle.Z_SSWU
+    zu2 = oracle.f2_mul(Z, oracle.f2_mul(u, u))
+    den = oracle.f2_add(oracle.f2_mul(zu2, zu2), zu2)
+    mba = oracle.f2_mul(oracle.f2_neg(oracle.B_ISO), oracle.f2_inv(oracle.A_ISO))
+    x1 = oracle.f2_mul(mba, oracle.f2_add(oracle.F2_ONE, oracle.f2_inv(den)))
+    return oracle.f2_add(oracle.f2_mul(oracle.f2_add(oracle.f2_mul(x1, x1), oracle.A_ISO), x1), oracle.B_ISO)
+
+
 def test_fp2_sqrt(hostsim, oracle):
     rng = random.Random(2)
     o = _buf(96)

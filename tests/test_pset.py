@@ -1,0 +1,79 @@
+"""Per-set cooperative programs (tools/gen_pset.py) over the step simulator, against
+the oracle: H(m) = hash_to_G2 from the two SSWU points, the G2 subgroup test,
+r*sig / r*pk and f_i = ML(r pk, H) ML(-g1, r sig).  CPU only."""
+from __future__ import annotations
+
+import random
+import sys
+from pathlib import Path
+
+import pytest
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "tools"))
+import gen_coop as GC  # noqa: E402
+import gen_pset as PS  # noqa: E402
+from circuits import P, simulate  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def progs():
+    progs, consts = GC.build_all()
+    return {p.name: p for p in progs}, consts
+
+
+def _frame_for(oracle, msg, sig_pt, pk_pt, zpk):
+    u0, u1 = oracle.hash_to_field_fp2(msg, 2, oracle.DST_POP)
+    q0 = oracle.map_to_curve_sswu(u0)
+    q1 = oracle.map_to_curve_sswu(u1)
+    fr = [0] * GC.FRAME
+    fr[PS.Q0:PS.Q0 + 4] = [q0[0][0], q0[0][1], q0[1][0], q0[1][1]]
+    fr[PS.Q1:PS.Q1 + 4] = [q1[0][0], q1[0][1], q1[1][0], q1[1][1]]
+    fr[PS.SIG:PS.SIG + 4] = [sig_pt[0][0], sig_pt[0][1], sig_pt[1][0], sig_pt[1][1]]
+    fr[PS.PK:PS.PK + 3] = [pk_pt[0] * zpk * zpk % P, pk_pt[1] * zpk ** 3 % P, zpk]
+    return fr
+
+
+def _inv(v):
+    return pow(v, P - 2, P) if v else 0
+
+
+def test_pset_valid_set(progs, oracle):
+    pg, consts = progs
+    rng = random.Random(11)
+    sk = rng.randrange(1, oracle.R)
+    msg = bytes(rng.randrange(256) for _ in range(32))
+    sig = oracle.E2.mul(oracle.hash_to_g2(msg), sk)
+    pk = oracle.E1.mul(oracle.G1, sk)
+    r = rng.randrange(1, 1 << 64)
+    fr = _frame_for(oracle, msg, sig, pk, rng.randrange(1, P))
+    flag, in_group = PS.run_pset(pg, consts, fr, r, simulate, _inv)
+    assert not flag and in_group
+    H = oracle.hash_to_g2(msg)
+    assert ((fr[PS.HQ], fr[PS.HQ + 1]), (fr[PS.HQ + 2], fr[PS.HQ + 3])) == H
+    assert ((fr[PS.RSQ], fr[PS.RSQ + 1]), (fr[PS.RSQ + 2], fr[PS.RSQ + 3])) == oracle.E2.mul(sig, r)
+    X, Y, Z = fr[PS.RP:PS.RP + 3]
+    zi = _inv(Z)
+    assert (X * zi * zi % P, Y * zi ** 3 % P) == oracle.E1.mul(pk, r)
+    f = [(fr[PS.F + 6 * (w % 2) + 2 * (w // 2)], fr[PS.F + 6 * (w % 2) + 2 * (w // 2) + 1]) for w in range(6)]
+    assert oracle.f12_is_one(oracle.final_exponentiation(f, hard_multiple=3))
+
+
+def test_pset_wrong_message_and_non_subgroup(progs, oracle):
+    pg, consts = progs
+    rng = random.Random(12)
+    sk = rng.randrange(1, oracle.R)
+    msg = bytes(rng.randrange(256) for _ in range(32))
+    sig = oracle.E2.mul(oracle.hash_to_g2(b"\x01" * 32), sk)   # signs another message
+    pk = oracle.E1.mul(oracle.G1, sk)
+    fr = _frame_for(oracle, msg, sig, pk, 1)
+    flag, in_group = PS.run_pset(pg, consts, fr, rng.randrange(1, 1 << 64), simulate, _inv)
+    assert not flag and in_group
+    f = [(fr[PS.F + 6 * (w % 2) + 2 * (w // 2)], fr[PS.F + 6 * (w % 2) + 2 * (w // 2) + 1]) for w in range(6)]
+    assert not oracle.f12_is_one(oracle.final_exponentiation(f, hard_multiple=3))
+    # a point of E2 outside G2 (the SSWU image before cofactor clearing)
+    u0, _ = oracle.hash_to_field_fp2(b"x" * 32, 2, oracle.DST_POP)
+    off = oracle.iso_map(oracle.map_to_curve_sswu(u0))
+    assert not oracle.g2_in_subgroup(off)
+    fr = _frame_for(oracle, msg, off, pk, 1)
+    flag, in_group = PS.run_pset(pg, consts, fr, 5, simulate, _inv)
+    assert not in_group

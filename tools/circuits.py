@@ -159,6 +159,83 @@ def _refs(l: Lin):
 
 def schedule(c: Circuit, frame_slots: int, reserved: set, lanes: int = LANES) -> Program:
     """Level-schedule circuit `c` into steps of <= `lanes` ops over a frame of
+    `frame_slots` slots; `reserved` slots (the caller's live registers) are never
+    used for temporaries.  Both as-soon-as-possible and as-late-as-possible level
+    assignments are tried (ALAP keeps values that are consumed late -- e.g. a Miller
+    loop's line coefficients -- out of the frame until they are needed); the shorter
+    program that fits the frame wins."""
+    import copy
+    best, err = None, None
+    for mode in ("asap", "alap", "list"):
+        try:
+            pg = _schedule_mode(copy.deepcopy(c), frame_slots, reserved, lanes, mode)
+        except RuntimeError as e:
+            err = e
+            continue
+        if best is None or len(pg.steps) < len(best.steps):
+            best = pg
+    if best is None:
+        raise err
+    return best
+
+
+def _relevel(nodes, roots, mode):
+    """Drop dead nodes; recompute levels (ASAP or ALAP) and LIN depths in a
+    topological order."""
+    byid = {n.id: n for n in nodes}
+    order, seen = [], set()
+    stack = [r[1] for l in roots for r in _refs(l)]
+    # iterative post-order DFS
+    for root in list(dict.fromkeys(stack)):
+        if root in seen:
+            continue
+        work = [(root, False)]
+        while work:
+            nid, done = work.pop()
+            if done:
+                order.append(byid[nid])
+                continue
+            if nid in seen:
+                continue
+            seen.add(nid)
+            work.append((nid, True))
+            n = byid[nid]
+            for l in (n.a, n.b):
+                for r in _refs(l):
+                    if r[1] not in seen:
+                        work.append((r[1], False))
+    # ASAP
+    for n in order:
+        lv = 0
+        for l in (n.a, n.b):
+            for r in _refs(l):
+                lv = max(lv, byid[r[1]].level)
+        n.level = lv + 1 if n.kind == OP_MUL else lv
+    if mode in ("alap", "list"):
+        lmax = max((n.level for n in order), default=0)
+        cons = {n.id: [] for n in order}
+        for n in order:
+            for l in (n.a, n.b):
+                for r in _refs(l):
+                    cons[r[1]].append(n)
+        for n in reversed(order):
+            lat = lmax
+            for cn in cons[n.id]:
+                lat = min(lat, cn.level - 1 if cn.kind == OP_MUL else cn.level)
+            n.level = lat
+    for n in order:
+        d = 0
+        if n.kind == OP_LIN:
+            for r in _refs(n.a):
+                m = byid[r[1]]
+                if m.kind == OP_LIN and m.level == n.level:
+                    d = max(d, m.depth + 1)
+        n.depth = d
+    return order
+
+
+def _schedule_mode(c: Circuit, frame_slots: int, reserved: set, lanes: int, mode: str) -> Program:
+    """Level-schedule circuit `c` into steps of <= `lanes` ops over a frame of
     `frame_slots` slots.  `reserved` slots (the caller's live registers) are never
     used for temporaries.  Products of level L run in phase (L, 0); linear
     combinations whose deepest reference has level L run in phases (L, 1, depth)."""
@@ -208,26 +285,78 @@ def schedule(c: Circuit, frame_slots: int, reserved: set, lanes: int = LANES) ->
         i += 1
     outs = [(slot, fit(v)) for slot, v in c.outputs]
     zchecks = [fit(z) for z in c.zchecks]
+    nodes = _relevel(nodes, [v for _, v in outs] + zchecks, mode)
 
-    def phase(n: Node):
-        return (n.level, 0, 0) if n.kind == OP_MUL else (n.level, 1, n.depth)
+    if mode == "list":
+        groups = _list_groups(nodes, lanes)
+    else:
+        def phase(n: Node):
+            return (n.level, 0, 0) if n.kind == OP_MUL else (n.level, 1, n.depth)
 
-    phases: dict = {}
-    for n in nodes:
-        phases.setdefault(phase(n), []).append(n)
-    order = sorted(phases)
-    rank = {ph: k for k, ph in enumerate(order)}
-    tail_rank = len(order)
+        phases: dict = {}
+        for n in nodes:
+            phases.setdefault(phase(n), []).append(n)
+        groups = []
+        for ph in sorted(phases):
+            ns = phases[ph]
+            for k in range(0, len(ns), lanes):
+                groups.append((ph[1] == 0, ns[k: k + lanes]))
+    return _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes)
+
+
+def _list_groups(nodes, lanes):
+    """Slack-driven list scheduling.  Walk the ALAP levels; at each product level
+    run every product whose ALAP level it is (mandatory) and fill the spare lanes
+    of the last step with ready products that have slack (earliest deadline first);
+    then run linear-combination steps until every combination due at this level is
+    done, again filling spare lanes with ready ones."""
+    byid = {n.id: n for n in nodes}
+    done = set()
+    todo_mul = [n for n in nodes if n.kind == OP_MUL]
+    todo_lin = [n for n in nodes if n.kind == OP_LIN]
+    groups = []
+
+    def ready(n):
+        return all(r[1] in done for l in (n.a, n.b) for r in _refs(l))
+
+    def run(kind_mul, pool, level):
+        rdy = [n for n in pool if ready(n)]
+        must = [n for n in rdy if n.level <= level]
+        if not must:
+            return pool, False
+        opt = sorted((n for n in rdy if n.level > level), key=lambda n: n.level)
+        nsteps = (len(must) + lanes - 1) // lanes
+        take = must + opt[: nsteps * lanes - len(must)]
+        for k in range(0, len(take), lanes):
+            groups.append((kind_mul, take[k: k + lanes]))
+        ids = {n.id for n in take}
+        done.update(ids)
+        return [n for n in pool if n.id not in ids], True
+
+    lmax = max((n.level for n in nodes), default=0)
+    for level in range(0, lmax + 1):
+        if level > 0:
+            todo_mul, _ = run(True, todo_mul, level)
+        while True:
+            todo_lin, progressed = run(False, todo_lin, level)
+            if not progressed:
+                break
+    assert not todo_mul and not todo_lin, "list scheduling left nodes behind"
+    return groups
+
+
+def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes) -> Program:
     last_use = {}
+    tail_rank = len(groups)
 
     def note(l: Lin, r):
         for x in _refs(l):
             last_use[x[1]] = max(last_use.get(x[1], -1), r)
 
-    for ph, ns in phases.items():
+    for r, (_, ns) in enumerate(groups):
         for n in ns:
-            note(n.a, rank[ph])
-            note(n.b, rank[ph])
+            note(n.a, r)
+            note(n.b, r)
     for _, v in outs:
         note(v, tail_rank)
     for z in zchecks:
@@ -238,26 +367,23 @@ def schedule(c: Circuit, frame_slots: int, reserved: set, lanes: int = LANES) ->
     busy_until = {}
     steps = []
     n_mul = 0
-    for ph in order:
-        r = rank[ph]
+    for r, (is_mul, ns) in enumerate(groups):
         for s, until in list(busy_until.items()):
             if until < r:
                 del busy_until[s]
                 free.append(s)
         free.sort()
-        ns = phases[ph]
-        for k in range(0, len(ns), lanes):
-            ops = []
-            for n in ns[k: k + lanes]:
-                if not free:
-                    raise RuntimeError(f"{c.name}: out of frame slots ({frame_slots})")
-                s = free.pop(0)
-                slot_of[n.id] = s
-                busy_until[s] = last_use.get(n.id, r)
-                ops.append(Op(n.kind, s, _emit(n.a, slot_of), _emit(n.b, slot_of)))
-            steps.append(ops)
-            if ph[1] == 0:
-                n_mul += 1
+        ops = []
+        for n in ns:
+            if not free:
+                raise RuntimeError(f"{c.name}: out of frame slots ({frame_slots})")
+            s = free.pop(0)
+            slot_of[n.id] = s
+            busy_until[s] = last_use.get(n.id, r)
+            ops.append(Op(n.kind, s, _emit(n.a, slot_of), _emit(n.b, slot_of)))
+        steps.append(ops)
+        if is_mul:
+            n_mul += 1
     tail = [Op(OP_LIN, slot, _emit(v, slot_of)) for slot, v in outs]
     tail += [Op(OP_LIN, ZCHECK, _emit(z, slot_of)) for z in zchecks]
     for k in range(0, len(tail), lanes):

@@ -17,13 +17,14 @@ progs, _ = gen_coop.build_all()
 kinds = {p.name: [any(op.kind == 1 for op in st) for st in p.steps] for p in progs}
 with GpuContext(0) as g:
     out = {}
-    for name, reps in (("fin_fmul", 200), ("fin_g2add", 100), ("set_ml", 3), ("fin_fe2", 2)):
+    for name, reps in (("fin_fmul", 200), ("pset_dbl_all", 100), ("pset_add_xr", 100), ("pset_phase2", 3),
+                       ("pset_ml2", 3), ("fin_fe2", 2)):
         for blocks in (1, 64, 1024):
             us, ms = g.coop_probe(name, blocks, reps)
             out[f"{name}@{blocks}"] = {"us_per_step": round(us, 3), "ms_per_run": round(ms / reps, 3)}
         k = kinds[name]
         _, _, st = g.coop_probe(name, 1, 1, len(k) + 1)
-        d = np.diff(st.astype(np.int64))  # s_memtime ticks (100 MHz constant clock on gfx9)
+        d = np.diff(st.astype(np.int64))  # s_memtime: shader-clock cycles
         mul = d[np.array(k)]
         lin = d[~np.array(k)]
         out[f"{name}:stamps"] = {"mul_steps": int(len(mul)), "mul_ticks_mean": float(mul.mean()) if len(mul) else 0,

@@ -9,10 +9,10 @@ structs in field.hpp / curve.hpp so global <-> LDS copies are straight):
 
   "fin" frame (chunk / per-request finalisation, k_fin_coop):
     F  0..11   Fp12 accumulator          G  12..23  Fp12 operand (f_i)
-    S  24..29  G2 Jacobian sum           R  30..35  G2 Jacobian operand (r_i sig_i)
-    Q  36..39  G2 affine                 40 INV_IN, 41 INV_OUT (lane-0 inversion)
-    E  42..49  saved easy-part values    HR 50..53  H, S2 - S1 of the last G2 addition
+    40 INV_IN, 41 INV_OUT (lane-0 inversion)   E 42..49  saved easy-part values
     temporaries 54..FRAME-1
+
+  "pset" frame: see tools/gen_pset.py.
 
     python tools/gen_coop.py   (run by lodestar_amd/build.py)
 """
@@ -37,8 +37,6 @@ INV_IN, INV_OUT = 40, 41
 E = 42
 HR = 50   # H (2 slots) and S2 - S1 (2 slots) of the last G2 addition
 
-# "set" frame registers
-SQ, SP, SF = 0, 4, 8
 
 
 # ----------------------------------------------------------------------------
@@ -376,49 +374,6 @@ def build_fin(consts: ConstBank) -> list[Program]:
     out12(c, F, t.mul12(t.f12(F), t.f12(G)))
     progs.append(schedule(c, FRAME, fin_regs))
 
-    # S = S + R (Jacobian)
-    c = Circuit("fin_g2add", consts)
-    t = T(c)
-    x3, y3, z3 = g2_add_jac(t, t.f2(S), t.f2(S + 2), t.f2(S + 4), t.f2(R), t.f2(R + 2), t.f2(R + 4),
-                            hr_out=HR)
-    out2(c, S, x3)
-    out2(c, S + 2, y3)
-    out2(c, S + 4, z3)
-    progs.append(schedule(c, FRAME, fin_regs))
-
-    # S = 2 R (exceptional case of the addition: S == R)
-    c = Circuit("fin_g2dbl", consts)
-    t = T(c)
-    x3, y3, z3 = g2_dbl_jac(t, t.f2(R), t.f2(R + 2), t.f2(R + 4))
-    out2(c, S, x3)
-    out2(c, S + 2, y3)
-    out2(c, S + 4, z3)
-    progs.append(schedule(c, FRAME, fin_regs))
-
-    # INV_IN = norm(S.z)
-    c = Circuit("fin_normz", consts)
-    z = (Circuit.inp(S + 4), Circuit.inp(S + 5))
-    c.out(INV_IN, c.mul(z[0], z[0]) + c.mul(z[1], z[1]))
-    progs.append(schedule(c, FRAME, fin_regs))
-
-    # Q = affine(S) given INV_OUT = 1 / norm(S.z)
-    c = Circuit("fin_affine", consts)
-    t = T(c)
-    w = Circuit.inp(INV_OUT)
-    zi = (c.mul(Circuit.inp(S + 4), w), -c.mul(Circuit.inp(S + 5), w))
-    zi2 = t.sqr2(zi)
-    zi3 = t.mul2(zi2, zi)
-    out2(c, Q, t.mul2(t.f2(S), zi2))
-    out2(c, Q + 2, t.mul2(t.f2(S + 2), zi3))
-    progs.append(schedule(c, FRAME, fin_regs))
-
-    # F = F * ML(-g1, Q)
-    c = Circuit("fin_ml_neg_g1", consts)
-    t = T(c)
-    ml = miller_loop(t, t.f2(Q), t.f2(Q + 2), c.const(G1X), c.const(-G1Y), None)
-    out12(c, F, t.mul12(t.f12(F), ml))
-    progs.append(schedule(c, FRAME, fin_regs))
-
     # FE part 1: norms down to Fp (Fp12 -> Fp6 -> Fp2 -> Fp)
     c = Circuit("fin_fe1", consts)
     t = T(c)
@@ -497,27 +452,20 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
     path.write_bytes(header + cbin + bytes(table) + bytes(steps_bin))
 
 
-def build_set(consts: ConstBank) -> list[Program]:
-    """Per-set programs ("set" frame):
-         SQ 0..3   H(m) affine (G2)           SP 4..6   r*pk Jacobian (G1)
-         SF 8..19  Miller-loop output f_i     temporaries 24..FRAME-1"""
-    progs = []
-    regs = set(range(0, 24))
-    c = Circuit("set_ml", consts)
-    t = T(c)
-    X, Y, Z = (Circuit.inp(SP + k) for k in range(3))
-    z2 = c.mul(Z, Z)
-    pz3 = c.mat(c.mul(z2, Z))
-    pxz = c.mat(c.mul(X, Z))
-    ml = miller_loop(t, t.f2(SQ), t.f2(SQ + 2), pxz, Y, pz3)
-    out12(c, SF, ml)
-    progs.append(schedule(c, FRAME, regs))
-    return progs
+def _curve_constants():
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        import gen_constants as gc
+    return (gc.PSI_X, gc.PSI_Y), (gc.ISO_XNUM, gc.ISO_XDEN, gc.ISO_YNUM, gc.ISO_YDEN)
 
 
 def build_all():
+    import gen_pset
     consts = ConstBank()
-    progs = build_fin(consts) + build_set(consts)
+    psi, iso = _curve_constants()
+    progs = build_fin(consts)
+    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, psi, iso, G1X, G1Y)
     return progs, consts
 
 
@@ -526,6 +474,12 @@ def main(out: str | None = None) -> None:
     path = Path(out) if out else Path(__file__).resolve().parent.parent / "lodestar_amd" / "_native" / "coop_tables.bin"
     path.parent.mkdir(parents=True, exist_ok=True)
     emit(progs, consts, path)
+    import json
+    summary = {pg.name: {"steps": len(pg.steps), "mul_steps": pg.n_mul_steps,
+                         "mul_ops": sum(1 for st in pg.steps for op in st if op.kind == OP_MUL),
+                         "lin_ops": sum(1 for st in pg.steps for op in st if op.kind == OP_LIN)}
+               for pg in progs}
+    path.with_name("coop_programs.json").write_text(json.dumps(summary, indent=1))
     for pg in progs:
         print(f"{pg.name:18s} steps={len(pg.steps):5d} mul_steps={pg.n_mul_steps:5d} "
               f"ops={sum(len(s) for s in pg.steps):7d}", file=sys.stderr)

@@ -1,0 +1,451 @@
+"""Per-set cooperative programs ("pset" frame) for the one-wavefront-per-set kernel
+(lodestar_amd/csrc/kernels/k_pset.hip).  Imported by tools/gen_coop.py.
+
+The set's work, after the single-lane kernel has produced the two SSWU points
+q0, q1 on E2', the decompressed signature and the public key:
+
+  H     = clear_cofactor(iso(q0) + iso(q1))                  (RFC 9380, Budroni-Pintore)
+  check = psi(sig) == [x] sig                                 (G2 membership, Scott)
+  RS    = [r] sig,  RP = [r] pk                               (64-bit batch scalar)
+  f_i   = ML(RP, H) * ML(-g1, RS)                             (two-pair Miller loop)
+
+Scalar multiplications run left to right, one doubling program per bit for every
+chain at once (lanes in parallel) and addition programs chosen per bit by the
+kernel: the |x| bits are fixed, the r bits per set.  The r chains start from sig
+(resp. pk) for an implicit top bit 2^64 and subtract [2^64] sig (resp. pk), a pure
+doubling chain run in the same programs, so every set runs the same 64 steps.
+Additions zero-check H: an exceptional case (possible only for adversarial
+signatures off the subgroup, or with negligible probability) flags the set for the
+exact single-lane path.
+
+Frame (slots):
+  Q0 0..3  Q1 4..7  SIG 8..11 (affine)  PK 12..14 (G1 Jacobian)
+  A 15..20 (cofactor chain [|x|]P)  C 21..26 (subgroup chain [|x|]sig)
+  D1 27..32 ([r + 2^64] sig)  D2 33..35 ([r + 2^64] pk)  E1 36..41 ([2^64] sig)  E2 42..44 ([2^64] pk)
+  PP 45..50 (P = iso(q0) + iso(q1))  H 51..56  RS 57..62  RP 63..65
+  HQ 66..69  RSQ 70..73 (affine)  INV_IN 74  INV_OUT 75  DIFF 76..79 (subgroup test)
+  F 80..91 (f_i)  temporaries 92..FRAME-1
+"""
+from __future__ import annotations
+
+from circuits import Circuit, Lin, schedule
+
+Q0, Q1, SIG, PK = 0, 4, 8, 12
+A, C, D1, D2, E1, E2 = 15, 21, 27, 33, 36, 42
+PP, H, RS, RP = 45, 51, 57, 63
+HQ, RSQ, INV_IN, INV_OUT, DIFF, F = 66, 70, 74, 75, 76, 80
+REGS = set(range(0, 92))
+
+
+class F1:
+    """Fp as a one-element field for the generic point formulas."""
+
+    def __init__(self, c: Circuit):
+        self.c = c
+
+    def add(self, a, b):
+        return a + b
+
+    def sub(self, a, b):
+        return a - b
+
+    def neg(self, a):
+        return -a
+
+    def sc(self, a, k):
+        return a * k
+
+    def mul(self, a, b):
+        return self.c.mul(a, b)
+
+    def sqr(self, a):
+        return self.c.mul(a, a)
+
+    def mat(self, a):
+        return self.c.mat(a)
+
+    def zero(self, a):
+        self.c.zcheck(a)
+
+    def reg(self, base):
+        return Circuit.inp(base)
+
+    def one(self):
+        return self.c.one()
+
+    def out(self, slot, v):
+        self.c.out(slot, v)
+
+    width = 1
+
+
+class F2:
+    def __init__(self, t):
+        self.t = t
+        self.c = t.c
+
+    def add(self, a, b):
+        return self.t.add2(a, b)
+
+    def sub(self, a, b):
+        return self.t.sub2(a, b)
+
+    def neg(self, a):
+        return self.t.neg2(a)
+
+    def sc(self, a, k):
+        return self.t.sc2(a, k)
+
+    def mul(self, a, b):
+        return self.t.mul2(a, b)
+
+    def sqr(self, a):
+        return self.t.sqr2(a)
+
+    def mat(self, a):
+        return self.t.mat2(a)
+
+    def zero(self, a):
+        self.c.zcheck(a[0])
+        self.c.zcheck(a[1])
+
+    def reg(self, base):
+        return self.t.f2(base)
+
+    def one(self):
+        return (self.c.one(), Lin())
+
+    def out(self, slot, v):
+        self.c.out(slot, v[0])
+        self.c.out(slot + 1, v[1])
+
+    width = 2
+
+
+def jac(fo, base):
+    w = fo.width
+    return (fo.reg(base), fo.reg(base + w), fo.reg(base + 2 * w))
+
+
+def aff(fo, base):
+    w = fo.width
+    return (fo.reg(base), fo.reg(base + w))
+
+
+def out_jac(fo, base, pt):
+    w = fo.width
+    for k in range(3):
+        fo.out(base + k * w, pt[k])
+
+
+def dbl(fo, p):
+    X, Y, Z = p
+    a = fo.sqr(X)
+    b = fo.sqr(Y)
+    cc = fo.sqr(b)
+    d = fo.sc(fo.sub(fo.sub(fo.sqr(fo.add(X, b)), a), cc), 2)
+    e = fo.sc(a, 3)
+    f = fo.sqr(e)
+    x3 = fo.mat(fo.sub(f, fo.sc(d, 2)))
+    y3 = fo.sub(fo.mul(e, fo.sub(d, x3)), fo.sc(cc, 8))
+    z3 = fo.sc(fo.mul(Y, Z), 2)
+    return x3, fo.mat(y3), fo.mat(z3)
+
+
+def add_gen(fo, p, q, check=True):
+    """add-2007-bl; zero-checks H (exceptional: P == +-Q or an input at infinity)."""
+    X1, Y1, Z1 = p
+    X2, Y2, Z2 = q
+    z1z1 = fo.sqr(Z1)
+    z2z2 = fo.sqr(Z2)
+    u1 = fo.mul(X1, z2z2)
+    u2 = fo.mul(X2, z1z1)
+    s1 = fo.mul(fo.mul(Y1, Z2), z2z2)
+    s2 = fo.mul(fo.mul(Y2, Z1), z1z1)
+    h = fo.mat(fo.sub(u2, u1))
+    if check:
+        fo.zero(h)
+    r = fo.sc(fo.sub(s2, s1), 2)
+    i = fo.sqr(fo.sc(h, 2))
+    j = fo.mul(h, i)
+    v = fo.mul(u1, i)
+    x3 = fo.mat(fo.sub(fo.sub(fo.sqr(r), j), fo.sc(v, 2)))
+    y3 = fo.sub(fo.mul(r, fo.sub(v, x3)), fo.sc(fo.mul(s1, j), 2))
+    z3 = fo.mul(fo.sub(fo.sub(fo.sqr(fo.add(Z1, Z2)), z1z1), z2z2), h)
+    return x3, fo.mat(y3), fo.mat(z3)
+
+
+def add_mixed(fo, p, q, check=True):
+    """madd-2007-bl: p Jacobian + q affine; zero-checks H."""
+    X1, Y1, Z1 = p
+    X2, Y2 = q
+    z1z1 = fo.sqr(Z1)
+    u2 = fo.mul(X2, z1z1)
+    s2 = fo.mul(fo.mul(Y2, Z1), z1z1)
+    h = fo.mat(fo.sub(u2, X1))
+    if check:
+        fo.zero(h)
+    hh = fo.sqr(h)
+    i = fo.sc(hh, 4)
+    j = fo.mul(h, i)
+    r = fo.sc(fo.sub(s2, Y1), 2)
+    v = fo.mul(X1, i)
+    x3 = fo.mat(fo.sub(fo.sub(fo.sqr(r), j), fo.sc(v, 2)))
+    y3 = fo.sub(fo.mul(r, fo.sub(v, x3)), fo.sc(fo.mul(Y1, j), 2))
+    z3 = fo.sub(fo.sub(fo.sqr(fo.add(Z1, h)), z1z1), hh)
+    return x3, fo.mat(y3), fo.mat(z3)
+
+
+def neg_pt(fo, p):
+    return (p[0], fo.neg(p[1]), p[2])
+
+
+def psi_jac(t, p, consts_psi):
+    cx, cy = consts_psi
+    X, Y, Z = p
+    return (t.mat2(t.mulc2(t.conj2(X), cx)), t.mat2(t.mulc2(t.conj2(Y), cy)), t.conj2(Z))
+
+
+def iso_jac(t, x, y, iso):
+    """3-isogeny E2' -> E2 in Jacobian form (no inversion):
+       Z = xd yd, X = xn xd yd^2, Y = y yn xd^3 yd^2; zero-checks xd and yd (infinity)."""
+    xnum, xden, ynum, yden = iso
+
+    def horner(coefs, monic):
+        # coefficients low -> high; a monic polynomial lists its leading 1 last
+        cs = list(coefs)
+        if monic:
+            acc = t.add2(x, const2(t, cs[-2]))
+            cs = cs[:-2]
+        else:
+            acc = const2(t, cs[-1])
+            cs = cs[:-1]
+        for cf in reversed(cs):
+            acc = t.add2(t.mat2(t.mul2(acc, x)), const2(t, cf))
+        return t.mat2(acc)
+
+    xn = horner(xnum, False)
+    xd = horner(xden, True)
+    yn = horner(ynum, False)
+    yd = horner(yden, True)
+    t.c.zcheck(xd[0])
+    t.c.zcheck(xd[1])
+    t.c.zcheck(yd[0])
+    t.c.zcheck(yd[1])
+    xd2 = t.mat2(t.sqr2(xd))
+    yd2 = t.mat2(t.sqr2(yd))
+    Z = t.mat2(t.mul2(xd, yd))
+    X = t.mat2(t.mul2(xn, t.mat2(t.mul2(xd, yd2))))
+    Y = t.mat2(t.mul2(t.mat2(t.mul2(y, yn)), t.mat2(t.mul2(t.mat2(t.mul2(xd, xd2)), yd2))))
+    return X, Y, Z
+
+
+def const2(t, v):
+    return (t.c.const(v[0]) if v[0] else Lin(), t.c.const(v[1]) if v[1] else Lin())
+
+
+def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G1Y):
+    progs = []
+
+    def new(name):
+        c = Circuit(name, consts)
+        t = T(c)
+        return c, t, F1(c), F2(t)
+
+    # P = iso(q0) + iso(q1); initialise every chain
+    c, t, f1, f2 = new("pset_prep")
+    p0 = iso_jac(t, t.f2(Q0), t.f2(Q0 + 2), ISO)
+    p1 = iso_jac(t, t.f2(Q1), t.f2(Q1 + 2), ISO)
+    pp = add_gen(f2, p0, p1)
+    out_jac(f2, PP, pp)
+    out_jac(f2, A, pp)
+    sig = aff(f2, SIG)
+    sigj = (sig[0], sig[1], f2.one())
+    for base in (C, D1, E1):
+        out_jac(f2, base, sigj)
+    pk = jac(f1, PK)
+    for base in (D2, E2):
+        out_jac(f1, base, pk)
+    progs.append(schedule(c, FRAME, REGS))
+
+    # doubling programs
+    def dbl_prog(name, g2_regs, g1_regs):
+        c, t, f1, f2 = new(name)
+        for base in g2_regs:
+            out_jac(f2, base, dbl(f2, jac(f2, base)))
+        for base in g1_regs:
+            out_jac(f1, base, dbl(f1, jac(f1, base)))
+        progs.append(schedule(c, FRAME, REGS))
+
+    dbl_prog("pset_dbl_r", (D1, E1), (D2, E2))
+    dbl_prog("pset_dbl_all", (A, C, D1, E1), (D2, E2))
+
+    def add_prog(name, x_part, r_part):
+        c, t, f1, f2 = new(name)
+        if x_part:
+            out_jac(f2, A, add_gen(f2, jac(f2, A), jac(f2, PP)))
+            out_jac(f2, C, add_mixed(f2, jac(f2, C), aff(f2, SIG)))
+        if r_part:
+            out_jac(f2, D1, add_mixed(f2, jac(f2, D1), aff(f2, SIG)))
+            out_jac(f1, D2, add_gen(f1, jac(f1, D2), jac(f1, PK)))
+        progs.append(schedule(c, FRAME, REGS))
+
+    add_prog("pset_add_x", True, False)
+    add_prog("pset_add_r", False, True)
+    add_prog("pset_add_xr", True, True)
+
+    # phase 2 (straight line): finish the cofactor clearing, the r multiples and the
+    # subgroup comparison
+    c, t, f1, f2 = new("pset_phase2")
+    P = jac(f2, PP)
+    t1 = neg_pt(f2, jac(f2, A))                        # [x]P = -[|x|]P
+    t2 = psi_jac(t, P, PSI)
+    t2p = add_gen(f2, t1, t2)                          # t1 + t2
+    # U = [|x|] t2p
+    U = t2p
+    for i in range(62, -1, -1):
+        U = dbl(f2, U)
+        if (X_ABS >> i) & 1:
+            U = add_gen(f2, U, t2p)
+    p2 = dbl(f2, P)
+    t3 = psi_jac(t, psi_jac(t, p2, PSI), PSI)          # psi^2(2P)
+    t3 = add_gen(f2, t3, neg_pt(f2, t2))               # - t2
+    t3 = add_gen(f2, t3, neg_pt(f2, U))                # + [x] t2p
+    t3 = add_gen(f2, t3, neg_pt(f2, t1))               # - t1
+    hh = add_gen(f2, t3, neg_pt(f2, P))                # - P
+    out_jac(f2, H, hh)
+    # RS = D1 - E1, RP = D2 - E2
+    out_jac(f2, RS, add_gen(f2, jac(f2, D1), neg_pt(f2, jac(f2, E1))))
+    out_jac(f1, RP, add_gen(f1, jac(f1, D2), neg_pt(f1, jac(f1, E2))))
+    # subgroup: psi(sig) == -C (= [x] sig): (psi.x) Z^2 == X and (psi.y) Z^3 == -Y
+    X, Y, Z = jac(f2, C)
+    f2.zero(Z)                                         # [|x|] sig hit infinity: exact path
+    sx, sy = t.mulc2(t.conj2(t.f2(SIG)), PSI[0]), t.mulc2(t.conj2(t.f2(SIG + 2)), PSI[1])
+    z2 = t.mat2(t.sqr2(Z))
+    z3 = t.mat2(t.mul2(z2, Z))
+    d0 = t.sub2(t.mul2(t.mat2(sx), z2), X)
+    d1 = t.add2(t.mul2(t.mat2(sy), z3), Y)
+    f2.out(DIFF, d0)
+    f2.out(DIFF + 2, d1)
+    progs.append(schedule(c, FRAME, REGS))
+
+    # one inversion for both affine conversions: INV_IN = N(H.z) N(RS.z)
+    c, t, f1, f2 = new("pset_norm2")
+    hz = t.f2(H + 4)
+    rz = t.f2(RS + 4)
+    nh = c.mat(c.mul(hz[0], hz[0]) + c.mul(hz[1], hz[1]))
+    nr = c.mat(c.mul(rz[0], rz[0]) + c.mul(rz[1], rz[1]))
+    inv_in = c.mat(c.mul(nh, nr))
+    c.zcheck(inv_in)                                   # H or r sig at infinity: exact path
+    c.out(INV_IN, inv_in)
+    c.out(DIFF, nh)       # stash the norms for the next program (DIFF is free by now)
+    c.out(DIFF + 1, nr)
+    progs.append(schedule(c, FRAME, REGS))
+
+    c, t, f1, f2 = new("pset_affine2")
+    w = Circuit.inp(INV_OUT)
+    inv_nh = c.mat(c.mul(w, Circuit.inp(DIFF + 1)))   # 1/N(H.z)
+    inv_nr = c.mat(c.mul(w, Circuit.inp(DIFF)))       # 1/N(RS.z)
+    for base, inv, dst in ((H, inv_nh, HQ), (RS, inv_nr, RSQ)):
+        z = t.f2(base + 4)
+        zi = t.mat2((c.mul(z[0], inv), -c.mul(z[1], inv)))
+        zi2 = t.mat2(t.sqr2(zi))
+        zi3 = t.mat2(t.mul2(zi2, zi))
+        f2.out(dst, t.mul2(t.f2(base), zi2))
+        f2.out(dst + 2, t.mul2(t.f2(base + 2), zi3))
+    progs.append(schedule(c, FRAME, REGS))
+
+    # f = ML(RP, HQ) * ML(-g1, RSQ): two-pair Miller loop sharing the squarings
+    c, t, f1, f2 = new("pset_ml2")
+    X, Y, Z = (Circuit.inp(RP + k) for k in range(3))
+    pz3 = c.mat(c.mul(c.mat(c.mul(Z, Z)), Z))
+    pxz = c.mat(c.mul(X, Z))
+    pairs = [(t.f2(HQ), t.f2(HQ + 2), pxz, Y, pz3),
+             (t.f2(RSQ), t.f2(RSQ + 2), c.const(G1X), c.const(-G1Y), None)]
+    f = miller_loop_multi(t, pairs, miller_dbl, miller_add, X_ABS)
+    for k in range(2):
+        for j in range(3):
+            for i in range(2):
+                c.out(F + 6 * k + 2 * j + i, f[k][j][i])
+    # last program: only its inputs are live
+    progs.append(schedule(c, FRAME, set(range(RP, RP + 3)) | set(range(HQ, RSQ + 4))))
+    return progs
+
+
+def miller_loop_multi(t, pairs, miller_dbl, miller_add, X_ABS):
+    """prod_k f_{|x|,Q_k}(P_k), conjugated.  Per iteration the pairs' sparse lines are
+    multiplied together (in parallel with f^2) and folded into f with one Fp12 product."""
+    c = t.c
+    Ts = [(qx, qy, (c.one(), Lin())) for qx, qy, _, _, _ in pairs]
+    f = None
+    z = (Lin(), Lin())
+
+    def line(coefs, pxz, py, pz3):
+        l0, l2, l3 = coefs
+        if pz3 is not None:
+            l0 = t.mulfp2(l0, pz3)
+        l2 = t.mulfp2(l2, pxz)
+        l3 = t.mulfp2(l3, py)
+        return t.mat2(l0), t.mat2(l2), t.mat2(l3)
+
+    def lines_product(ls):
+        (a0, a2, a3), (b0, b2, b3) = ls
+        p00 = t.mul2(a0, b0)
+        p22 = t.mul2(a2, b2)
+        p33 = t.mul2(a3, b3)
+        c2 = t.sub2(t.sub2(t.mul2(t.add2(a0, a2), t.add2(b0, b2)), p00), p22)
+        c3 = t.sub2(t.sub2(t.mul2(t.add2(a0, a3), t.add2(b0, b3)), p00), p33)
+        c5 = t.sub2(t.sub2(t.mul2(t.add2(a2, a3), t.add2(b2, b3)), p22), p33)
+        c0 = t.add2(p00, t.xi2(p33))
+        return t.mat12(t.from_coefs([c0, z, c2, c3, p22, c5]))
+
+    def step(f, ls):
+        if len(ls) == 1:
+            l0, l2, l3 = ls[0]
+            if f is None:
+                return ((l0, l2, z), (z, l3, z))
+            return t.mat12(t.mul_line(f, l0, l2, l3))
+        L = lines_product(ls)
+        return L if f is None else t.mat12(t.mul12(f, L))
+
+    for i in range(62, -1, -1):
+        if f is not None:
+            f = t.mat12(t.sqr12(f))
+        ls = []
+        for k, (qx, qy, pxz, py, pz3) in enumerate(pairs):
+            Tk, coefs = miller_dbl(t, *Ts[k])
+            Ts[k] = tuple(t.mat2(x) for x in Tk)
+            ls.append(line(coefs, pxz, py, pz3))
+        f = step(f, ls)
+        if (X_ABS >> i) & 1:
+            ls = []
+            for k, (qx, qy, pxz, py, pz3) in enumerate(pairs):
+                Tk, coefs = miller_add(t, *Ts[k], qx, qy)
+                Ts[k] = tuple(t.mat2(x) for x in Tk)
+                ls.append(line(coefs, pxz, py, pz3))
+            f = step(f, ls)
+    return t.conj12(f)
+
+
+def run_pset(pg, consts, frame, r, simulate, inv):
+    """The k_pset controller (lodestar_amd/csrc/kernels/k_pset.hip) over the
+    simulator: returns the zero-check flag.  pg: name -> Program; inv: Fp inverse."""
+    flag = simulate(pg["pset_prep"], frame, consts)
+    flag |= simulate(pg["pset_dbl_r"], frame, consts)
+    if (r >> 63) & 1:
+        flag |= simulate(pg["pset_add_r"], frame, consts)
+    for i in range(62, -1, -1):
+        flag |= simulate(pg["pset_dbl_all"], frame, consts)
+        xb, rb = (X_ABS_BITS >> i) & 1, (r >> i) & 1
+        if xb or rb:
+            flag |= simulate(pg["pset_add_xr" if xb and rb else ("pset_add_x" if xb else "pset_add_r")], frame, consts)
+    flag |= simulate(pg["pset_phase2"], frame, consts)
+    in_group = all(frame[DIFF + k] == 0 for k in range(4))
+    flag |= simulate(pg["pset_norm2"], frame, consts)
+    frame[INV_OUT] = inv(frame[INV_IN])
+    flag |= simulate(pg["pset_affine2"], frame, consts)
+    flag |= simulate(pg["pset_ml2"], frame, consts)
+    return flag, in_group
+
+
+X_ABS_BITS = 0xD201000000010000
