@@ -128,10 +128,11 @@ int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iters, double* 
 /* Probe: time the cooperative (one wavefront per task) program `name` on `blocks`
  * tasks, `reps` runs each; us_per_step = run time / step count. */
 int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint32_t reps, double* us_per_step,
-                       double* ms_total, uint64_t* step_stamps /* nullable, n_steps + 1 s_memtime stamps */);
+                       double* ms_total,
+                       uint64_t* step_stamps /* nullable, 2 n_steps + 1 s_memtime stamps (step start, compute done) */);
 
 /* Test hook: BLS_DEBUG_FORCE_EXACT routes every set through the exact single-lane
- * path (k_exact) instead of the cooperative kernel, so parity tests cover both. */
+ * path (stage_exact_set) instead of the cooperative programs, so parity tests cover both. */
 #define BLS_DEBUG_FORCE_EXACT 1u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 

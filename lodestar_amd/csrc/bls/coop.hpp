@@ -39,6 +39,15 @@ struct CoopProg {
   uint32_t first, n;
 };
 
+// Per-block LDS of a cooperative task: the frame, then the constant bank, so one
+// slot index (constants at COOP_FRAME + k, tools/gen_coop.py:emit) addresses both.
+struct CoopLds {
+  Fp frame[COOP_FRAME];
+  Fp cbank[COOP_MAX_CONSTS];
+  uint32_t flag;
+};
+static_assert(offsetof(CoopLds, cbank) == COOP_FRAME * sizeof(Fp), "constant bank must follow the frame");
+
 // Programs of the finalisation frame ("fin", tools/gen_coop.py:build_fin)
 struct CoopEnv {
   const CoopOp* ops;
@@ -94,9 +103,26 @@ __device__ __forceinline__ void lds_store_fp(Fp* frame, uint32_t slot, const Fp&
   p[2] = make_uint4(v.l[8], v.l[9], v.l[10], v.l[11]);
 }
 
-// frame slot or (bit 15) constant-bank entry; both live in LDS
-__device__ __forceinline__ Fp coop_term(uint16_t ref, const Fp* frame, const Fp* cbank) {
-  return (ref & 0x8000u) ? lds_load_fp(cbank, ref & 0x7fffu) : lds_load_fp(frame, ref);
+// The same through an explicit LDS (address space 3) pointer: 32-bit addressing with
+// no generic-pointer checks per access (the interpreter converts its frame once).
+typedef unsigned int bls_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bls_u32x4 LdsU4;
+
+__device__ __forceinline__ Fp lds_load_fp(const LdsU4* base, uint32_t slot) {
+  const LdsU4* p = base + 3 * slot;
+  bls_u32x4 w0 = p[0], w1 = p[1], w2 = p[2];
+  Fp r;
+  r.l[0] = w0.x; r.l[1] = w0.y; r.l[2] = w0.z; r.l[3] = w0.w;
+  r.l[4] = w1.x; r.l[5] = w1.y; r.l[6] = w1.z; r.l[7] = w1.w;
+  r.l[8] = w2.x; r.l[9] = w2.y; r.l[10] = w2.z; r.l[11] = w2.w;
+  return r;
+}
+
+__device__ __forceinline__ void lds_store_fp(LdsU4* base, uint32_t slot, const Fp& v) {
+  LdsU4* p = base + 3 * slot;
+  p[0] = bls_u32x4{v.l[0], v.l[1], v.l[2], v.l[3]};
+  p[1] = bls_u32x4{v.l[4], v.l[5], v.l[6], v.l[7]};
+  p[2] = bls_u32x4{v.l[8], v.l[9], v.l[10], v.l[11]};
 }
 
 // Lazy linear combination: terms accumulate unreduced in a 13-limb two's-complement
@@ -105,36 +131,19 @@ struct Acc13 {
   uint32_t l[13];
 };
 
-__device__ __forceinline__ void acc_add(Acc13& a, const Fp& x) { asm_acc_add12(a.l, x.l); }
-
-__device__ __forceinline__ void acc_sub(Acc13& a, const Fp& x) { asm_acc_sub12(a.l, x.l); }
-
-// a += c * x for a small signed c
-__device__ __forceinline__ void acc_add_small(Acc13& a, const Fp& x, int c) {
-  const uint32_t m = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
-  uint32_t t[13], carry = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t v = (uint64_t)x.l[i] * m + carry;
-    t[i] = (uint32_t)v;
-    carry = (uint32_t)(v >> 32);
-  }
-  t[12] = carry;
-  if (c < 0) asm_acc_sub13(a.l, t);
-  else asm_acc_add13(a.l, t);
-}
-
 __device__ __forceinline__ uint32_t k20p_limb(int i) {  // 2^20 * p, 13 limbs
   const uint32_t t[13] = {0xaab00000u, 0xfffffffau, 0xfffb9fefu, 0xffeb153fu, 0x6241eabfu, 0x2a0f6b0fu, 0x2bf6730du,
                           0xb84f3851u, 0xcd764774u, 0x7b6434bau, 0x69a4b1bau, 0x1ea397feu, 0x0001a011u};
   return t[i];
 }
 
-// canonical (sum mod p) of the accumulator
-__device__ __forceinline__ Fp acc_reduce(Acc13 a) {
+// canonical (sum + extra) mod p of the accumulator; extra < 2^20 (the +1s of
+// the negated terms, see coop_lin)
+__device__ __forceinline__ Fp acc_reduce(Acc13 a, uint32_t extra) {
   uint32_t k20p[13];
 #pragma unroll
   for (int i = 0; i < 13; ++i) k20p[i] = k20p_limb(i);
+  k20p[0] += extra;          // 0xaab00000 + extra: no carry
   asm_acc_add13(a.l, k20p);  // now 0 <= a < 2^21 p
   // q ~ a / p from the top 96 bits in double precision (error < 1)
   double d = (double)a.l[12] * 18446744073709551616.0 + (double)a.l[11] * 4294967296.0 + (double)a.l[10];
@@ -160,23 +169,65 @@ __device__ __forceinline__ Fp acc_reduce(Acc13 a) {
   return negative ? up : (ge_p ? dn : lo);
 }
 
-__device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n,
-                                       const Fp* frame, const Fp* cbank) {
-  if (n == 1 && cf[0] == 1) return coop_term(refs[0], frame, cbank);
+// Wave-uniform max of n over the active lanes (n <= 8)
+__device__ __forceinline__ int coop_wave_max_terms(int n) {
+  int m = 0;
+#pragma unroll
+  for (int k = 1; k <= 8; ++k) m += __any(n >= k) ? 1 : 0;
+  return m;
+}
+
+// sum_k cf[k] * slot[refs[k]] mod p over n <= 8 terms.  refs index the block's LDS
+// slot array (frame, then the constant bank at COOP_FRAME).  Each term is added
+// branch-free (up to the wave's largest n):
+// x * |c| (only when some lane of the wave has |c| != 1), then the two's-complement
+// add a + (x ^ mask) (mask = ~0 for c < 0); the +1 of each negation is folded into
+// the reduction bias.  Loop bounds and the multiply test are wave-uniform.
+__device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n, const LdsU4* slots) {
+  if (__all(n == 1 && cf[0] == 1)) return lds_load_fp(slots, refs[0]);
+  const int nmax = coop_wave_max_terms(n);
   Acc13 acc;
 #pragma unroll
   for (int i = 0; i < 13; ++i) acc.l[i] = 0;
+  uint32_t negs = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
+    if (k >= nmax) break;
     if (k < n) {
-      const Fp x = coop_term(refs[k], frame, cbank);
       const int c = cf[k];
-      if (c == 1) acc_add(acc, x);
-      else if (c == -1) acc_sub(acc, x);
-      else acc_add_small(acc, x, c);
+      const uint32_t mask = c < 0 ? 0xffffffffu : 0u;
+      const uint32_t m = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
+      negs += mask & 1u;
+      const Fp x = lds_load_fp(slots, refs[k]);
+      uint32_t t[13];
+      if (__any(m != 1u)) {
+        // 12 independent 32x32 products, then one carry chain
+        uint64_t pr[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) pr[i] = (uint64_t)x.l[i] * m;
+        uint32_t hs[12], ls[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          ls[i] = (uint32_t)pr[i];
+          hs[i] = (uint32_t)(pr[i] >> 32);
+        }
+        uint32_t mid[12];
+        mid[0] = ls[0];
+#pragma unroll
+        for (int i = 1; i < 12; ++i) mid[i] = ls[i];
+        uint32_t c12 = asm_add11_shift(mid, hs);  // mid[i] += hs[i-1], i = 1..11; returns hs[11] + carry
+#pragma unroll
+        for (int i = 0; i < 12; ++i) t[i] = mid[i] ^ mask;
+        t[12] = c12 ^ mask;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) t[i] = x.l[i] ^ mask;
+        t[12] = mask;
+      }
+      asm_acc_add13(acc.l, t);
     }
   }
-  return acc_reduce(acc);
+  return acc_reduce(acc, negs);
 }
 
 union CoopOpWords {
@@ -199,29 +250,32 @@ __device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* fra
   const int lane = threadIdx.x;
   const uint4* base = reinterpret_cast<const uint4*>(env.ops);
   if (pg.n == 0) return;
-  CoopOpWords cur, nxt;
+  LdsU4* slots = (LdsU4*)frame;
+  // the next step's ops are in flight while a step computes
+  CoopOpWords cur, n1;
   coop_fetch(cur, base, pg.first, lane);
   for (uint32_t s = 0; s < pg.n; ++s) {
-    if (TIMED && lane == 0) stamps[s] = __builtin_amdgcn_s_memtime();
-    if (s + 1 < pg.n) coop_fetch(nxt, base, pg.first + s + 1, lane);
+    if (TIMED && lane == 0) stamps[2 * s] = __builtin_amdgcn_s_memtime();
+    if (s + 1 < pg.n) coop_fetch(n1, base, pg.first + s + 1, lane);
     const CoopOp& op = cur.op;
     Fp r = fp_zero();
     if (op.kind != 0) {
-      r = coop_lin(op.a, op.ca, op.na, frame, cbank);
-      if (op.kind == 1) r = fp_mul(r, coop_lin(op.b, op.cb, op.nb, frame, cbank));
+      r = coop_lin(op.a, op.ca, op.na, slots);
+      if (op.kind == 1) r = fp_mul_inl(r, coop_lin(op.b, op.cb, op.nb, slots));
     }
+    if (TIMED && lane == 0) stamps[2 * s + 1] = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if (op.kind != 0) {
       if (op.out == COOP_OUT_ZCHECK) {
         if (fp_is_zero(r)) *flag = 1u;
       } else {
-        lds_store_fp(frame, op.out, r);
+        lds_store_fp(slots, op.out, r);
       }
     }
     __syncthreads();
-    cur = nxt;
+    cur = n1;
   }
-  if (TIMED && lane == 0) stamps[pg.n] = __builtin_amdgcn_s_memtime();
+  if (TIMED && lane == 0) stamps[2 * pg.n] = __builtin_amdgcn_s_memtime();
 }
 
 __device__ __forceinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,

@@ -246,46 +246,76 @@ __device__ __forceinline__ void bls_mac2(uint64_t& lo, uint32_t& hi, uint32_t a,
       : "v"(a), "v"(b), "v"(m), "s"(p));
 }
 
-BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
-  uint32_t m[12];
-  Fp u;
-  uint64_t lo = 0, lo2 = 0;
-  uint32_t hi = 0, hi2 = 0;
+// Four independent multiply-accumulates (columns c0..c3) in one block: the four
+// v_mad_u64_u32 issue back to back and each carry is consumed three instructions
+// later, so the wave does not stall on the 64-bit multiply latency.
+#define BLS_MAC4(L, H, k, x, y0, y1, y2, y3, YC)                                                       \
+  do {                                                                                             \
+    uint64_t c0_, c1_, c2_, c3_;                                                                   \
+    asm("v_mad_u64_u32 %0, %8, %12, %13, %0\n\t"                                                  \
+        "v_mad_u64_u32 %2, %9, %12, %14, %2\n\t"                                                  \
+        "v_mad_u64_u32 %4, %10, %12, %15, %4\n\t"                                                 \
+        "v_mad_u64_u32 %6, %11, %12, %16, %6\n\t"                                                 \
+        "v_addc_co_u32 %1, %8, 0, %1, %8\n\t"                                                     \
+        "v_addc_co_u32 %3, %9, 0, %3, %9\n\t"                                                     \
+        "v_addc_co_u32 %5, %10, 0, %5, %10\n\t"                                                   \
+        "v_addc_co_u32 %7, %11, 0, %7, %11"                                                        \
+        : "+v"(L[k]), "+v"(H[k]), "+v"(L[k + 1]), "+v"(H[k + 1]), "+v"(L[k + 2]), "+v"(H[k + 2]),   \
+          "+v"(L[k + 3]), "+v"(H[k + 3]), "=&s"(c0_), "=&s"(c1_), "=&s"(c2_), "=&s"(c3_)            \
+        : "v"(x), YC(y0), YC(y1), YC(y2), YC(y3));                                                  \
+  } while (0)
+
+// 64-bit add of c into column (L, H): L += c, carry into H
+__device__ __forceinline__ void bls_col_add(uint64_t& lo, uint32_t& hi, uint64_t c) {
+  uint32_t l0 = (uint32_t)lo, l1 = (uint32_t)(lo >> 32);
+  uint64_t cc;
+  asm("v_add_co_u32 %0, %3, %0, %4\n\t"
+      "v_addc_co_u32 %1, %3, %1, %5, %3\n\t"
+      "v_addc_co_u32 %2, %3, 0, %2, %3"
+      : "+v"(l0), "+v"(l1), "+v"(hi), "=&s"(cc)
+      : "v"((uint32_t)c), "v"((uint32_t)(c >> 32)));
+  lo = ((uint64_t)l1 << 32) | l0;
+}
+
+// gfx950 Montgomery product with column accumulators (separated operand scanning):
+// the 144 a*b products fill 24 columns row by row, four independent columns per
+// block; the reduction then adds m_i * p into columns i..i+11, where only
+// m_i = col_i * (-p^-1) and the carry col_i >> 64-bit into col_{i+1} are on the
+// dependency chain.  288 products, 2 instructions each.
+__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) {
+  uint64_t L[24];
+  uint32_t H[24];
 #pragma unroll
-  for (int k = 0; k < 12; ++k) {
-#pragma unroll
-    for (int i = 0; i < k; ++i) {
-      bls_mac2(lo, hi, a.l[i], b.l[k - i], lo2, hi2, m[i], p_limb(k - i));
-    }
-    bls_mac(lo, hi, a.l[k], b.l[0]);
-    uint64_t s = lo + lo2;
-    hi = hi + hi2 + (s < lo ? 1u : 0u);
-    lo = s;
-    lo2 = 0;
-    hi2 = 0;
-    m[k] = (uint32_t)lo * BLS_NP0;
-    bls_mac_s(lo, hi, m[k], p_limb(0));
-    lo = (lo >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
+  for (int k = 0; k < 24; ++k) {
+    L[k] = 0;
+    H[k] = 0;
   }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+#pragma unroll
+    for (int j = 0; j < 12; j += 4) BLS_MAC4(L, H, i + j, a.l[i], b.l[j], b.l[j + 1], b.l[j + 2], b.l[j + 3], "v");
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint32_t m = (uint32_t)L[i] * BLS_NP0;
+    BLS_MAC4(L, H, i, m, p_limb(0), p_limb(1), p_limb(2), p_limb(3), "s");
+    // column i is now 0 mod 2^32: carry (col_i >> 32) into column i+1
+    const uint64_t c = (L[i] >> 32) | ((uint64_t)H[i] << 32);
+    bls_col_add(L[i + 1], H[i + 1], c);
+    BLS_MAC4(L, H, i + 4, m, p_limb(4), p_limb(5), p_limb(6), p_limb(7), "s");
+    BLS_MAC4(L, H, i + 8, m, p_limb(8), p_limb(9), p_limb(10), p_limb(11), "s");
+  }
+  Fp u;
 #pragma unroll
   for (int k = 12; k < 23; ++k) {
-#pragma unroll
-    for (int i = k - 11; i < 12; ++i) {
-      bls_mac2(lo, hi, a.l[i], b.l[k - i], lo2, hi2, m[i], p_limb(k - i));
-    }
-    uint64_t s = lo + lo2;
-    hi = hi + hi2 + (s < lo ? 1u : 0u);
-    lo = s;
-    lo2 = 0;
-    hi2 = 0;
-    u.l[k - 12] = (uint32_t)lo;
-    lo = (lo >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
+    u.l[k - 12] = (uint32_t)L[k];
+    const uint64_t c = (L[k] >> 32) | ((uint64_t)H[k] << 32);
+    bls_col_add(L[k + 1], H[k + 1], c);
   }
-  u.l[11] = (uint32_t)lo;
+  u.l[11] = (uint32_t)L[23];
   return fp_reduce_once(u);
 }
+BLS_NOINLINE Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
 #else
 // Host build (test harness): Montgomery product a*b/R mod p, CIOS with the no-carry
 // optimisation (valid because p's top limb 0x1a0111ea < 2^31 - 1).  Inputs < p, output < p.
@@ -317,6 +347,7 @@ BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
   for (int j = 0; j < 12; ++j) r.l[j] = t[j];
   return fp_reduce_once(r);
 }
+BLS_HD Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul(a, b); }
 #endif
 
 BLS_HD Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }

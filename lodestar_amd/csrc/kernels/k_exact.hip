@@ -6,7 +6,7 @@
 
 using namespace bls;
 
-__global__ __launch_bounds__(BLS_BLOCK) void k_exact(PipeBufs b) {
+__global__ __launch_bounds__(BLS_BLOCK, 2) void k_exact(PipeBufs b) {
   stage_exact_set(b, blockIdx.x * BLS_BLOCK + threadIdx.x);
 }
 

@@ -11,11 +11,7 @@
 
 using namespace bls;
 
-struct FinShared {
-  Fp frame[COOP_FRAME];
-  Fp cbank[COOP_MAX_CONSTS];
-  uint32_t flag;
-};
+typedef CoopLds FinShared;
 
 __device__ void fin_accumulate_set(const PipeBufs& b, const CoopEnv& env, FinShared& sh, uint32_t i, bool& first) {
   if (first) {

@@ -13,16 +13,14 @@
 // Reference semantics: Signature.fromBytes(.., validate=true) (maybeBatch.ts:23,36)
 // for the subgroup test, hash_to_G2 + the random-scalar pairing product of
 // verifyMultipleSignatures ([ext] blst) for f_i.  A zero-checked exceptional
-// addition, an infinity signature or a flag from k_pre sends the set to k_exact.
+// addition, an infinity signature or a flag from k_pre sends the set to k_exact
+// (pipeline.hpp stage_exact_set; kept out of this kernel so its registers and
+// stack do not lower this kernel's occupancy).
 #include "../launchers.hpp"
 
 using namespace bls;
 
-struct PsetShared {
-  Fp frame[COOP_FRAME];
-  Fp cbank[COOP_MAX_CONSTS];
-  uint32_t flag;
-};
+typedef CoopLds PsetShared;
 
 // frame registers (tools/gen_pset.py)
 enum : int { PS_Q0 = 0, PS_SIG = 8, PS_PK = 12, PS_INV_IN = 74, PS_INV_OUT = 75, PS_DIFF = 76, PS_F = 80 };

@@ -228,7 +228,7 @@ def test_fp_mul_device_vs_bigint(gpu):
 
 @pytest.mark.gpu
 def test_exact_path_matches_cooperative_path(gpu, oracle, golden, table):
-    """The same calls with every set forced through k_exact (complete single-lane
+    """The same calls with every set forced through the exact path (complete single-lane
     formulas) give the verdicts of the cooperative k_pset path."""
     sets = _sets(gpu, oracle, 4, tag=b"exact")
     reqs = [(True, [s]) for s in sets] + [(False, sets)]

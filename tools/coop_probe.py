@@ -22,11 +22,15 @@ with GpuContext(0) as g:
         for blocks in (1, 64, 1024):
             us, ms = g.coop_probe(name, blocks, reps)
             out[f"{name}@{blocks}"] = {"us_per_step": round(us, 3), "ms_per_run": round(ms / reps, 3)}
-        k = kinds[name]
-        _, _, st = g.coop_probe(name, 1, 1, len(k) + 1)
-        d = np.diff(st.astype(np.int64))  # s_memtime: shader-clock cycles
-        mul = d[np.array(k)]
-        lin = d[~np.array(k)]
-        out[f"{name}:stamps"] = {"mul_steps": int(len(mul)), "mul_ticks_mean": float(mul.mean()) if len(mul) else 0,
-                                 "lin_steps": int(len(lin)), "lin_ticks_mean": float(lin.mean()) if len(lin) else 0}
+        k = np.array(kinds[name])
+        _, _, st = g.coop_probe(name, 1, 1, 2 * len(k) + 1)
+        st = st.astype(np.int64)  # s_memtime: shader-clock cycles; 2 stamps per step
+        start, comp = st[0:-1:2], st[1::2]
+        total = np.diff(st[0::2])
+        compute = comp - start
+        out[f"{name}:stamps"] = {
+            "mul_steps": int(k.sum()), "mul_total": float(total[k].mean()) if k.any() else 0,
+            "mul_compute": float(compute[k].mean()) if k.any() else 0,
+            "lin_steps": int((~k).sum()), "lin_total": float(total[~k].mean()) if (~k).any() else 0,
+            "lin_compute": float(compute[~k].mean()) if (~k).any() else 0}
     print(json.dumps(out, indent=1))

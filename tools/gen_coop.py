@@ -439,7 +439,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                     out, kind, a, b = 0xFFFE, 0, [], []
                 assert len(a) <= 8 and len(b) <= 8
                 def refs(lst):
-                    r = [((0x8000 | x[1]) if isinstance(x, tuple) else x) for x, _ in lst]
+                    r = [((FRAME + x[1]) if isinstance(x, tuple) else x) for x, _ in lst]
                     return r + [0] * (8 - len(r))
                 def cfs(lst):
                     r = [cf for _, cf in lst]
@@ -447,6 +447,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                 steps_bin += struct.pack("<HBBB3x8H8H8h8h8x", out, kind, len(a), len(b),
                                          *refs(a), *refs(b), *cfs(a), *cfs(b))
         first += len(pg.steps)
+    assert len(consts.vals) <= 64, "constant bank exceeds COOP_MAX_CONSTS"
     header = struct.pack("<4sIIII", b"BLSC", 1, len(consts.vals), len(progs), first)
     cbin = b"".join(_le_limbs(v * MONT_R % P) for v in consts.vals)
     path.write_bytes(header + cbin + bytes(table) + bytes(steps_bin))
