@@ -1,0 +1,278 @@
+"""GpuBlsVerifier: the IBlsVerifier contract over the MI355X C-ABI.
+
+Mirrors `BlsMultiThreadWorkerPool` (beacon-node/src/chain/bls/multithread/index.ts)
+with GPU contexts in place of worker threads:
+
+* `verify_signature_sets(sets, batchable, verify_on_main_thread)` (interface.ts:20-46,
+  index.ts:134-174): the main-thread branch (`verify_on_main_thread` and not
+  `verify_all_multi_thread`) runs the call at once as one non-batchable request
+  (verifySignatureSetsMaybeBatch semantics, maybeBatch.ts:16-39); otherwise the sets
+  are split by chunkifyMaximizeChunkSize(sets, 128) into jobs (index.ts:156) whose
+  results are AND-ed.
+* job queue (index.ts:238-285): batchable jobs are buffered until more than 32
+  signatures are waiting or 100 ms passed since the first (MAX_BUFFERED_SIGS,
+  MAX_BUFFER_WAIT_MS); other jobs go straight to the queue.
+* dispatch (runJob / prepareWork, index.ts:290-400): an idle context takes queued
+  jobs up to `max_sets_per_call` signature sets (the reference's 128 by default) and
+  runs one verifyManySignatureSets call (bls_gpu_verify, worker.ts:32-108); per job a
+  verdict resolves the job's future, an error code rejects it with the blst-style
+  message ("BLST_ERROR: BLST_INVALID_SIZE", "Empty signature set", ...).
+* `close()` (index.ts:176-197) rejects pending jobs with QUEUE_ABORTED.
+
+Sets are `SignatureSet(pubkey, signing_root, signature)` where pubkey is an int
+index into the context's device pubkey table (Index2PubkeyCache), a list of
+indices (an aggregate set, getAggregatedPubkey, utils.ts:5-16), or 96 raw bytes
+(uncompressed affine, the worker wire format of index.ts:126).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from concurrent.futures import Future
+from dataclasses import dataclass
+from typing import Sequence, Union
+
+from ._abi import ERROR_MESSAGES
+from .native import GpuContext, pack_requests
+
+MAX_SIGNATURE_SETS_PER_JOB = 128   # multithread/index.ts:39
+MAX_BUFFERED_SIGS = 32             # multithread/index.ts:48 (flush when >)
+MAX_BUFFER_WAIT_MS = 100           # multithread/index.ts:57
+
+PubkeyRef = Union[int, Sequence[int], bytes]
+
+
+@dataclass
+class SignatureSet:
+    """ISignatureSet (state-transition/src/util/signatureSets.ts:5-22)."""
+
+    pubkey: PubkeyRef
+    signing_root: bytes
+    signature: bytes
+
+
+class BlsError(Exception):
+    """A rejected verification (the worker's WorkResult error, types.ts:26-38)."""
+
+
+class QueueAborted(Exception):
+    """QueueError QUEUE_ABORTED (util/queue)."""
+
+
+def chunkify_maximize_chunk_size(arr: list, min_per_chunk: int) -> list:
+    """multithread/utils.ts:4-19."""
+    chunk_count = len(arr) // min_per_chunk
+    if chunk_count <= 1:
+        return [arr]
+    per = -(-len(arr) // chunk_count)
+    return [arr[i: i + per] for i in range(0, len(arr), per)]
+
+
+@dataclass
+class _Job:
+    sets: list
+    batchable: bool
+    future: Future
+    added: float
+
+
+def _wire(s: SignatureSet):
+    pk = s.pubkey
+    if isinstance(pk, int):
+        pk = [pk]
+    elif not isinstance(pk, (bytes, bytearray, memoryview)):
+        pk = list(pk)
+    return (pk, bytes(s.signing_root), bytes(s.signature))
+
+
+class GpuBlsVerifier:
+    """IBlsVerifier on one GPU with `n_contexts` contexts (HIP streams) in flight."""
+
+    def __init__(self, device: int = 0, n_contexts: int = 2, verify_all_multi_thread: bool = False,
+                 max_sets_per_call: int = MAX_SIGNATURE_SETS_PER_JOB, pubkeys48: bytes | None = None):
+        self.verify_all_multi_thread = verify_all_multi_thread
+        self.max_sets_per_call = max_sets_per_call
+        self._ctxs = [GpuContext(device) for _ in range(n_contexts)]
+        self._main = self._ctxs[0]
+        self._main_lock = threading.Lock()
+        if pubkeys48 is not None:
+            self.load_pubkeys(pubkeys48)
+        self._cv = threading.Condition()
+        self._jobs: list[_Job] = []
+        self._buffer: list[_Job] = []
+        self._buffer_sigs = 0
+        self._buffer_first = 0.0
+        self._closed = False
+        self.metrics = {"jobs_started": 0, "sig_sets_started": 0, "batch_retries": 0, "batch_sigs_success": 0,
+                        "success_sig_sets": 0, "error_sig_sets": 0, "main_thread_calls": 0}
+        self._threads = [threading.Thread(target=self._worker, args=(c,), daemon=True) for c in self._ctxs]
+        self._timer = threading.Thread(target=self._buffer_timer, daemon=True)
+        for t in self._threads:
+            t.start()
+        self._timer.start()
+
+    # -- pubkey cache -----------------------------------------------------------
+    def load_pubkeys(self, pubkeys48: bytes) -> None:
+        """Append validator pubkeys (48 B compressed) to every context's device table."""
+        for c in self._ctxs:
+            codes = c.load_pubkeys(pubkeys48, 48)
+            if (codes != 0).any():
+                raise BlsError(f"invalid pubkey at table index {int((codes != 0).argmax())}")
+
+    # -- IBlsVerifier --------------------------------------------------------------
+    def verify_signature_sets(self, sets: Sequence[SignatureSet], batchable: bool = False,
+                              verify_on_main_thread: bool = False) -> bool:
+        return self.verify_signature_sets_async(sets, batchable, verify_on_main_thread).result()
+
+    def verify_signature_sets_async(self, sets: Sequence[SignatureSet], batchable: bool = False,
+                                    verify_on_main_thread: bool = False) -> Future:
+        if verify_on_main_thread and not self.verify_all_multi_thread:
+            fut: Future = Future()
+            self.metrics["main_thread_calls"] += 1
+            try:
+                with self._main_lock:
+                    fut.set_result(self._run_now(list(sets)))
+            except Exception as e:  # noqa: BLE001 - the contract rejects with the error
+                fut.set_exception(e)
+            return fut
+        jobs = [self._queue(chunk, batchable)
+                for chunk in chunkify_maximize_chunk_size(list(sets), MAX_SIGNATURE_SETS_PER_JOB)]
+        out: Future = Future()
+        pending = [len(jobs)]
+        results = [None] * len(jobs)
+        lock = threading.Lock()
+
+        def done(k, f):
+            with lock:
+                if out.done():
+                    return
+                if f.exception() is not None:
+                    out.set_exception(f.exception())
+                    return
+                results[k] = f.result()
+                pending[0] -= 1
+                if pending[0] == 0:
+                    out.set_result(all(r is True for r in results))
+
+        for k, j in enumerate(jobs):
+            j.future.add_done_callback(lambda f, k=k: done(k, f))
+        return out
+
+    def close(self) -> None:
+        with self._cv:
+            self._closed = True
+            pending = self._jobs + self._buffer
+            self._jobs, self._buffer = [], []
+            self._cv.notify_all()
+        for j in pending:
+            if not j.future.done():
+                j.future.set_exception(QueueAborted("QUEUE_ABORTED"))
+        for t in self._threads:
+            t.join(timeout=30)
+        for c in self._ctxs:
+            c.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- internals ------------------------------------------------------------------
+    def _run_now(self, sets: list) -> bool:
+        v, _ = self._call(self._main, [(False, [_wire(s) for s in sets])])
+        return self._verdict(int(v[0]))
+
+    @staticmethod
+    def _verdict(code: int) -> bool:
+        if code < 0:
+            raise BlsError(ERROR_MESSAGES.get(-code, f"BLST_ERROR: {-code}"))
+        return code == 1
+
+    def _call(self, ctx: GpuContext, reqs):
+        """One bls_gpu_verify; raw and table pubkeys go in separate calls."""
+        def is_raw(req):
+            return any(isinstance(pk, (bytes, bytearray, memoryview)) for pk, _, _ in req[1])
+        groups = {}
+        for k, r in enumerate(reqs):
+            groups.setdefault(is_raw(r), []).append(k)
+        verdicts = [0] * len(reqs)
+        stats = None
+        for idx in groups.values():
+            v, stats = ctx.verify_packed(pack_requests([reqs[k] for k in idx]))
+            for k, x in zip(idx, v):
+                verdicts[k] = int(x)
+            if stats is not None:
+                self.metrics["batch_retries"] += stats.batch_retries
+                self.metrics["batch_sigs_success"] += stats.batch_sigs_success
+        return verdicts, stats
+
+    def _queue(self, sets: list, batchable: bool) -> _Job:
+        job = _Job([_wire(s) for s in sets], batchable, Future(), time.monotonic())
+        with self._cv:
+            if self._closed:
+                job.future.set_exception(QueueAborted("QUEUE_ABORTED"))
+                return job
+            if batchable:
+                if not self._buffer:
+                    self._buffer_first = time.monotonic()
+                self._buffer.append(job)
+                self._buffer_sigs += len(sets)
+                if self._buffer_sigs > MAX_BUFFERED_SIGS:
+                    self._flush_locked()
+            else:
+                self._jobs.append(job)
+            self._cv.notify_all()
+        return job
+
+    def _flush_locked(self):
+        self._jobs.extend(self._buffer)
+        self._buffer, self._buffer_sigs = [], 0
+
+    def _buffer_timer(self):
+        while True:
+            with self._cv:
+                if self._closed:
+                    return
+                if self._buffer and time.monotonic() - self._buffer_first >= MAX_BUFFER_WAIT_MS / 1e3:
+                    self._flush_locked()
+                    self._cv.notify_all()
+                wait = MAX_BUFFER_WAIT_MS / 1e3
+                if self._buffer:
+                    wait = max(0.0, self._buffer_first + MAX_BUFFER_WAIT_MS / 1e3 - time.monotonic())
+                self._cv.wait(timeout=wait if self._buffer else 0.05)
+
+    def _prepare_work(self) -> list:
+        """prepareWork (index.ts:385-400): take jobs up to max_sets_per_call sets."""
+        jobs, total = [], 0
+        while self._jobs and total < self.max_sets_per_call:
+            j = self._jobs.pop(0)
+            jobs.append(j)
+            total += len(j.sets)
+        return jobs
+
+    def _worker(self, ctx: GpuContext):
+        while True:
+            with self._cv:
+                while not self._jobs and not self._closed:
+                    self._cv.wait(timeout=0.05)
+                if self._closed:
+                    return
+                jobs = self._prepare_work()
+            if not jobs:
+                continue
+            self.metrics["jobs_started"] += len(jobs)
+            self.metrics["sig_sets_started"] += sum(len(j.sets) for j in jobs)
+            try:
+                verdicts, _ = self._call(ctx, [(j.batchable, j.sets) for j in jobs])
+            except Exception as e:  # noqa: BLE001 - reject every job of the call
+                for j in jobs:
+                    j.future.set_exception(e)
+                continue
+            for j, code in zip(jobs, verdicts):
+                try:
+                    j.future.set_result(self._verdict(code))
+                    self.metrics["success_sig_sets"] += len(j.sets)
+                except BlsError as e:
+                    j.future.set_exception(e)
+                    self.metrics["error_sig_sets"] += len(j.sets)

@@ -2,7 +2,7 @@
 # One GPU call: parity tests, Fp-product and cooperative-program probes, short bench.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 120 python -u tools/fpm_probe.py > gpurun_out/fpm_probe.log 2>&1 || { echo "fpm probe failed"; cat gpurun_out/fpm_probe.log; exit 1; }
 cat gpurun_out/fpm_probe.log
