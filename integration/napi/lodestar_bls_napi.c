@@ -1,0 +1,211 @@
+/*
+ * Thin N-API addon over the C-ABI of include/lodestar_bls.h: what Lodestar's
+ * `GpuBlsVerifier` (integration/js/gpuBlsVerifier.js) loads in place of the
+ * @chainsafe/blst worker pool (beacon-node/src/chain/bls/multithread/index.ts).
+ *
+ *   init(device) -> handle
+ *   loadPubkeys(handle, Uint8Array pks, pkLen) -> Int32Array codes
+ *   verify(handle, {reqSetOffsets, reqBatchable, messages, signatures,
+ *                   setPkOffsets?, pkIndices?, pubkeys?, signatureLens?, seed?})
+ *          -> Promise<Int32Array verdicts>   (1 valid, 0 invalid, -code error)
+ *   close(handle)
+ *
+ * verify runs bls_gpu_verify on a libuv worker thread (napi_async_work): the JS
+ * main thread never blocks on the GPU.  Input buffers are referenced until the
+ * call completes (the library copies them into pinned staging at the start).
+ *
+ * Build (no node-gyp needed):
+ *   gcc -O2 -shared -fPIC -I/usr/include/node -I include integration/napi/lodestar_bls_napi.c \
+ *       -L lodestar_amd/_native -llodestar_bls -Wl,-rpath,'$ORIGIN' -o lodestar_amd/_native/lodestar_bls.node
+ */
+#define NAPI_VERSION 4
+#include <node_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "lodestar_bls.h"
+
+#define CHECK(env, call)                                            \
+  do {                                                              \
+    if ((call) != napi_ok) {                                        \
+      napi_throw_error((env), NULL, "lodestar_bls: N-API failure"); \
+      return NULL;                                                  \
+    }                                                               \
+  } while (0)
+
+static napi_value js_init(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int32_t dev = 0;
+  if (argc > 0) CHECK(env, napi_get_value_int32(env, argv[0], &dev));
+  bls_gpu_ctx* ctx = NULL;
+  if (bls_gpu_init(dev, &ctx) != 0 || !ctx) {
+    napi_throw_error(env, NULL, "bls_gpu_init failed (no HIP device?)");
+    return NULL;
+  }
+  napi_value ext;
+  CHECK(env, napi_create_external(env, ctx, NULL, NULL, &ext));
+  return ext;
+}
+
+static bls_gpu_ctx* get_ctx(napi_env env, napi_value v) {
+  void* p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
+  return (bls_gpu_ctx*)p;
+}
+
+static napi_value js_close(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_gpu_ctx* ctx = get_ctx(env, argv[0]);
+  if (ctx) bls_gpu_close(ctx);
+  return NULL;
+}
+
+/* typed array / buffer data pointer and byte length (NULL for undefined / null) */
+static int view_of(napi_env env, napi_value v, void** data, size_t* bytes) {
+  napi_valuetype t;
+  *data = NULL;
+  *bytes = 0;
+  if (napi_typeof(env, v, &t) != napi_ok) return -1;
+  if (t == napi_undefined || t == napi_null) return 0;
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (is_ta) {
+    napi_typedarray_type tt;
+    size_t len, off;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &tt, &len, data, &ab, &off) != napi_ok) return -1;
+    size_t el = (tt == napi_uint32_array || tt == napi_int32_array) ? 4 : 1;
+    *bytes = len * el;
+    return 0;
+  }
+  return napi_get_buffer_info(env, v, data, bytes) == napi_ok ? 0 : -1;
+}
+
+static napi_value js_load_pubkeys(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_gpu_ctx* ctx = get_ctx(env, argv[0]);
+  void* pks;
+  size_t bytes;
+  uint32_t pk_len = 48;
+  if (!ctx || view_of(env, argv[1], &pks, &bytes)) {
+    napi_throw_type_error(env, NULL, "loadPubkeys(handle, Uint8Array, pkLen)");
+    return NULL;
+  }
+  if (argc > 2) CHECK(env, napi_get_value_uint32(env, argv[2], &pk_len));
+  uint32_t n = (uint32_t)(bytes / pk_len);
+  napi_value ab, out;
+  void* codes;
+  CHECK(env, napi_create_arraybuffer(env, 4 * (size_t)(n ? n : 1), &codes, &ab));
+  CHECK(env, napi_create_typedarray(env, napi_int32_array, n, ab, 0, &out));
+  if (bls_gpu_load_pubkeys(ctx, (const uint8_t*)pks, n, pk_len, (int32_t*)codes) < 0) {
+    napi_throw_error(env, NULL, bls_gpu_last_error(ctx));
+    return NULL;
+  }
+  return out;
+}
+
+typedef struct {
+  bls_gpu_ctx* ctx;
+  bls_batch batch;
+  napi_ref keep;          /* the request object: keeps the input buffers alive */
+  int32_t* verdicts;
+  int rc;
+  napi_deferred deferred;
+  napi_async_work work;
+} verify_job;
+
+static void verify_execute(napi_env env, void* data) {
+  (void)env;
+  verify_job* j = (verify_job*)data;
+  j->rc = bls_gpu_verify(j->ctx, &j->batch, j->verdicts, NULL);
+}
+
+static void verify_complete(napi_env env, napi_status status, void* data) {
+  verify_job* j = (verify_job*)data;
+  if (status != napi_ok || j->rc != 0) {
+    napi_value msg, err;
+    napi_create_string_utf8(env, j->rc ? bls_gpu_last_error(j->ctx) : "verify cancelled", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, j->deferred, err);
+  } else {
+    napi_value ab, out;
+    void* dst;
+    uint32_t n = j->batch.n_reqs;
+    napi_create_arraybuffer(env, 4 * (size_t)(n ? n : 1), &dst, &ab);
+    memcpy(dst, j->verdicts, 4 * (size_t)n);
+    napi_create_typedarray(env, napi_int32_array, n, ab, 0, &out);
+    napi_resolve_deferred(env, j->deferred, out);
+  }
+  napi_delete_reference(env, j->keep);
+  napi_delete_async_work(env, j->work);
+  free(j->verdicts);
+  free(j);
+}
+
+static int prop(napi_env env, napi_value obj, const char* name, void** data, size_t* bytes) {
+  napi_value v;
+  if (napi_get_named_property(env, obj, name, &v) != napi_ok) return -1;
+  return view_of(env, v, data, bytes);
+}
+
+static napi_value js_verify(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_gpu_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx || argc < 2) {
+    napi_throw_type_error(env, NULL, "verify(handle, request)");
+    return NULL;
+  }
+  verify_job* j = (verify_job*)calloc(1, sizeof(verify_job));
+  j->ctx = ctx;
+  void *ro, *rb, *msg, *sig, *spo, *pki, *pks, *sl, *seed;
+  size_t nro, nrb, nmsg, nsig, nspo, npki, npks, nsl, nseed;
+  if (prop(env, argv[1], "reqSetOffsets", &ro, &nro) || prop(env, argv[1], "reqBatchable", &rb, &nrb) ||
+      prop(env, argv[1], "messages", &msg, &nmsg) || prop(env, argv[1], "signatures", &sig, &nsig) ||
+      prop(env, argv[1], "setPkOffsets", &spo, &nspo) || prop(env, argv[1], "pkIndices", &pki, &npki) ||
+      prop(env, argv[1], "pubkeys", &pks, &npks) || prop(env, argv[1], "signatureLens", &sl, &nsl) ||
+      prop(env, argv[1], "seed", &seed, &nseed) || nro < 4) {
+    free(j);
+    napi_throw_type_error(env, NULL, "verify: bad request object");
+    return NULL;
+  }
+  j->batch.n_reqs = (uint32_t)(nro / 4 - 1);
+  j->batch.n_sets = ((const uint32_t*)ro)[j->batch.n_reqs];
+  j->batch.req_set_offsets = (const uint32_t*)ro;
+  j->batch.req_batchable = (const uint8_t*)rb;
+  j->batch.messages = (const uint8_t*)msg;
+  j->batch.signatures = (const uint8_t*)sig;
+  j->batch.set_pk_offsets = (const uint32_t*)spo;
+  j->batch.pk_indices = (const uint32_t*)pki;
+  j->batch.pubkeys = (const uint8_t*)pks;
+  j->batch.signature_lens = (const uint32_t*)sl;
+  j->batch.seed = nseed >= 32 ? (const uint8_t*)seed : NULL;
+  j->verdicts = (int32_t*)calloc(j->batch.n_reqs ? j->batch.n_reqs : 1, 4);
+  napi_value promise, name;
+  CHECK(env, napi_create_reference(env, argv[1], 1, &j->keep));
+  CHECK(env, napi_create_promise(env, &j->deferred, &promise));
+  CHECK(env, napi_create_string_utf8(env, "lodestar_bls_verify", NAPI_AUTO_LENGTH, &name));
+  CHECK(env, napi_create_async_work(env, NULL, name, verify_execute, verify_complete, j, &j->work));
+  CHECK(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+static napi_value module_init(napi_env env, napi_value exports) {
+  napi_property_descriptor d[] = {
+      {"init", NULL, js_init, NULL, NULL, NULL, napi_default, NULL},
+      {"close", NULL, js_close, NULL, NULL, NULL, napi_default, NULL},
+      {"loadPubkeys", NULL, js_load_pubkeys, NULL, NULL, NULL, napi_default, NULL},
+      {"verify", NULL, js_verify, NULL, NULL, NULL, napi_default, NULL},
+  };
+  napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, module_init)

@@ -96,7 +96,7 @@ def build_hostsim(verbose: bool = True) -> Path:
     hdr = _headers_digest()
     key = hashlib.sha256(hdr.encode() + src.read_bytes()).hexdigest()[:16]
     stamp = out.with_suffix(".stamp")
-    if out.exists() and out.with_name("coop_programs.json").exists() and stamp.exists() and stamp.read_text() == key:
+    if out.exists() and stamp.exists() and stamp.read_text() == key:
         return out
     cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-DBLS_COUNT_OPS", "-I", str(CSRC), "-I",
            str(ROOT / "include"), "-o", str(out), str(src)]
@@ -107,6 +107,28 @@ def build_hostsim(verbose: bool = True) -> Path:
     return out
 
 
+def build_napi(verbose: bool = True) -> Path | None:
+    """N-API addon (integration/napi/lodestar_bls_napi.c) over the C-ABI, next to the
+    library; skipped when the Node headers are absent."""
+    hdr_dir = Path("/usr/include/node")
+    if not (hdr_dir / "node_api.h").exists():
+        return None
+    src = ROOT / "integration" / "napi" / "lodestar_bls_napi.c"
+    out = OUT_DIR / "lodestar_bls.node"
+    key = hashlib.sha256(src.read_bytes() + (ROOT / "include" / "lodestar_bls.h").read_bytes()).hexdigest()[:16]
+    stamp = OUT_DIR / ".napi_stamp"
+    if out.exists() and stamp.exists() and stamp.read_text() == key:
+        return out
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-I", str(hdr_dir), "-I", str(ROOT / "include"), str(src),
+           "-L", str(OUT_DIR), "-llodestar_bls", "-Wl,-rpath,$ORIGIN", "-o", str(out)]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    stamp.write_text(key)
+    return out
+
+
 if __name__ == "__main__":
     build(jobs=int(sys.argv[1]) if len(sys.argv) > 1 else None)
+    build_napi()
     build_hostsim()

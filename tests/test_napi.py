@@ -1,0 +1,47 @@
+"""The N-API addon (integration/napi/lodestar_bls_napi.c) and the JS GpuBlsVerifier
+(integration/js/gpuBlsVerifier.js): the reference's pool e2e test
+(beacon-node/test/e2e/chain/bls/multithread.test.ts) run under Node against the GPU."""
+from __future__ import annotations
+
+import hashlib
+import json
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+ADDON = ROOT / "lodestar_amd" / "_native" / "lodestar_bls.node"
+NODE = shutil.which("node")
+
+pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node or the N-API addon is absent")
+
+
+def test_addon_exports():
+    code = ("const a = require(process.argv[1]);"
+            "console.log(JSON.stringify(['init','close','loadPubkeys','verify'].map(k => typeof a[k])))")
+    out = subprocess.run([NODE, "-e", code, str(ADDON)], capture_output=True, text=True, timeout=60, check=True)
+    assert json.loads(out.stdout) == ["function"] * 4
+
+
+@pytest.mark.gpu
+def test_js_pool_matches_reference_tests(gpu, golden, oracle, tmp_path):
+    sks = [oracle.interop_secret_key(i).to_bytes(32, "big") for i in range(3)]
+    msgs = [hashlib.sha256(b"napi%d" % i).digest() for i in range(3)]
+    sigs = gpu.sign(b"".join(sks), b"".join(msgs))
+    data = {"pubkeys48": "".join(golden["kat2_interop_pubkeys"]),
+            "sets": [{"idx": i, "msg": msgs[i].hex(), "sig": sigs[i].tobytes().hex()} for i in range(3)]}
+    f = tmp_path / "sets.json"
+    f.write_text(json.dumps(data))
+    out = subprocess.run([NODE, str(ROOT / "integration" / "js" / "poolTest.js"), str(f)], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["chunkify"] == [[[0]], [[0, 1]], [[0, 1, 2]], [[0, 1, 2, 3]], [[0, 1, 2, 3, 4]],
+                             [[0, 1, 2], [3, 4, 5]], [[0, 1, 2, 3], [4, 5, 6]], [[0, 1, 2, 3], [4, 5, 6, 7]]]
+    for k in ("sync", "async", "batched", "mainThread", "firstInvalidOthers"):
+        assert r[k] == [True] * 8, k
+    assert "BLST_INVALID_SIZE" in r["firstInvalid"]
+    assert r["wrongMessage"] is False
+    assert r["empty"] == "Empty signature set"
