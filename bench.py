@@ -166,12 +166,9 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     if failures:
         raise SystemExit("verification failed inside the timed region")
-    if dist is not None:
-        import torch
+    from lodestar_amd.shard import global_throughput
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    value, elapsed = global_throughput(args.sets * args.steps, elapsed, dist, device=f"cuda:{local_rank}")
 
     # p50 latency of one 128-set non-batchable call (cfg1 shape)
     lat = []
@@ -191,8 +188,6 @@ def main() -> None:
     peak_rate, _ = gpu.mad_peak()
     peak = peak_rate / 1e12
 
-    total_sets = args.sets * args.steps * world
-    value = total_sets / elapsed
     if rank == 0:
         out = {
             "metric": "BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch",
