@@ -64,6 +64,7 @@ typedef struct bls_stats {
   uint32_t batch_sigs_success; /* sets accepted by a successful batch */
   uint32_t n_chunks;           /* batchable chunks (chunkifyMaximizeChunkSize(reqs, 16)) */
   uint32_t n_individual;       /* requests verified on their own */
+  uint32_t n_flagged;          /* sets finished by the exact single-lane path */
   double device_ms;            /* device time of the call (HIP events) */
   double stage_ms[8];          /* per stage: h2d, pk, pre (SSWU + sig decode), pset, exact, -, status+chunk, individual */
 } bls_stats;

@@ -56,6 +56,6 @@ async function main() {
 }
 
 main().catch((e) => {
-  console.error(e);
+  console.error("poolTest failed:", e && e.message, e && e.stack);
   process.exit(1);
 });

@@ -20,6 +20,7 @@
  */
 #define NAPI_VERSION 4
 #include <node_api.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -130,7 +131,10 @@ static void verify_complete(napi_env env, napi_status status, void* data) {
   verify_job* j = (verify_job*)data;
   if (status != napi_ok || j->rc != 0) {
     napi_value msg, err;
-    napi_create_string_utf8(env, j->rc ? bls_gpu_last_error(j->ctx) : "verify cancelled", NAPI_AUTO_LENGTH, &msg);
+    char text[640];
+    snprintf(text, sizeof(text), "bls_gpu_verify failed (rc %d, status %d): %s", j->rc, (int)status,
+             j->rc ? bls_gpu_last_error(j->ctx) : "cancelled");
+    napi_create_string_utf8(env, text, NAPI_AUTO_LENGTH, &msg);
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, j->deferred, err);
   } else {

@@ -77,6 +77,7 @@ class BlsStats(ctypes.Structure):
         ("batch_sigs_success", ctypes.c_uint32),
         ("n_chunks", ctypes.c_uint32),
         ("n_individual", ctypes.c_uint32),
+        ("n_flagged", ctypes.c_uint32),
         ("device_ms", ctypes.c_double),
         ("stage_ms", ctypes.c_double * 8),
     ]

@@ -137,17 +137,19 @@ __device__ __forceinline__ uint32_t k20p_limb(int i) {  // 2^20 * p, 13 limbs
   return t[i];
 }
 
-// canonical (sum + extra) mod p of the accumulator; extra < 2^20 (the +1s of
-// the negated terms, see coop_lin)
+// (sum + extra) mod p of the accumulator as a value in [0, 3p) (the interpreter's
+// lazy representation); extra < 2^20 (the +1s of the negated terms, see coop_lin)
 __device__ __forceinline__ Fp acc_reduce(Acc13 a, uint32_t extra) {
   uint32_t k20p[13];
 #pragma unroll
   for (int i = 0; i < 13; ++i) k20p[i] = k20p_limb(i);
   k20p[0] += extra;          // 0xaab00000 + extra: no carry
   asm_acc_add13(a.l, k20p);  // now 0 <= a < 2^21 p
-  // q ~ a / p from the top 96 bits in double precision (error < 1)
+  // q ~ a / p from the top 96 bits in double precision (|error| < 1); q - 1 makes
+  // a - (q - 1) p land in [0, 3p)
   double d = (double)a.l[12] * 18446744073709551616.0 + (double)a.l[11] * 4294967296.0 + (double)a.l[10];
   uint32_t q = (uint32_t)(d * 0x1.3b06ba5e7993dp-61);
+  q = q > 0u ? q - 1u : 0u;
   uint32_t qp[13], carry = 0;
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
@@ -156,18 +158,23 @@ __device__ __forceinline__ Fp acc_reduce(Acc13 a, uint32_t extra) {
     carry = (uint32_t)(v >> 32);
   }
   qp[12] = carry;
-  asm_acc_sub13(a.l, qp);  // a - q p in [-p, 2p)
-  // a < 0 -> + p ; a >= p -> - p
-  const uint32_t pl[12] = {BLS_P_LIMBS};
-  Fp lo, up, dn;
+  asm_acc_sub13(a.l, qp);
+  Fp r;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) lo.l[i] = a.l[i];
-  const bool negative = (int32_t)a.l[12] < 0;
-  asm_add12(up.l, lo.l, pl);
-  const uint32_t bb = asm_sub12(dn.l, lo.l, pl);
-  const bool ge_p = !negative && bb == 0;
-  return negative ? up : (ge_p ? dn : lo);
+  for (int i = 0; i < 12; ++i) r.l[i] = a.l[i];
+  return r;
 }
+
+// canonical form of a lazy value x < 3p
+__device__ __forceinline__ Fp fp_canon3(const Fp& x) {
+  const uint32_t pl[12] = {BLS_P_LIMBS};
+  Fp d1, d2;
+  const uint32_t b1 = asm_sub12(d1.l, x.l, pl);
+  const uint32_t b2 = asm_sub12(d2.l, d1.l, pl);
+  return b1 ? x : (b2 ? d1 : d2);
+}
+
+__device__ __forceinline__ bool fp_is_zero_lazy(const Fp& x) { return fp_is_zero(fp_canon3(x)); }
 
 // Wave-uniform max of n over the active lanes (n <= 8)
 __device__ __forceinline__ int coop_wave_max_terms(int n) {
@@ -219,10 +226,14 @@ __device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t 
 #pragma unroll
         for (int i = 0; i < 12; ++i) t[i] = mid[i] ^ mask;
         t[12] = c12 ^ mask;
-      } else {
+      } else if (__any(mask != 0u)) {
 #pragma unroll
         for (int i = 0; i < 12; ++i) t[i] = x.l[i] ^ mask;
         t[12] = mask;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) t[i] = x.l[i];
+        t[12] = 0u;
       }
       asm_acc_add13(acc.l, t);
     }
@@ -261,13 +272,13 @@ __device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* fra
     Fp r = fp_zero();
     if (op.kind != 0) {
       r = coop_lin(op.a, op.ca, op.na, slots);
-      if (op.kind == 1) r = fp_mul_inl(r, coop_lin(op.b, op.cb, op.nb, slots));
+      if (op.kind == 1) r = fp_mul_lazy(r, coop_lin(op.b, op.cb, op.nb, slots));
     }
     if (TIMED && lane == 0) stamps[2 * s + 1] = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if (op.kind != 0) {
       if (op.out == COOP_OUT_ZCHECK) {
-        if (fp_is_zero(r)) *flag = 1u;
+        if (fp_is_zero_lazy(r)) *flag = 1u;
       } else {
         lds_store_fp(slots, op.out, r);
       }
@@ -291,7 +302,7 @@ __device__ __forceinline__ void coop_stage_consts(const CoopEnv& env, Fp* cbank)
 
 // lane 0 inverts frame[in] into frame[out]; the whole block waits
 __device__ __forceinline__ void coop_invert(Fp* frame, int in, int out) {
-  if (threadIdx.x == 0) lds_store_fp(frame, out, fp_inv_gcd(lds_load_fp(frame, in)));
+  if (threadIdx.x == 0) lds_store_fp(frame, out, fp_inv_gcd(fp_canon3(lds_load_fp(frame, in))));
   __syncthreads();
 }
 
@@ -303,8 +314,11 @@ __device__ __forceinline__ void coop_load(Fp* frame, int slot, const Fp* src, in
 
 __device__ __forceinline__ bool coop_is_zero(const Fp* frame, int slot, int n) {
   bool z = true;
-  for (int k = 0; k < n; ++k) z = z && fp_is_zero(lds_load_fp(frame, slot + k));
+  for (int k = 0; k < n; ++k) z = z && fp_is_zero_lazy(lds_load_fp(frame, slot + k));
   return z;
 }
+
+// canonical value of a frame slot (for export to global memory / exact compares)
+__device__ __forceinline__ Fp coop_get(const Fp* frame, int slot) { return fp_canon3(lds_load_fp(frame, slot)); }
 
 }  // namespace bls

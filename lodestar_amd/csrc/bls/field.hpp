@@ -282,7 +282,10 @@ __device__ __forceinline__ void bls_col_add(uint64_t& lo, uint32_t& hi, uint64_t
 // block; the reduction then adds m_i * p into columns i..i+11, where only
 // m_i = col_i * (-p^-1) and the carry col_i >> 64-bit into col_{i+1} are on the
 // dependency chain.  288 products, 2 instructions each.
-__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) {
+// LAZY: inputs < 3p, output < 2p (no final subtraction; 9p^2/R + p < 2p since
+// p < R/9.8) -- the cooperative interpreter's representation.  Otherwise canonical.
+template <bool LAZY>
+__device__ __forceinline__ Fp fp_mul_cols(const Fp& a, const Fp& b) {
   uint64_t L[24];
   uint32_t H[24];
 #pragma unroll
@@ -313,8 +316,55 @@ __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) {
     bls_col_add(L[k + 1], H[k + 1], c);
   }
   u.l[11] = (uint32_t)L[23];
+  return LAZY ? u : fp_reduce_once(u);
+}
+// Montgomery square: 66 cross products (doubled) + 12 squares + the 144-product
+// reduction = 222 multiply-adds instead of 288.
+__device__ __forceinline__ Fp fp_sqr_cols(const Fp& a) {
+  uint64_t L[24];
+  uint32_t H[24];
+#pragma unroll
+  for (int k = 0; k < 24; ++k) {
+    L[k] = 0;
+    H[k] = 0;
+  }
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    int j = i + 1;
+#pragma unroll
+    for (; j + 3 < 12; j += 4) BLS_MAC4(L, H, i + j, a.l[i], a.l[j], a.l[j + 1], a.l[j + 2], a.l[j + 3], "v");
+#pragma unroll
+    for (; j < 12; ++j) bls_mac(L[i + j], H[i + j], a.l[i], a.l[j]);
+  }
+#pragma unroll
+  for (int k = 1; k < 23; ++k) {  // double the cross-product columns
+    H[k] = (H[k] << 1) | (uint32_t)(L[k] >> 63);
+    L[k] <<= 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) bls_mac(L[2 * i], H[2 * i], a.l[i], a.l[i]);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint32_t m = (uint32_t)L[i] * BLS_NP0;
+    BLS_MAC4(L, H, i, m, p_limb(0), p_limb(1), p_limb(2), p_limb(3), "s");
+    const uint64_t c = (L[i] >> 32) | ((uint64_t)H[i] << 32);
+    bls_col_add(L[i + 1], H[i + 1], c);
+    BLS_MAC4(L, H, i + 4, m, p_limb(4), p_limb(5), p_limb(6), p_limb(7), "s");
+    BLS_MAC4(L, H, i + 8, m, p_limb(8), p_limb(9), p_limb(10), p_limb(11), "s");
+  }
+  Fp u;
+#pragma unroll
+  for (int k = 12; k < 23; ++k) {
+    u.l[k - 12] = (uint32_t)L[k];
+    const uint64_t c = (L[k] >> 32) | ((uint64_t)H[k] << 32);
+    bls_col_add(L[k + 1], H[k + 1], c);
+  }
+  u.l[11] = (uint32_t)L[23];
   return fp_reduce_once(u);
 }
+BLS_NOINLINE Fp fp_sqr_dev(Fp a) { return fp_sqr_cols(a); }
+__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul_cols<false>(a, b); }
+__device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cols<true>(a, b); }
 BLS_NOINLINE Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
 #else
 // Host build (test harness): Montgomery product a*b/R mod p, CIOS with the no-carry
@@ -348,9 +398,14 @@ BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
   return fp_reduce_once(r);
 }
 BLS_HD Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul(a, b); }
+BLS_HD Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul(a, b); }
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+BLS_HD Fp fp_sqr(const Fp& a) { return fp_sqr_dev(a); }
+#else
 BLS_HD Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }
+#endif
 
 BLS_HD Fp fp_to_mont(const Fp& a) { return fp_mul(a, c_r2()); }
 
@@ -363,10 +418,30 @@ BLS_HD Fp fp_from_mont(const Fp& a) {
 // a^e for an exponent given as a limb accessor (wave-uniform, MSB first).
 template <uint32_t (*E)(int), int BITS>
 BLS_HD Fp fp_pow_const(const Fp& a) {
-  Fp r = a;  // top bit of every exponent used here is 1
-  for (int i = BITS - 2; i >= 0; --i) {
-    r = fp_sqr(r);
-    if ((E(i >> 5) >> (i & 31)) & 1u) r = fp_mul(r, a);
+  // sliding window of width 4 over the fixed exponent, odd powers a, a^3, .., a^15
+  Fp tab[8];
+  tab[0] = a;
+  const Fp a2 = fp_sqr(a);
+  for (int k = 1; k < 8; ++k) tab[k] = fp_mul(tab[k - 1], a2);
+  Fp r = a;
+  bool started = false;
+  int i = BITS - 1;
+  while (i >= 0) {
+    if (!((E(i >> 5) >> (i & 31)) & 1u)) {
+      r = fp_sqr(r);
+      --i;
+      continue;
+    }
+    int j = i - 3 < 0 ? 0 : i - 3;
+    while (!((E(j >> 5) >> (j & 31)) & 1u)) ++j;
+    uint32_t val = 0;
+    for (int k = i; k >= j; --k) {
+      val = (val << 1) | ((E(k >> 5) >> (k & 31)) & 1u);
+      if (started) r = fp_sqr(r);
+    }
+    r = started ? fp_mul(r, tab[val >> 1]) : tab[val >> 1];
+    started = true;
+    i = j - 1;
   }
   return r;
 }

@@ -57,6 +57,7 @@ struct PipeBufs {
   int32_t* req_status;
   Fp* q;               // n_sets * 8: the two SSWU points on E2' (x.c0, x.c1, y.c0, y.c1) per set
   uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
+  uint32_t* flag_count;  // 1 word: sets flagged by the cooperative kernel (GPU path)
   // outputs
   int32_t* chunk_ok;       // n_chunks: 1 ok, 0 failed (retry)
   int32_t* indiv_verdict;  // n_indiv: 1 / 0 / -code

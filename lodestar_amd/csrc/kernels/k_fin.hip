@@ -27,8 +27,8 @@ __device__ bool fin_finish(const CoopEnv& env, FinShared& sh) {
   coop_run(env, env.fin_fe1, sh.frame, sh.cbank, &sh.flag);
   coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
   coop_run(env, env.fin_fe2, sh.frame, sh.cbank, &sh.flag);
-  bool one = fp_eq(lds_load_fp(sh.frame, FIN_F), c_one());
-  for (int k = 1; k < 12; ++k) one = one && fp_is_zero(lds_load_fp(sh.frame, FIN_F + k));
+  bool one = fp_eq(coop_get(sh.frame, FIN_F), c_one());
+  for (int k = 1; k < 12; ++k) one = one && fp_is_zero(coop_get(sh.frame, FIN_F + k));
   return one;
 }
 

@@ -15,7 +15,8 @@
 // verifyMultipleSignatures ([ext] blst) for f_i.  A zero-checked exceptional
 // addition, an infinity signature or a flag from k_pre sends the set to k_exact
 // (pipeline.hpp stage_exact_set; kept out of this kernel so its registers and
-// stack do not lower this kernel's occupancy).
+// stack do not lower this kernel's occupancy).  Flagged sets are counted; the host
+// launches k_exact (and redoes status + chunks) only when the count is non-zero.
 #include "../launchers.hpp"
 
 using namespace bls;
@@ -32,6 +33,12 @@ __device__ __forceinline__ void pset_store_one(Fp12* dst) {
   if (threadIdx.x < 12) d[threadIdx.x] = threadIdx.x == 0 ? c_one() : fp_zero();
 }
 
+// hand the set to the exact path (lane 0)
+__device__ __forceinline__ void pset_flag(const PipeBufs& b, uint32_t i) {
+  b.set_flag[i] = 1u;
+  atomicAdd(b.flag_count, 1u);
+}
+
 __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
   __shared__ PsetShared sh;
   const uint32_t i = blockIdx.x;
@@ -41,7 +48,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
     return;
   }
   if (b.sig[i].inf || b.set_flag[i]) {
-    if (lane == 0) b.set_flag[i] = 1u;
+    if (lane == 0) pset_flag(b, i);
     return;
   }
   coop_stage_consts(env, sh.cbank);
@@ -64,7 +71,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
   }
   coop_run(env, env.pset_phase2, sh.frame, sh.cbank, &sh.flag);
   if (sh.flag) {
-    if (lane == 0) b.set_flag[i] = 1u;
+    if (lane == 0) pset_flag(b, i);
     return;
   }
   if (!coop_is_zero(sh.frame, PS_DIFF, 4)) {  // psi(sig) != [x] sig: not in G2
@@ -74,13 +81,13 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
   }
   coop_run(env, env.pset_norm2, sh.frame, sh.cbank, &sh.flag);
   if (sh.flag) {
-    if (lane == 0) b.set_flag[i] = 1u;
+    if (lane == 0) pset_flag(b, i);
     return;
   }
   coop_invert(sh.frame, PS_INV_IN, PS_INV_OUT);
   coop_run(env, env.pset_affine2, sh.frame, sh.cbank, &sh.flag);
   coop_run(env, env.pset_ml2, sh.frame, sh.cbank, &sh.flag);
-  if (lane < 12) reinterpret_cast<Fp*>(&b.f[i])[lane] = lds_load_fp(sh.frame, PS_F + lane);
+  if (lane < 12) reinterpret_cast<Fp*>(&b.f[i])[lane] = coop_get(sh.frame, PS_F + lane);
 }
 
 hipError_t launch_k_pset(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {

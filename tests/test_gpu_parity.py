@@ -221,6 +221,8 @@ def test_fp_mul_device_vs_bigint(gpu):
     vals = [0, 1, 2, P - 1, P - 2, (1 << 380), (1 << 381) % P, P // 2, P // 2 + 1]
     a = vals + [rng.randrange(P) for _ in range(500)]
     b = list(reversed(vals)) + [rng.randrange(P) for _ in range(500)]
+    sq = vals + [rng.randrange(P) for _ in range(200)]      # squares: the dedicated fp_sqr
+    a, b = a + sq, b + sq
     out = gpu.fp_mul_test(b"".join(x.to_bytes(48, "big") for x in a), b"".join(x.to_bytes(48, "big") for x in b))
     got = [int.from_bytes(out[48 * i: 48 * i + 48], "big") for i in range(len(a))]
     assert got == [(x * y) % P for x, y in zip(a, b)]
@@ -236,11 +238,12 @@ def test_exact_path_matches_cooperative_path(gpu, oracle, golden, table):
     for case in golden["sig_decode"]:                                       # decode / subgroup codes
         reqs.append((False, [(sets[0][0], sets[0][1], bytes.fromhex(case["bytes"]))]))
     pb = pack_requests(reqs)
-    v0, _ = gpu.verify_packed(pb)
+    v0, st0 = gpu.verify_packed(pb)
     try:
         gpu.set_debug_flags(1)
-        v1, _ = gpu.verify_packed(pb)
+        v1, st1 = gpu.verify_packed(pb)
     finally:
         gpu.set_debug_flags(0)
     assert list(v0) == list(v1)
+    assert st1.n_flagged >= 5 and st0.n_flagged < st1.n_flagged
     assert list(v0[:5]) == [1] * 5 and v0[5] == 0

@@ -438,6 +438,10 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                 else:
                     out, kind, a, b = 0xFFFE, 0, [], []
                 assert len(a) <= 8 and len(b) <= 8
+                # +-1 terms first, positive before negative: the interpreter skips the
+                # multiply / negate work for term positions no lane of the wave needs
+                a = sorted(a, key=lambda t: (abs(t[1]) != 1, t[1] < 0))
+                b = sorted(b, key=lambda t: (abs(t[1]) != 1, t[1] < 0))
                 def refs(lst):
                     r = [((FRAME + x[1]) if isinstance(x, tuple) else x) for x, _ in lst]
                     return r + [0] * (8 - len(r))
