@@ -57,6 +57,18 @@ def pset_products_per_set() -> float:
     return n + m["pset_phase2"] + m["pset_norm2"] + m["pset_affine2"] + m["pset_ml2"]
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"), key=lambda p: p.stat().st_mtime)
+    for p in reversed(files):
+        d = json.loads(p.read_text())
+        if kernel in d:
+            return int(d[kernel]["hbm_bytes_per_launch"]), p.name
+    return None, None
+
+
 def interop_sk(i: int) -> bytes:
     v = int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R_ORDER
     return v.to_bytes(32, "big")
@@ -186,6 +198,7 @@ def main() -> None:
     mads = fpm_set * MADS_PER_FPM * args.sets
     achieved = mads / (dom_ms * 1e-3) / 1e12
     peak_rate, _ = gpu.mad_peak()
+    traffic, traffic_src = pmc_traffic(dom)
     peak = peak_rate / 1e12
 
     if rank == 0:
@@ -209,7 +222,9 @@ def main() -> None:
             "p50_latency_ms_128": round(statistics.median(lat), 3),
             "stage_ms": {k: round(float(x), 3) for k, x in zip(STAGE_NAMES, stage_ms)},
             "roofline": {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
-                         "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5), "traffic": None,
+                         "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5), "traffic": traffic,
+                         "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                                         f"{traffic_src})" if traffic else None,
                          "work": f"{fpm_set:.0f} Fp products/set x {MADS_PER_FPM} MAD x {args.sets} sets "
                                  f"per launch, {dom_ms:.3f} ms/launch (HIP events)"},
         }
