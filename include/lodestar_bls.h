@@ -100,6 +100,26 @@ int64_t bls_gpu_load_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, u
  * verdicts: n_reqs int32 (see top of file).  stats nullable. */
 int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* batch, int32_t* verdicts, bls_stats* stats);
 
+/* Sharded call across GPUs (north_star "each GPU reduces its shard to
+ * an Fp12 partial, the partials are combined over RCCL/xGMI, and one final
+ * exponentiation follows").  The reference verifies one call as ONE random-scalar
+ * batch (maybeBatch.ts:18-25, blst verifyMultipleSignatures [ext]); here each rank
+ * holds a contiguous shard of the call's sets and computes
+ *     P_rank = prod_{i in shard} e(r_i pk_i, H(m_i)) e(-g1, r_i sig_i)   (Miller loops only)
+ * with r_i drawn from the call's shared seed at index set_index_base + i, so the
+ * scalars of all shards are distinct draws of one batch.  batch->seed must be set
+ * (the same 32 bytes on every rank).  out576 receives P_rank as 12 Fp (opaque device
+ * form: 12 x 48-byte Montgomery limbs; only bls_gpu_final_check reads it).  status:
+ * 0 if every set decoded, else -(code) of the first failing request in order -- the
+ * whole call then rejects (rule 2 of SURVEY §8a) and out576 is undefined.
+ * The shard must hold >= 1 set. */
+int bls_gpu_partial(bls_gpu_ctx* ctx, const bls_batch* batch, uint32_t set_index_base, uint8_t* out576,
+                    int32_t* status, bls_stats* stats);
+
+/* The combine step after the all-gather: *verdict = 1 iff FE(prod_k partials[k]) == 1,
+ * one final exponentiation for the whole call (n >= 1 partials of 576 bytes). */
+int bls_gpu_final_check(bls_gpu_ctx* ctx, const uint8_t* partials576, uint32_t n, int32_t* verdict);
+
 /* getAggregatedPubkey (chain/bls/utils.ts:5-16) for n_sets index lists over the device
  * table; out: n_sets * 96 bytes uncompressed (PointFormat.uncompressed, index.ts:126,160);
  * codes: n_sets (0 ok, BLS_CODE_EMPTY_AGGREGATE for an empty list). */

@@ -42,6 +42,7 @@ struct PipeBufs {
   const uint8_t* sigs;         // n_sets * 96
   const uint32_t* sig_lens;    // nullable
   const uint32_t* seed;        // 8 words
+  uint32_t scalar_base;        // set i draws r from index scalar_base + i (shards of one call, bls_gpu_partial)
   const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs
   const uint32_t* chunk_reqs;
   const uint32_t* indiv_reqs;  // n_indiv
@@ -136,7 +137,7 @@ BLS_HD void stage_h2c(const PipeBufs& b, uint32_t i) {
 
 BLS_HD void stage_scale(const PipeBufs& b, uint32_t i) {
   if (i >= b.n_sets) return;
-  uint64_t r = set_scalar(b.seed, i);
+  uint64_t r = set_scalar(b.seed, b.scalar_base + i);
   if (b.pk_status[i] == BLS_OK && b.sig_status[i] == BLS_OK) {
     b.rpk[i] = jac_mul_u64(b.pk[i], r);
     b.rsig[i] = aff_mul_u64(b.sig[i], r);
@@ -222,7 +223,7 @@ BLS_HD void stage_exact_set(const PipeBufs& b, uint32_t i) {
   uint32_t w[8];
   msg_words_from_bytes(b.msgs + 32ull * i, w);
   const G2A H = hash_to_g2(w);
-  const uint64_t r = set_scalar(b.seed, i);
+  const uint64_t r = set_scalar(b.seed, b.scalar_base + i);
   const G1J rpk = jac_mul_u64(b.pk[i], r);
   const G2J rsig = sig.inf ? jac_infinity<Fp2>() : aff_mul_u64(sig, r);
   b.f[i] = pair_set(rpk, H, rsig, sig.inf);

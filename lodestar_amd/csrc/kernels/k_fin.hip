@@ -75,6 +75,36 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
   if (threadIdx.x == 0) b.indiv_verdict[t] = ok ? 1 : 0;
 }
 
+// Product tree over Fp12 values (sharded calls): block k multiplies
+// in[k*FPROD_FAN .. min(n, (k+1)*FPROD_FAN)) into out[k].  With `verdict` non-null
+// (one block, n <= FPROD_FAN) it runs the final exponentiation of the product
+// instead and writes FE(prod) == 1.
+__global__ __launch_bounds__(COOP_LANES) void k_fprod(const Fp12* in, uint32_t n, Fp12* out, int32_t* verdict,
+                                                      CoopEnv env) {
+  __shared__ FinShared sh;
+  const uint32_t beg = blockIdx.x * FPROD_FAN;
+  const uint32_t end = beg + FPROD_FAN < n ? beg + FPROD_FAN : n;
+  fin_init(env, sh);
+  for (uint32_t k = beg; k < end; ++k) {
+    coop_load(sh.frame, k == beg ? FIN_F : FIN_G, reinterpret_cast<const Fp*>(&in[k]), 12);
+    if (k != beg) coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
+  }
+  if (verdict) {
+    const bool ok = fin_finish(env, sh);
+    if (threadIdx.x == 0) *verdict = ok ? 1 : 0;
+  } else if (threadIdx.x < 12) {
+    reinterpret_cast<Fp*>(&out[blockIdx.x])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
+  }
+}
+
+hipError_t launch_k_fprod(const Fp12* in, uint32_t n, Fp12* out, int32_t* verdict, const CoopEnv& env,
+                          hipStream_t s) {
+  const uint32_t blocks = verdict ? 1u : (n + FPROD_FAN - 1) / FPROD_FAN;
+  if (n == 0 || (verdict && n > FPROD_FAN)) return hipErrorInvalidValue;
+  k_fprod<<<blocks, COOP_LANES, 0, s>>>(in, n, out, verdict, env);
+  return hipGetLastError();
+}
+
 hipError_t launch_k_chunk_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
   k_chunk_coop<<<b.n_chunks, COOP_LANES, 0, s>>>(b, env);
   return hipGetLastError();

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
   if (lane >= 12 && lane < 15) lds_store_fp(sh.frame, PS_PK + lane - 12, reinterpret_cast<const Fp*>(&b.pk[i])[lane - 12]);
   if (lane == 0) sh.flag = 0;
   __syncthreads();
-  const uint64_t r = set_scalar(b.seed, i);
+  const uint64_t r = set_scalar(b.seed, b.scalar_base + i);
 
   coop_run(env, env.pset_prep, sh.frame, sh.cbank, &sh.flag);
   coop_run(env, env.pset_dbl_r, sh.frame, sh.cbank, &sh.flag);

@@ -28,4 +28,7 @@ hipError_t launch_k_chunk_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, 
 hipError_t launch_k_indiv_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_coop_probe(const bls::CoopEnv& env, bls::CoopProg pg, uint32_t blocks, uint32_t reps,
                                uint32_t* sink, uint64_t* stamps, hipStream_t s);
+#define FPROD_FAN 64u
+hipError_t launch_k_fprod(const bls::Fp12* in, uint32_t n, bls::Fp12* out, int32_t* verdict,
+                          const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);

@@ -142,7 +142,8 @@ class GpuContext:
         return codes[:n]
 
     # -- verification -------------------------------------------------------------
-    def verify_packed(self, pb: PackedBatch) -> tuple[np.ndarray, BlsStats]:
+    @staticmethod
+    def _batch_struct(pb: PackedBatch):
         keep = []
         b = BlsBatch()
         b.n_sets = pb.n_sets
@@ -158,11 +159,38 @@ class GpuContext:
         if pb.seed is not None:
             seed_buf = ctypes.create_string_buffer(bytes(pb.seed), 32)
             b.seed = ctypes.cast(seed_buf, ctypes.c_void_p)
+        keep.append(seed_buf)
+        return b, keep
+
+    def verify_packed(self, pb: PackedBatch) -> tuple[np.ndarray, BlsStats]:
+        b, _keep = self._batch_struct(pb)
         verdicts = np.zeros(max(pb.n_reqs, 1), dtype=np.int32)
         stats = BlsStats()
         rc = self.lib.bls_gpu_verify(self._h, ctypes.byref(b), _ptr(verdicts), ctypes.byref(stats))
         self._check(rc, "bls_gpu_verify")
         return verdicts[: pb.n_reqs], stats
+
+    def partial(self, pb: PackedBatch, set_index_base: int) -> tuple[bytes | None, int, BlsStats]:
+        """Miller-loop partial of this shard of a sharded call (bls_gpu_partial):
+        (576 opaque bytes or None on a decode error, status 0 / -code, stats)."""
+        if pb.seed is None:
+            raise ValueError("a sharded call needs the call's shared 32-byte seed")
+        b, _keep = self._batch_struct(pb)
+        out = np.zeros(576, dtype=np.uint8)
+        status = ctypes.c_int32(0)
+        stats = BlsStats()
+        rc = self.lib.bls_gpu_partial(self._h, ctypes.byref(b), set_index_base, _ptr(out), ctypes.byref(status),
+                                      ctypes.byref(stats))
+        self._check(rc, "bls_gpu_partial")
+        return (out.tobytes() if status.value == 0 else None), status.value, stats
+
+    def final_check(self, partials: list[bytes]) -> bool:
+        """FE(prod partials) == 1: the one final exponentiation of a sharded call."""
+        buf = _u8(b"".join(partials))
+        v = ctypes.c_int32(-1)
+        rc = self.lib.bls_gpu_final_check(self._h, _ptr(buf), len(partials), ctypes.byref(v))
+        self._check(rc, "bls_gpu_final_check")
+        return v.value == 1
 
     # -- standalone primitives (parity tests, fixtures) ---------------------------
     def aggregate_pubkeys(self, index_lists) -> tuple[list[bytes], np.ndarray]:

@@ -247,3 +247,167 @@ def test_exact_path_matches_cooperative_path(gpu, oracle, golden, table):
     assert list(v0) == list(v1)
     assert st1.n_flagged >= 5 and st0.n_flagged < st1.n_flagged
     assert list(v0[:5]) == [1] * 5 and v0[5] == 0
+
+
+# ---------------------------------------------------------------------------
+# one call sharded into Fp12 partials + one final exponentiation
+# ---------------------------------------------------------------------------
+def test_sharded_partials_final_check(gpu, oracle, table):
+    from lodestar_amd.shard import shard_bounds
+
+    seed = bytes(range(32))
+    sets = _sets(gpu, oracle, 10, tag=b"shard")
+    bounds = shard_bounds(len(sets), 3)
+
+    def partials(ss):
+        out = []
+        for beg, end in bounds:
+            p, st, _ = gpu.partial(pack_requests([(True, ss[beg:end])], seed=seed), beg)
+            assert st == 0
+            out.append(p)
+        return out
+
+    good = partials(sets)
+    assert gpu.final_check(good)
+    assert gpu.final_check(good[::-1])                    # the product is order-free
+    # the same call verified unsharded agrees
+    v, _ = gpu.verify_packed(pack_requests([(False, sets)], seed=seed))
+    assert v[0] == 1
+    # one invalid set (wrong message) in the last shard: the call fails, its shard is found
+    bad = list(sets)
+    bad[8] = (bad[8][0], _h(b"tampered"), bad[8][2])
+    ps = partials(bad)
+    assert not gpu.final_check(ps)
+    assert [gpu.final_check([p]) for p in ps] == [True, True, False]
+    # an undecodable signature rejects the call with its code
+    enc = list(sets)
+    enc[4] = (enc[4][0], enc[4][1], b"\x00" * 96)
+    beg, end = bounds[1]
+    p, st, _ = gpu.partial(pack_requests([(True, enc[beg:end])], seed=seed), beg)
+    assert p is None and st == -CODE_BAD_ENCODING
+
+
+def _sharded_gpu_rank(rank, world, port, sets, q):
+    import os
+
+    import torch.distributed as dist
+
+    from lodestar_amd.native import GpuContext
+    from lodestar_amd.shard import GpuPartialBackend, verify_call_sharded
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    with GpuContext(0) as gpu:
+        be = GpuPartialBackend(gpu)
+        for ss in sets:
+            out.append(verify_call_sharded(ss, bytes(32), be, dist))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_sharded_call_two_ranks(gpu, oracle):
+    """Two processes (gloo exchange of the 580-byte records; both ranks on cuda:0)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    sks = _keys(oracle, 6)
+    msgs = [_h(b"r2-%d" % i) for i in range(6)]
+    sigs = gpu.sign(b"".join(sks), b"".join(msgs))
+    raw = [oracle.g1_serialize(oracle.sk_to_pk(int.from_bytes(s, "big"))) for s in sks]
+    good = [(raw[i], msgs[i], sigs[i].tobytes()) for i in range(6)]
+    bad = good[:1] + [(raw[1], msgs[2], sigs[1].tobytes())] + good[2:]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad], q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert res[r][0] == (True, {"bad_shards": []})
+        assert res[r][1] == (False, {"bad_shards": [0]})
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs as parity cases (size-independent properties)
+# ---------------------------------------------------------------------------
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def _interop_sks(n):
+    return [int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R_ORDER for i in range(n)]
+
+
+@pytest.fixture(scope="module")
+def big_table():
+    """A separate context with a 65,536-key device table (interop keys), so the
+    session's `gpu` table stays as the other tests expect."""
+    from lodestar_amd.native import GpuContext
+
+    n = 65536
+    sks = _interop_sks(n)
+    ctx = GpuContext(0)
+    pks = ctx.sk_to_pk(b"".join(s.to_bytes(32, "big") for s in sks))
+    assert (ctx.load_pubkeys(pks.tobytes(), 48) == 0).all()
+    yield ctx, sks, pks
+    ctx.close()
+
+
+def test_cfg3_block_import_aggregates(big_table, oracle):
+    """cfg3: one block = 128 aggregate sets x 512 distinct pubkeys + the sync aggregate
+    x 512 (indices sampled without replacement; table of 65,536 keys instead of 1M),
+    verified as one call.  Aggregate signatures are made with the summed secret key
+    (sum_j sk_j H(m) = sum_j sig_j).  Valid -> true; one tampered set -> false; the
+    device aggregate pubkeys equal the oracle's for two sets."""
+    ctx, sks, _ = big_table
+    rng = np.random.default_rng(1)
+    n_sets, k = 129, 512
+    idx = [sorted(rng.choice(len(sks), size=k, replace=False).tolist()) for _ in range(n_sets)]
+    msgs = [_h(b"block%d" % i) for i in range(n_sets)]
+    agg_sks = [sum(sks[j] for j in ix) % R_ORDER for ix in idx]
+    sigs = ctx.sign(b"".join(s.to_bytes(32, "big") for s in agg_sks), b"".join(msgs))
+    sets = [(idx[i], msgs[i], sigs[i].tobytes()) for i in range(n_sets)]
+    v, _ = ctx.verify_packed(pack_requests([(False, sets)]))
+    assert v[0] == 1
+    bad = list(sets)
+    bad[77] = (idx[77][:-1], msgs[77], sigs[77].tobytes())       # one signer missing
+    v, _ = ctx.verify_packed(pack_requests([(False, bad), (True, sets[:64]), (True, sets[64:])]))
+    assert list(v) == [0, 1, 1]
+    outs, codes = ctx.aggregate_pubkeys([idx[0], idx[128]])
+    assert list(codes) == [0, 0]
+    for o, ix in zip(outs, (idx[0], idx[128])):
+        assert o == oracle.g1_serialize(oracle.sk_to_pk(sum(sks[j] for j in ix) % R_ORDER))
+
+
+def test_cfg4_range_sync_mixed_with_invalid(big_table):
+    """cfg4 at 1/64 scale on one GPU: 16,384 sets, 90% single / 10% aggregate (k=128),
+    1% invalid (half wrong message, half another key's signature, seed 2), grouped
+    into calls of 128 sets; each call's verdict equals the expected one."""
+    ctx, sks, _ = big_table
+    rng = np.random.default_rng(2)
+    n = 16384
+    is_agg = rng.random(n) < 0.10
+    idx = [sorted(rng.choice(len(sks), size=128, replace=False).tolist()) if a else [int(rng.integers(len(sks)))]
+           for a in is_agg]
+    msgs = [_h(b"range%d" % i) for i in range(n)]
+    sk_of = [sum(sks[j] for j in ix) % R_ORDER for ix in idx]
+    bad = set(rng.choice(n, size=n // 100, replace=False).tolist())
+    wrong_key = {i for i in bad if rng.random() < 0.5}
+    sign_sk = [sk_of[(i + 1) % n] if i in wrong_key else sk_of[i] for i in range(n)]
+    sigs = ctx.sign(b"".join(s.to_bytes(32, "big") for s in sign_sk), b"".join(msgs))
+    sets = []
+    for i in range(n):
+        m = _h(b"wrong%d" % i) if (i in bad and i not in wrong_key) else msgs[i]
+        sets.append((idx[i], m, sigs[i].tobytes()))
+    calls = [sets[c:c + 128] for c in range(0, n, 128)]
+    v, st = ctx.verify_packed(pack_requests([(False, c) for c in calls]))
+    expect = [0 if any(i in bad for i in range(c, c + 128)) else 1 for c in range(0, n, 128)]
+    assert list(v) == expect
+    assert 0 < sum(expect) < len(expect)
