@@ -36,6 +36,12 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+# One HIP stream per in-flight batch; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
+# queues (default 4 on this image), and streams sharing a queue serialise.  Give the
+# in-flight contexts their own queues (set before the HIP runtime initialises; the
+# box exports 4, so raise it rather than default it).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 STAGE_NAMES = ["h2d", "k_pk", "k_pre", "k_pset", "k_exact", "-", "k_status+k_chunk", "k_indiv"]
@@ -111,12 +117,12 @@ def cpu_baseline(sample_sets: int = 24) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=1024)
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=3, help="batches in flight per GPU (contexts/streams)")
+    ap.add_argument("--inflight", type=int, default=6, help="batches in flight per GPU (contexts/streams)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

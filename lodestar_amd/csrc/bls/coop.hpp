@@ -22,7 +22,8 @@ namespace bls {
 #define COOP_LANES 64
 #define COOP_FRAME 256
 #define COOP_OUT_ZCHECK 0xFFFFu
-#define COOP_OUT_NONE 0xFFFEu
+#define COOP_OUT_NONE 0xFFFEu   // lane idle (kind 0, never written)
+#define COOP_OUT_ZSET 0xFFF0u   // zero-check of packed set s >= 1: 0xFFF0 + s
 #define COOP_MAX_CONSTS 64
 
 struct CoopOp {  // 80 bytes, one per lane per step (tools/gen_coop.py:emit)
@@ -48,6 +49,24 @@ struct CoopLds {
 };
 static_assert(offsetof(CoopLds, cbank) == COOP_FRAME * sizeof(Fp), "constant bank must follow the frame");
 
+// LDS of a task whose programs were scheduled for a FRAME_N-slot frame (constants at
+// slot FRAME_N + k, tools/gen_coop.py:emit)
+template <int FRAME_N>
+struct CoopLdsN {
+  Fp frame[FRAME_N];
+  Fp cbank[COOP_MAX_CONSTS];
+  uint32_t flag;
+};
+
+#define COOP_FRAME2 512  // the 2-set packed programs (tools/gen_coop.py FRAME2)
+#define COOP_FRAME3 640  // the 3-set packed programs (tools/gen_coop.py FRAME3)
+
+// Programs of S sets packed in one wavefront (tools/gen_pset.py build_pset(S)):
+// add[(xb << S) | rmask], bit s of rmask = r bit of packed set s; add[0] unused
+struct CoopPsetN {
+  CoopProg prep, dbl_r, dbl_all, add[16], phase2, norm2, affine2, ml2;
+};
+
 // Programs of the finalisation frame ("fin", tools/gen_coop.py:build_fin)
 struct CoopEnv {
   const CoopOp* ops;
@@ -57,6 +76,7 @@ struct CoopEnv {
   // per-set frame (tools/gen_pset.py, kernels/k_pset.hip)
   CoopProg pset_prep, pset_dbl_r, pset_dbl_all, pset_add_x, pset_add_r, pset_add_xr, pset_phase2, pset_norm2,
       pset_affine2, pset_ml2;
+  CoopPsetN packed[2];  // [0]: 2 sets per wavefront, [1]: 3 sets
 };
 
 // fin frame registers
@@ -277,8 +297,8 @@ __device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* fra
     if (TIMED && lane == 0) stamps[2 * s + 1] = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if (op.kind != 0) {
-      if (op.out == COOP_OUT_ZCHECK) {
-        if (fp_is_zero_lazy(r)) *flag = 1u;
+      if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
+        if (fp_is_zero_lazy(r)) atomicOr(flag, op.out == COOP_OUT_ZCHECK ? 1u : 1u << (op.out - COOP_OUT_ZSET));
       } else {
         lds_store_fp(slots, op.out, r);
       }

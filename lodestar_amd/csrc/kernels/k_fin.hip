@@ -118,9 +118,9 @@ hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, hipStream_
 // field elements (timing of the interpreter; results discarded).
 __global__ __launch_bounds__(COOP_LANES) void k_coop_probe(CoopEnv env, CoopProg pg, uint32_t reps, uint32_t* sink,
                                                           uint64_t* stamps) {
-  __shared__ FinShared sh;
+  __shared__ CoopLdsN<COOP_FRAME3> sh;  // large enough for every program (1-, 2- and 3-set frames)
   coop_stage_consts(env, sh.cbank);
-  for (int k = threadIdx.x; k < COOP_FRAME; k += COOP_LANES) {
+  for (int k = threadIdx.x; k < COOP_FRAME3; k += COOP_LANES) {
     Fp v = fp_zero();
     for (int i = 0; i < 11; ++i) v.l[i] = (uint32_t)(k * 2654435761u + i * 40503u + blockIdx.x);
     lds_store_fp(sh.frame, k, v);

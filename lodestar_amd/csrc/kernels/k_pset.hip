@@ -90,7 +90,146 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
   if (lane < 12) reinterpret_cast<Fp*>(&b.f[i])[lane] = coop_get(sh.frame, PS_F + lane);
 }
 
+// S sets per wavefront (tools/gen_pset.py build_pset(S): set s at frame offset 92 s,
+// its zero-checks on flag bit s).  The same programs as k_pset scheduled jointly: the
+// narrow chains of one set leave most lanes idle, so further sets ride along at
+// almost no extra steps (r-chain and phase 2 unchanged; Miller loop 689 steps for
+// 2 sets, 935 for 3, vs 486 for 1).  A set that needs no programs (error status,
+// flagged) borrows the inputs of the first live set so every part of the frame holds
+// well-formed points; its results are dropped.  Controller decisions (program
+// choice, early exits) are wave-uniform.
+#define PSN_SLOTS 92
+
+template <int S, int FRAME_N>
+__global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
+  __shared__ CoopLdsN<FRAME_N> sh;
+  const CoopPsetN& pg = env.packed[S - 2];
+  const int lane = threadIdx.x;
+  const uint32_t i0 = (uint32_t)S * blockIdx.x;
+  bool live[S];
+  int first_live = -1;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const uint32_t i = i0 + s;
+    live[s] = false;
+    if (i >= b.n_sets) continue;
+    if (b.pk_status[i] != BLS_OK || b.sig_status[i] != BLS_OK || jac_is_inf(b.pk[i])) {
+      pset_store_one(&b.f[i]);
+    } else if (b.sig[i].inf || b.set_flag[i]) {
+      if (lane == 0) pset_flag(b, i);
+    } else {
+      live[s] = true;
+      if (first_live < 0) first_live = s;
+    }
+  }
+  if (first_live < 0) return;
+  uint32_t src[S];
+  uint64_t r[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    src[s] = i0 + (live[s] ? s : first_live);
+    r[s] = set_scalar(b.seed, b.scalar_base + src[s]);
+  }
+  coop_stage_consts(env, sh.cbank);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const uint32_t i = src[s], o = PSN_SLOTS * s;
+    if (lane < 8) lds_store_fp(sh.frame, o + PS_Q0 + lane, b.q[8ull * i + lane]);
+    if (lane >= 8 && lane < 12)
+      lds_store_fp(sh.frame, o + PS_SIG + lane - 8, reinterpret_cast<const Fp*>(&b.sig[i])[lane - 8]);
+    if (lane >= 12 && lane < 15)
+      lds_store_fp(sh.frame, o + PS_PK + lane - 12, reinterpret_cast<const Fp*>(&b.pk[i])[lane - 12]);
+  }
+  if (lane == 0) sh.flag = 0;
+  __syncthreads();
+
+  auto rbits = [&](int k) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) m |= (uint32_t)((r[s] >> k) & 1ull) << s;
+    return m;
+  };
+  coop_run(env, pg.prep, sh.frame, sh.cbank, &sh.flag);
+  coop_run(env, pg.dbl_r, sh.frame, sh.cbank, &sh.flag);
+  {
+    const uint32_t m = rbits(63);
+    if (m) coop_run(env, pg.add[m], sh.frame, sh.cbank, &sh.flag);
+  }
+  for (int k = 62; k >= 0; --k) {
+    coop_run(env, pg.dbl_all, sh.frame, sh.cbank, &sh.flag);
+    const uint32_t m = (uint32_t)((PS_X_ABS >> k) & 1ull) << S | rbits(k);
+    if (m) coop_run(env, pg.add[m], sh.frame, sh.cbank, &sh.flag);
+  }
+  coop_run(env, pg.phase2, sh.frame, sh.cbank, &sh.flag);
+  bool run[S];
+  bool any = false;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    run[s] = live[s];
+    if (!run[s]) continue;
+    const uint32_t i = i0 + s;
+    if ((sh.flag >> s) & 1u) {
+      if (lane == 0) pset_flag(b, i);
+      run[s] = false;
+    } else if (!coop_is_zero(sh.frame, PSN_SLOTS * s + PS_DIFF, 4)) {  // psi(sig) != [x] sig: not in G2
+      if (lane == 0) b.sig_status[i] = BLS_POINT_NOT_IN_GROUP;
+      pset_store_one(&b.f[i]);
+      run[s] = false;
+    }
+    any = any || run[s];
+  }
+  if (!any) return;
+  coop_run(env, pg.norm2, sh.frame, sh.cbank, &sh.flag);
+  any = false;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (run[s] && ((sh.flag >> s) & 1u)) {
+      if (lane == 0) pset_flag(b, i0 + s);
+      run[s] = false;
+    }
+    any = any || run[s];
+  }
+  if (!any) return;
+  // all S inversions at once (lanes 0..S-1; fp_inv_gcd(0) = 0 for a dropped part)
+  if (lane < S) {
+    const int o = PSN_SLOTS * lane;
+    lds_store_fp(sh.frame, o + PS_INV_OUT, fp_inv_gcd(fp_canon3(lds_load_fp(sh.frame, o + PS_INV_IN))));
+  }
+  __syncthreads();
+  coop_run(env, pg.affine2, sh.frame, sh.cbank, &sh.flag);
+  coop_run(env, pg.ml2, sh.frame, sh.cbank, &sh.flag);
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (run[s] && lane < 12)
+      reinterpret_cast<Fp*>(&b.f[i0 + s])[lane] = coop_get(sh.frame, PSN_SLOTS * s + PS_F + lane);
+}
+
+// Sets per wavefront for a batch: 1 for small batches (latency: one wave per set
+// spreads a small call over more SIMDs), 3 from BLS_PACK_MIN_SETS sets on
+// (throughput).  $BLS_PACK (1, 2 or 3) forces a packing; $BLS_PACK_MIN overrides
+// the threshold.
+#define BLS_PACK_MIN_SETS 512u
+static uint32_t pack_for(uint32_t n_sets) {
+  static const int forced = [] {
+    const char* e = getenv("BLS_PACK");
+    return e ? atoi(e) : 0;
+  }();
+  static const uint32_t min_sets = [] {
+    const char* e = getenv("BLS_PACK_MIN");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : BLS_PACK_MIN_SETS;
+  }();
+  if (forced >= 1 && forced <= 3) return (uint32_t)forced;
+  return n_sets >= min_sets ? 3u : 1u;
+}
+
 hipError_t launch_k_pset(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
-  k_pset<<<b.n_sets, COOP_LANES, 0, s>>>(b, env);
+  const uint32_t S = pack_for(b.n_sets);
+  if (S == 3 && env.packed[1].ml2.n > 0) {
+    k_psetn<3, COOP_FRAME3><<<(b.n_sets + 2) / 3, COOP_LANES, 0, s>>>(b, env);
+  } else if (S == 2 && env.packed[0].ml2.n > 0) {
+    k_psetn<2, COOP_FRAME2><<<(b.n_sets + 1) / 2, COOP_LANES, 0, s>>>(b, env);
+  } else {
+    k_pset<<<b.n_sets, COOP_LANES, 0, s>>>(b, env);
+  }
   return hipGetLastError();
 }

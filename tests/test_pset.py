@@ -1,6 +1,6 @@
 """Per-set cooperative programs (tools/gen_pset.py) over the step simulator, against
 the oracle: H(m) = hash_to_G2 from the two SSWU points, the G2 subgroup test,
-r*sig / r*pk and f_i = ML(r pk, H) ML(-g1, r sig).  CPU only."""
+r*g1 / r*pk and f_i = ML(r pk, H) ML(-r g1, sig).  CPU only."""
 from __future__ import annotations
 
 import random
@@ -50,7 +50,9 @@ def test_pset_valid_set(progs, oracle):
     assert not flag and in_group
     H = oracle.hash_to_g2(msg)
     assert ((fr[PS.HQ], fr[PS.HQ + 1]), (fr[PS.HQ + 2], fr[PS.HQ + 3])) == H
-    assert ((fr[PS.RSQ], fr[PS.RSQ + 1]), (fr[PS.RSQ + 2], fr[PS.RSQ + 3])) == oracle.E2.mul(sig, r)
+    X, Y, Z = fr[PS.RG:PS.RG + 3]
+    zi = _inv(Z)
+    assert (X * zi * zi % P, Y * zi ** 3 % P) == oracle.E1.mul(oracle.G1, r)
     X, Y, Z = fr[PS.RP:PS.RP + 3]
     zi = _inv(Z)
     assert (X * zi * zi % P, Y * zi ** 3 % P) == oracle.E1.mul(pk, r)
@@ -77,3 +79,28 @@ def test_pset_wrong_message_and_non_subgroup(progs, oracle):
     fr = _frame_for(oracle, msg, off, pk, 1)
     flag, in_group = PS.run_pset(pg, consts, fr, 5, simulate, _inv)
     assert not in_group
+
+
+def test_pset2_two_sets_per_wavefront(progs, oracle):
+    """The 2-set packed programs (k_pset2): a valid set next to a set whose signature
+    signs another message; each half of the frame gets its own f_i and flags."""
+    pg, consts = progs
+    rng = random.Random(13)
+    frame = [0] * GC.FRAME2
+    rs, expect_one = [], []
+    for s, good in enumerate((True, False)):
+        sk = rng.randrange(1, oracle.R)
+        msg = bytes(rng.randrange(256) for _ in range(32))
+        sig = oracle.E2.mul(oracle.hash_to_g2(msg if good else b"\x02" * 32), sk)
+        pk = oracle.E1.mul(oracle.G1, sk)
+        fr = _frame_for(oracle, msg, sig, pk, rng.randrange(1, P))
+        o = PS.SET_SLOTS * s
+        frame[o:o + PS.SET_SLOTS] = fr[:PS.SET_SLOTS]
+        rs.append(rng.randrange(1, 1 << 64))
+        expect_one.append(good)
+    flag, in_group = PS.run_pset2(pg, consts, frame, rs, simulate, _inv)
+    assert flag == 0 and in_group == [True, True]
+    for s in range(2):
+        o = PS.SET_SLOTS * s + PS.F
+        f = [(frame[o + 6 * (w % 2) + 2 * (w // 2)], frame[o + 6 * (w % 2) + 2 * (w // 2) + 1]) for w in range(6)]
+        assert oracle.f12_is_one(oracle.final_exponentiation(f, hard_multiple=3)) == expect_one[s]

@@ -100,6 +100,8 @@ class Circuit:
         self.consts = consts
         self.outputs: list[tuple[int, Lin]] = []
         self.zchecks: list[Lin] = []
+        self.zsets: list[int] = []   # set index of each zero-check (packed multi-set programs)
+        self.zset = 0
 
     @staticmethod
     def inp(slot: int) -> Lin:
@@ -131,6 +133,7 @@ class Circuit:
 
     def zcheck(self, v: Lin):
         self.zchecks.append(v)
+        self.zsets.append(self.zset)
 
 
 # ----------------------------------------------------------------------------
@@ -385,11 +388,18 @@ def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes) -> Program
         if is_mul:
             n_mul += 1
     tail = [Op(OP_LIN, slot, _emit(v, slot_of)) for slot, v in outs]
-    tail += [Op(OP_LIN, ZCHECK, _emit(z, slot_of)) for z in zchecks]
+    tail += [Op(OP_LIN, ZCHECK - zs, _emit(z, slot_of)) for z, zs in zip(zchecks, c.zsets)]
+    # the outputs land in as few steps as fit the lanes; a later output step may not
+    # read a slot an earlier one wrote (outputs are written simultaneously in spirit)
+    written = set()
     for k in range(0, len(tail), lanes):
-        if k > 0:
-            raise RuntimeError(f"{c.name}: {len(tail)} outputs exceed one step")
-        steps.append(tail[k: k + lanes])
+        chunk = tail[k: k + lanes]
+        for op in chunk:
+            for ref, _ in op.a:
+                if not isinstance(ref, tuple) and ref in written:
+                    raise RuntimeError(f"{c.name}: output step {k // lanes} reads slot {ref} written before")
+        steps.append(chunk)
+        written |= {op.out for op in chunk if op.out >= 0}
     return Program(c.name, steps, frame_slots, [s for s, _ in outs], n_mul)
 
 
@@ -408,9 +418,10 @@ def _emit(l: Lin, slot_of) -> list:
 # ----------------------------------------------------------------------------
 # simulation (exact device semantics)
 # ----------------------------------------------------------------------------
-def simulate(prog: Program, frame: list, consts: ConstBank) -> bool:
-    """Run `prog` in place on `frame` (list of ints mod P); returns the zero-check flag."""
-    flag = False
+def simulate(prog: Program, frame: list, consts: ConstBank) -> int:
+    """Run `prog` in place on `frame` (list of ints mod P); returns the zero-check
+    flags (bit s: a zero-check of packed set s saw zero)."""
+    flag = 0
 
     def val(terms):
         s = 0
@@ -425,8 +436,9 @@ def simulate(prog: Program, frame: list, consts: ConstBank) -> bool:
             a = val(op.a)
             res.append((op, a * val(op.b) % P if op.kind == OP_MUL else a))
         for op, r in res:
-            if op.out == ZCHECK:
-                flag = flag or r == 0
+            if op.out <= ZCHECK:
+                if r == 0:
+                    flag |= 1 << (ZCHECK - op.out)
             else:
                 frame[op.out] = r
     return flag

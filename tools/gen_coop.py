@@ -29,6 +29,8 @@ from circuits import (  # noqa: E402
 
 X_ABS = 0xD201000000010000
 FRAME = 256
+FRAME2 = 512   # frame of the 2-set programs (kernels/k_pset.hip, CoopLdsN<COOP_FRAME2>)
+FRAME3 = 640   # frame of the 3-set programs (CoopLdsN<COOP_FRAME3>)
 MONT_R = 1 << 384
 
 # "fin" frame registers
@@ -432,7 +434,13 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
             for lane in range(LANES):
                 if lane < len(step):
                     op = step[lane]
-                    out = 0xFFFF if op.out == ZCHECK else op.out
+                    # zero-checks: 0xFFFF for set 0, 0xFFF0 + s for packed set s >= 1
+                    if op.out == ZCHECK:
+                        out = 0xFFFF
+                    elif op.out < ZCHECK:
+                        out = 0xFFF0 + (ZCHECK - op.out)
+                    else:
+                        out = op.out
                     kind = op.kind
                     a, b = op.a, op.b if op.kind == OP_MUL else []
                 else:
@@ -443,7 +451,8 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                 a = sorted(a, key=lambda t: (abs(t[1]) != 1, t[1] < 0))
                 b = sorted(b, key=lambda t: (abs(t[1]) != 1, t[1] < 0))
                 def refs(lst):
-                    r = [((FRAME + x[1]) if isinstance(x, tuple) else x) for x, _ in lst]
+                    # constants follow the program's frame in LDS (CoopLdsN)
+                    r = [((pg.n_slots + x[1]) if isinstance(x, tuple) else x) for x, _ in lst]
                     return r + [0] * (8 - len(r))
                 def cfs(lst):
                     r = [cf for _, cf in lst]
@@ -471,6 +480,11 @@ def build_all():
     psi, iso = _curve_constants()
     progs = build_fin(consts)
     progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, psi, iso, G1X, G1Y)
+    # two / three sets packed per wavefront (k_psetn, large batches)
+    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, psi, iso, G1X, G1Y,
+                                 S=2, prefix="pset2")
+    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME3, psi, iso, G1X, G1Y,
+                                 S=3, prefix="pset3")
     return progs, consts
 
 

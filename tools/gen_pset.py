@@ -6,8 +6,13 @@ q0, q1 on E2', the decompressed signature and the public key:
 
   H     = clear_cofactor(iso(q0) + iso(q1))                  (RFC 9380, Budroni-Pintore)
   check = psi(sig) == [x] sig                                 (G2 membership, Scott)
-  RS    = [r] sig,  RP = [r] pk                               (64-bit batch scalar)
-  f_i   = ML(RP, H) * ML(-g1, RS)                             (two-pair Miller loop)
+  RG    = [r] g1,   RP = [r] pk                               (64-bit batch scalar)
+  f_i   = ML(RP, H) * ML(-RG, sig)                            (two-pair Miller loop)
+
+The random scalar sits on G1 on both sides: e(-g1, r sig) = e(-[r] g1, sig) for sig
+in G2 (checked here), so the batch product is the reference's element of GT while
+both scalar chains run on G1 (3x cheaper than G2) and sig stays affine for the
+Miller loop (one inversion per set, for H only).
 
 Scalar multiplications run left to right, one doubling program per bit for every
 chain at once (lanes in parallel) and addition programs chosen per bit by the
@@ -21,9 +26,9 @@ exact single-lane path.
 Frame (slots):
   Q0 0..3  Q1 4..7  SIG 8..11 (affine)  PK 12..14 (G1 Jacobian)
   A 15..20 (cofactor chain [|x|]P)  C 21..26 (subgroup chain [|x|]sig)
-  D1 27..32 ([r + 2^64] sig)  D2 33..35 ([r + 2^64] pk)  E1 36..41 ([2^64] sig)  E2 42..44 ([2^64] pk)
-  PP 45..50 (P = iso(q0) + iso(q1))  H 51..56  RS 57..62  RP 63..65
-  HQ 66..69  RSQ 70..73 (affine)  INV_IN 74  INV_OUT 75  DIFF 76..79 (subgroup test)
+  D3 27..29 ([r + 2^64] g1)  D2 33..35 ([r + 2^64] pk)  E2 42..44 ([2^64] pk)
+  PP 45..50 (P = iso(q0) + iso(q1))  H 51..56  RG 57..59  RP 63..65
+  HQ 66..69 (affine)  INV_IN 74  INV_OUT 75  DIFF 76..79 (subgroup test)
   F 80..91 (f_i)  temporaries 92..FRAME-1
 """
 from __future__ import annotations
@@ -31,9 +36,9 @@ from __future__ import annotations
 from circuits import Circuit, Lin, schedule
 
 Q0, Q1, SIG, PK = 0, 4, 8, 12
-A, C, D1, D2, E1, E2 = 15, 21, 27, 33, 36, 42
-PP, H, RS, RP = 45, 51, 57, 63
-HQ, RSQ, INV_IN, INV_OUT, DIFF, F = 66, 70, 74, 75, 76, 80
+A, C, D3, D2, E2 = 15, 21, 27, 33, 42
+PP, H, RG, RP = 45, 51, 57, 63
+HQ, INV_IN, INV_OUT, DIFF, F = 66, 74, 75, 76, 80
 REGS = set(range(0, 92))
 
 
@@ -244,131 +249,201 @@ def const2(t, v):
     return (t.c.const(v[0]) if v[0] else Lin(), t.c.const(v[1]) if v[1] else Lin())
 
 
-def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G1Y):
+P_MOD = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+_G1 = (0x17F1D3A73197D7942695638C4FA9AC0FC3688C4F9774B905A14E3A3F171BAC586C55E83FF97A1AEFFB3AF00ADB22C6BB,
+       0x08B3F481E3AAA0F1A09E30ED741D8AE4FCF5E095D5D00AF600DB18CB2C04B3EDD03CC744A2888AE40CAA232946C5E7E1)
+
+
+def _g1_dbl_affine(p):
+    x, y = p
+    lam = 3 * x * x * pow(2 * y, P_MOD - 2, P_MOD) % P_MOD
+    x3 = (lam * lam - 2 * x) % P_MOD
+    return x3, (lam * (x - x3) - y) % P_MOD
+
+
+def _g1_2_64():
+    p = _G1
+    for _ in range(64):
+        p = _g1_dbl_affine(p)
+    return p
+
+
+G1_2_64 = _g1_2_64()   # [2^64] g1, subtracted from the [r + 2^64] g1 chain
+
+SET_SLOTS = 92   # registers per set; packed set s uses slots [s * SET_SLOTS, (s + 1) * SET_SLOTS)
+
+
+def add_program_name(prefix: str, S: int, xb: int, rmask: int) -> str:
+    """Addition program for one bit: the |x| bit xb and the r bits of the packed sets
+    (bit s of rmask = set s).  S == 1 keeps the historical names."""
+    if S == 1:
+        return f"{prefix}_add_" + ("x" if xb else "") + ("r" if rmask else "")
+    return f"{prefix}_add_{xb}{rmask:0{S}b}"
+
+
+def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G1Y, S=1, prefix="pset"):
+    """The per-set programs for S sets packed in one wavefront (set s at register
+    offset s * SET_SLOTS; its zero-checks carry its set index)."""
     progs = []
+    offs = [SET_SLOTS * s for s in range(S)]
+    regs = set(range(0, SET_SLOTS * S))
 
     def new(name):
-        c = Circuit(name, consts)
+        c = Circuit(f"{prefix}_{name}", consts)
         t = T(c)
         return c, t, F1(c), F2(t)
 
+    def per_set(c, body):
+        for s, o in enumerate(offs):
+            c.zset = s
+            body(o)
+        c.zset = 0
+
     # P = iso(q0) + iso(q1); initialise every chain
-    c, t, f1, f2 = new("pset_prep")
-    p0 = iso_jac(t, t.f2(Q0), t.f2(Q0 + 2), ISO)
-    p1 = iso_jac(t, t.f2(Q1), t.f2(Q1 + 2), ISO)
-    pp = add_gen(f2, p0, p1)
-    out_jac(f2, PP, pp)
-    out_jac(f2, A, pp)
-    sig = aff(f2, SIG)
-    sigj = (sig[0], sig[1], f2.one())
-    for base in (C, D1, E1):
-        out_jac(f2, base, sigj)
-    pk = jac(f1, PK)
-    for base in (D2, E2):
-        out_jac(f1, base, pk)
-    progs.append(schedule(c, FRAME, REGS))
+    c, t, f1, f2 = new("prep")
+
+    def prep(o):
+        p0 = iso_jac(t, t.f2(o + Q0), t.f2(o + Q0 + 2), ISO)
+        p1 = iso_jac(t, t.f2(o + Q1), t.f2(o + Q1 + 2), ISO)
+        pp = add_gen(f2, p0, p1)
+        out_jac(f2, o + PP, pp)
+        out_jac(f2, o + A, pp)
+        sig = aff(f2, o + SIG)
+        sigj = (sig[0], sig[1], f2.one())
+        out_jac(f2, o + C, sigj)
+        out_jac(f1, o + D3, (f1.c.const(G1X), f1.c.const(G1Y), f1.one()))
+        pk = jac(f1, o + PK)
+        for base in (D2, E2):
+            out_jac(f1, o + base, pk)
+
+    per_set(c, prep)
+    progs.append(schedule(c, FRAME, regs))
 
     # doubling programs
     def dbl_prog(name, g2_regs, g1_regs):
         c, t, f1, f2 = new(name)
-        for base in g2_regs:
-            out_jac(f2, base, dbl(f2, jac(f2, base)))
-        for base in g1_regs:
-            out_jac(f1, base, dbl(f1, jac(f1, base)))
-        progs.append(schedule(c, FRAME, REGS))
 
-    dbl_prog("pset_dbl_r", (D1, E1), (D2, E2))
-    dbl_prog("pset_dbl_all", (A, C, D1, E1), (D2, E2))
+        def body(o):
+            for base in g2_regs:
+                out_jac(f2, o + base, dbl(f2, jac(f2, o + base)))
+            for base in g1_regs:
+                out_jac(f1, o + base, dbl(f1, jac(f1, o + base)))
 
-    def add_prog(name, x_part, r_part):
-        c, t, f1, f2 = new(name)
-        if x_part:
-            out_jac(f2, A, add_gen(f2, jac(f2, A), jac(f2, PP)))
-            out_jac(f2, C, add_mixed(f2, jac(f2, C), aff(f2, SIG)))
-        if r_part:
-            out_jac(f2, D1, add_mixed(f2, jac(f2, D1), aff(f2, SIG)))
-            out_jac(f1, D2, add_gen(f1, jac(f1, D2), jac(f1, PK)))
-        progs.append(schedule(c, FRAME, REGS))
+        per_set(c, body)
+        progs.append(schedule(c, FRAME, regs))
 
-    add_prog("pset_add_x", True, False)
-    add_prog("pset_add_r", False, True)
-    add_prog("pset_add_xr", True, True)
+    dbl_prog("dbl_r", (), (D2, E2, D3))
+    dbl_prog("dbl_all", (A, C), (D2, E2, D3))
+
+    def add_prog(xb, rmask):
+        c, t, f1, f2 = new(add_program_name(prefix, S, xb, rmask)[len(prefix) + 1:])
+
+        def body(o):
+            s = o // SET_SLOTS
+            if xb:
+                out_jac(f2, o + A, add_gen(f2, jac(f2, o + A), jac(f2, o + PP)))
+                out_jac(f2, o + C, add_mixed(f2, jac(f2, o + C), aff(f2, o + SIG)))
+            if (rmask >> s) & 1:
+                out_jac(f1, o + D3, add_mixed(f1, jac(f1, o + D3), (c.const(G1X), c.const(G1Y))))
+                out_jac(f1, o + D2, add_gen(f1, jac(f1, o + D2), jac(f1, o + PK)))
+
+        per_set(c, body)
+        progs.append(schedule(c, FRAME, regs))
+
+    for xb in (0, 1):
+        for rmask in range(1 << S):
+            if xb or rmask:
+                add_prog(xb, rmask)
 
     # phase 2 (straight line): finish the cofactor clearing, the r multiples and the
     # subgroup comparison
-    c, t, f1, f2 = new("pset_phase2")
-    P = jac(f2, PP)
-    t1 = neg_pt(f2, jac(f2, A))                        # [x]P = -[|x|]P
-    t2 = psi_jac(t, P, PSI)
-    t2p = add_gen(f2, t1, t2)                          # t1 + t2
-    # U = [|x|] t2p
-    U = t2p
-    for i in range(62, -1, -1):
-        U = dbl(f2, U)
-        if (X_ABS >> i) & 1:
-            U = add_gen(f2, U, t2p)
-    p2 = dbl(f2, P)
-    t3 = psi_jac(t, psi_jac(t, p2, PSI), PSI)          # psi^2(2P)
-    t3 = add_gen(f2, t3, neg_pt(f2, t2))               # - t2
-    t3 = add_gen(f2, t3, neg_pt(f2, U))                # + [x] t2p
-    t3 = add_gen(f2, t3, neg_pt(f2, t1))               # - t1
-    hh = add_gen(f2, t3, neg_pt(f2, P))                # - P
-    out_jac(f2, H, hh)
-    # RS = D1 - E1, RP = D2 - E2
-    out_jac(f2, RS, add_gen(f2, jac(f2, D1), neg_pt(f2, jac(f2, E1))))
-    out_jac(f1, RP, add_gen(f1, jac(f1, D2), neg_pt(f1, jac(f1, E2))))
-    # subgroup: psi(sig) == -C (= [x] sig): (psi.x) Z^2 == X and (psi.y) Z^3 == -Y
-    X, Y, Z = jac(f2, C)
-    f2.zero(Z)                                         # [|x|] sig hit infinity: exact path
-    sx, sy = t.mulc2(t.conj2(t.f2(SIG)), PSI[0]), t.mulc2(t.conj2(t.f2(SIG + 2)), PSI[1])
-    z2 = t.mat2(t.sqr2(Z))
-    z3 = t.mat2(t.mul2(z2, Z))
-    d0 = t.sub2(t.mul2(t.mat2(sx), z2), X)
-    d1 = t.add2(t.mul2(t.mat2(sy), z3), Y)
-    f2.out(DIFF, d0)
-    f2.out(DIFF + 2, d1)
-    progs.append(schedule(c, FRAME, REGS))
+    c, t, f1, f2 = new("phase2")
 
-    # one inversion for both affine conversions: INV_IN = N(H.z) N(RS.z)
-    c, t, f1, f2 = new("pset_norm2")
-    hz = t.f2(H + 4)
-    rz = t.f2(RS + 4)
-    nh = c.mat(c.mul(hz[0], hz[0]) + c.mul(hz[1], hz[1]))
-    nr = c.mat(c.mul(rz[0], rz[0]) + c.mul(rz[1], rz[1]))
-    inv_in = c.mat(c.mul(nh, nr))
-    c.zcheck(inv_in)                                   # H or r sig at infinity: exact path
-    c.out(INV_IN, inv_in)
-    c.out(DIFF, nh)       # stash the norms for the next program (DIFF is free by now)
-    c.out(DIFF + 1, nr)
-    progs.append(schedule(c, FRAME, REGS))
+    def phase2(o):
+        P = jac(f2, o + PP)
+        t1 = neg_pt(f2, jac(f2, o + A))                    # [x]P = -[|x|]P
+        t2 = psi_jac(t, P, PSI)
+        t2p = add_gen(f2, t1, t2)                          # t1 + t2
+        # U = [|x|] t2p
+        U = t2p
+        for i in range(62, -1, -1):
+            U = dbl(f2, U)
+            if (X_ABS >> i) & 1:
+                U = add_gen(f2, U, t2p)
+        p2 = dbl(f2, P)
+        t3 = psi_jac(t, psi_jac(t, p2, PSI), PSI)          # psi^2(2P)
+        t3 = add_gen(f2, t3, neg_pt(f2, t2))               # - t2
+        t3 = add_gen(f2, t3, neg_pt(f2, U))                # + [x] t2p
+        t3 = add_gen(f2, t3, neg_pt(f2, t1))               # - t1
+        hh = add_gen(f2, t3, neg_pt(f2, P))                # - P
+        out_jac(f2, o + H, hh)
+        # RG = D3 - [2^64] g1 (a constant), RP = D2 - E2
+        out_jac(f1, o + RG, add_mixed(f1, jac(f1, o + D3), (c.const(G1_2_64[0]), c.const(P_MOD - G1_2_64[1]))))
+        out_jac(f1, o + RP, add_gen(f1, jac(f1, o + D2), neg_pt(f1, jac(f1, o + E2))))
+        # subgroup: psi(sig) == -C (= [x] sig): (psi.x) Z^2 == X and (psi.y) Z^3 == -Y
+        X, Y, Z = jac(f2, o + C)
+        f2.zero(Z)                                         # [|x|] sig hit infinity: exact path
+        sx = t.mulc2(t.conj2(t.f2(o + SIG)), PSI[0])
+        sy = t.mulc2(t.conj2(t.f2(o + SIG + 2)), PSI[1])
+        z2 = t.mat2(t.sqr2(Z))
+        z3 = t.mat2(t.mul2(z2, Z))
+        d0 = t.sub2(t.mul2(t.mat2(sx), z2), X)
+        d1 = t.add2(t.mul2(t.mat2(sy), z3), Y)
+        f2.out(o + DIFF, d0)
+        f2.out(o + DIFF + 2, d1)
 
-    c, t, f1, f2 = new("pset_affine2")
-    w = Circuit.inp(INV_OUT)
-    inv_nh = c.mat(c.mul(w, Circuit.inp(DIFF + 1)))   # 1/N(H.z)
-    inv_nr = c.mat(c.mul(w, Circuit.inp(DIFF)))       # 1/N(RS.z)
-    for base, inv, dst in ((H, inv_nh, HQ), (RS, inv_nr, RSQ)):
-        z = t.f2(base + 4)
-        zi = t.mat2((c.mul(z[0], inv), -c.mul(z[1], inv)))
+    per_set(c, phase2)
+    progs.append(schedule(c, FRAME, regs))
+
+    # one inversion per set (H to affine): INV_IN = N(H.z)
+    c, t, f1, f2 = new("norm2")
+
+    def norm2(o):
+        hz = t.f2(o + H + 4)
+        nh = c.mat(c.mul(hz[0], hz[0]) + c.mul(hz[1], hz[1]))
+        c.zcheck(nh)                                       # H at infinity: exact path
+        c.out(o + INV_IN, nh)
+
+    per_set(c, norm2)
+    progs.append(schedule(c, FRAME, regs))
+
+    c, t, f1, f2 = new("affine2")
+
+    def affine2(o):
+        w = Circuit.inp(o + INV_OUT)                       # 1/N(H.z)
+        z = t.f2(o + H + 4)
+        zi = t.mat2((c.mul(z[0], w), -c.mul(z[1], w)))
         zi2 = t.mat2(t.sqr2(zi))
         zi3 = t.mat2(t.mul2(zi2, zi))
-        f2.out(dst, t.mul2(t.f2(base), zi2))
-        f2.out(dst + 2, t.mul2(t.f2(base + 2), zi3))
-    progs.append(schedule(c, FRAME, REGS))
+        f2.out(o + HQ, t.mul2(t.f2(o + H), zi2))
+        f2.out(o + HQ + 2, t.mul2(t.f2(o + H + 2), zi3))
 
-    # f = ML(RP, HQ) * ML(-g1, RSQ): two-pair Miller loop sharing the squarings
-    c, t, f1, f2 = new("pset_ml2")
-    X, Y, Z = (Circuit.inp(RP + k) for k in range(3))
-    pz3 = c.mat(c.mul(c.mat(c.mul(Z, Z)), Z))
-    pxz = c.mat(c.mul(X, Z))
-    pairs = [(t.f2(HQ), t.f2(HQ + 2), pxz, Y, pz3),
-             (t.f2(RSQ), t.f2(RSQ + 2), c.const(G1X), c.const(-G1Y), None)]
-    f = miller_loop_multi(t, pairs, miller_dbl, miller_add, X_ABS)
-    for k in range(2):
-        for j in range(3):
-            for i in range(2):
-                c.out(F + 6 * k + 2 * j + i, f[k][j][i])
+    per_set(c, affine2)
+    progs.append(schedule(c, FRAME, regs))
+
+    # f = ML(RP, HQ) * ML(-RG, SIG): two-pair Miller loop sharing the squarings
+    c, t, f1, f2 = new("ml2")
+
+    def ml2(o):
+        pairs = []
+        for qb, pb, sgn in ((HQ, RP, 1), (SIG, RG, -1)):
+            X, Y, Z = (Circuit.inp(o + pb + k) for k in range(3))
+            pz3 = c.mat(c.mul(c.mat(c.mul(Z, Z)), Z))
+            pxz = c.mat(c.mul(X, Z))
+            pairs.append((t.f2(o + qb), t.f2(o + qb + 2), pxz, Y * sgn, pz3))
+        f = miller_loop_multi(t, pairs, miller_dbl, miller_add, X_ABS)
+        for k in range(2):
+            for j in range(3):
+                for i in range(2):
+                    c.out(o + F + 6 * k + 2 * j + i, f[k][j][i])
+
+    per_set(c, ml2)
     # last program: only its inputs are live
-    progs.append(schedule(c, FRAME, set(range(RP, RP + 3)) | set(range(HQ, RSQ + 4))))
+    live = set()
+    for o in offs:
+        live |= set(range(o + RP, o + RP + 3)) | set(range(o + RG, o + RG + 3)) | set(range(o + HQ, o + HQ + 4))
+        live |= set(range(o + SIG, o + SIG + 4))
+    progs.append(schedule(c, FRAME, live))
     return progs
 
 
@@ -449,3 +524,29 @@ def run_pset(pg, consts, frame, r, simulate, inv):
 
 
 X_ABS_BITS = 0xD201000000010000
+
+
+def run_pset2(pg, consts, frame, rs, simulate, inv):
+    """The k_pset2 controller (two sets per wavefront) over the simulator: returns the
+    zero-check flag bits and the per-set subgroup results.  frame: 2 * SET_SLOTS
+    registers + temporaries; rs: the two scalars."""
+    r0, r1 = rs
+    flag = simulate(pg["pset2_prep"], frame, consts)
+    flag |= simulate(pg["pset2_dbl_r"], frame, consts)
+    m = ((r0 >> 63) & 1) | (((r1 >> 63) & 1) << 1)
+    if m:
+        flag |= simulate(pg[add_program_name("pset2", 2, 0, m)], frame, consts)
+    for i in range(62, -1, -1):
+        flag |= simulate(pg["pset2_dbl_all"], frame, consts)
+        xb = (X_ABS_BITS >> i) & 1
+        m = ((r0 >> i) & 1) | (((r1 >> i) & 1) << 1)
+        if xb or m:
+            flag |= simulate(pg[add_program_name("pset2", 2, xb, m)], frame, consts)
+    flag |= simulate(pg["pset2_phase2"], frame, consts)
+    in_group = [all(frame[SET_SLOTS * s + DIFF + k] == 0 for k in range(4)) for s in range(2)]
+    flag |= simulate(pg["pset2_norm2"], frame, consts)
+    for s in range(2):
+        frame[SET_SLOTS * s + INV_OUT] = inv(frame[SET_SLOTS * s + INV_IN])
+    flag |= simulate(pg["pset2_affine2"], frame, consts)
+    flag |= simulate(pg["pset2_ml2"], frame, consts)
+    return flag, in_group
