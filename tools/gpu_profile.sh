@@ -14,4 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof/trace"
 tail -1 gpurun_out/prof/trace.log
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof/pmc_fetch" -o bench --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 --inflight 1 --latency-runs 1 > gpurun_out/prof/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail -20 gpurun_out/prof/pmc_fetch.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/prof/pmc_write" -o bench --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 --inflight 1 --latency-runs 1 > gpurun_out/prof/pmc_write.log 2>&1 || { echo "pmc write failed"; tail -20 gpurun_out/prof/pmc_write.log; exit 1; }
+python tools/pmc_traffic.py gpurun_out/prof/pmc_fetch/bench_counter_collection.csv gpurun_out/prof/pmc_write/bench_counter_collection.csv gpurun_out/prof/pmc_traffic.json
 find gpurun_out/prof -name "*.csv" | sort

@@ -19,7 +19,8 @@ def per_launch(path: str, counter: str) -> dict:
     acc = collections.defaultdict(list)
     for row in csv.DictReader(open(path)):
         if row["Counter_Name"] == counter:
-            acc[row["Kernel_Name"].split("(")[0]].append(float(row["Counter_Value"]) * 1024.0)
+            name = row["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
+            acc[name].append(float(row["Counter_Value"]) * 1024.0)
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
