@@ -91,6 +91,14 @@ const char* bls_gpu_last_error(const bls_gpu_ctx* ctx);
  * size (>= 0) or < 0 on failure. */
 int64_t bls_gpu_load_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes);
 
+/* KeyValidate for n public keys (blst PublicKey.fromBytes(bytes, validate=true) [ext],
+ * the check deposits get before a key enters the registry, state-transition
+ * block/processDeposit.ts:56-65 -> index2pubkey, pubkeyCache.ts:56-77): decode
+ * (48 compressed / 96 uncompressed), then BLST_PK_IS_INFINITY for the point at
+ * infinity and BLST_POINT_NOT_IN_GROUP outside G1 (Scott's endomorphism test).
+ * codes: n entries, 0 = valid.  Does not touch the device table. */
+int bls_gpu_validate_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes);
+
 /* verifyManySignatureSets (worker.ts:32-108) on the GPU: per-request verdicts with
  * the reference's batch / fallback semantics:
  *   - batchable requests are grouped by chunkifyMaximizeChunkSize(reqs, 16) and each

@@ -282,6 +282,18 @@ BLS_HD bool g2_in_subgroup(const G2A& a) {
   return jac_eq(g2_psi(p), xp);
 }
 
+// G1 membership: sigma(P) == [-x^2]P with sigma(x, y) = (beta x, y) (Scott's test,
+// "A note on group membership tests for G1, G2 and GT"); equals r*P == O on E1.
+BLS_HD bool g1_in_subgroup(const G1A& a) {
+  if (a.inf) return true;
+  const G1J q = jac_mul_xabs(jac_mul_xabs(jac_from_aff(a)));  // [x^2]P
+  if (jac_is_inf(q)) return false;                              // sigma(P) != O
+  const Fp z2 = fp_sqr(q.z);
+  const Fp z3 = fp_mul(z2, q.z);
+  // -[x^2]P == sigma(P):  X == beta x Z^2  and  -Y == y Z^3
+  return fp_eq(q.x, fp_mul(fp_mul(c_g1_beta(), a.x), z2)) && fp_eq(fp_neg(q.y), fp_mul(a.y, z3));
+}
+
 // Budroni-Pintore cofactor clearing = [h_eff]P (RFC 9380 Appendix G.3)
 BLS_HD G2J g2_clear_cofactor(const G2J& p) {
   G2J t1 = jac_neg(jac_mul_xabs(p));  // [x]P

@@ -27,6 +27,24 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_load_pubkeys(const uint8_t* pks, 
   codes[i] = c;
 }
 
+// KeyValidate (blst PublicKey.fromBytes(bytes, validate=true) [ext], as the deposit
+// path uses it, block/processDeposit.ts:56-65): decode, reject infinity, G1 subgroup.
+__global__ __launch_bounds__(BLS_BLOCK) void k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len,
+                                                                int32_t* codes) {
+  uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  G1A a;
+  int32_t c = pk_len == 48 ? g1_decompress48(pks + 48ull * i, a) : g1_deserialize96(pks + 96ull * i, a);
+  if (c == BLS_OK && a.inf) c = BLS_PK_IS_INFINITY;
+  if (c == BLS_OK && !g1_in_subgroup(a)) c = BLS_POINT_NOT_IN_GROUP;
+  codes[i] = c;
+}
+
+hipError_t launch_k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes, hipStream_t s) {
+  k_validate_pubkeys<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(pks, n, pk_len, codes);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(BLS_BLOCK) void k_status(PipeBufs b) {
   stage_req_status(b, blockIdx.x * BLS_BLOCK + threadIdx.x);
 }

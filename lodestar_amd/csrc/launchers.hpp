@@ -15,6 +15,7 @@ hipError_t launch_k_aggregate(const bls::PipeBufs& b, uint8_t* out96, hipStream_
 hipError_t launch_k_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, bls::G1A* out, int32_t* codes,
                                  hipStream_t s);
 hipError_t launch_k_status(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes, hipStream_t s);
 hipError_t launch_k_pre(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_exact(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_hash_to_g2(const uint8_t* msgs, uint32_t n, uint8_t* out192, hipStream_t s);

@@ -141,6 +141,15 @@ class GpuContext:
         self._check(rc, "bls_gpu_load_pubkeys")
         return codes[:n]
 
+    def validate_pubkeys(self, pks: bytes | np.ndarray, pk_len: int = 48) -> np.ndarray:
+        """KeyValidate codes (0 valid, else BLST-style code) for n keys (bls_gpu_validate_pubkeys)."""
+        arr = _u8(pks)
+        n = arr.size // pk_len
+        codes = np.zeros(max(n, 1), dtype=np.int32)
+        rc = self.lib.bls_gpu_validate_pubkeys(self._h, _ptr(arr), n, pk_len, _ptr(codes))
+        self._check(rc, "bls_gpu_validate_pubkeys")
+        return codes[:n]
+
     # -- verification -------------------------------------------------------------
     @staticmethod
     def _batch_struct(pb: PackedBatch):

@@ -408,6 +408,24 @@ def g2_in_subgroup(pt):
     return E2.mul(pt, R) is None
 
 
+def g1_in_subgroup(pt):
+    """Naive r*P == O membership test (GPU uses sigma(P) == [-x^2]P; the two must agree)."""
+    return E1.mul(pt, R) is None
+
+
+def key_validate(b: bytes) -> int:
+    """blst PublicKey.fromBytes(b, validate=true) [ext] as the deposit path uses it
+    (state-transition block/processDeposit.ts:56-65): decode (48 compressed or 96
+    uncompressed), infinity -> BLST_PK_IS_INFINITY, outside G1 -> BLST_POINT_NOT_IN_GROUP.
+    Returns 0 or the error code."""
+    code, pt = g1_decompress(b) if len(b) == 48 else g1_deserialize(b)
+    if code != E_OK:
+        return code
+    if pt is None:
+        return E_PK_IS_INFINITY
+    return E_OK if g1_in_subgroup(pt) else E_POINT_NOT_IN_GROUP
+
+
 def signature_from_bytes(b: bytes, validate=True):
     """Signature.fromBytes(b, affine, validate) [ext]: decode + optional subgroup check."""
     code, pt = g2_decompress(b)

@@ -411,3 +411,21 @@ def test_cfg4_range_sync_mixed_with_invalid(big_table):
     expect = [0 if any(i in bad for i in range(c, c + 128)) else 1 for c in range(0, n, 128)]
     assert list(v) == expect
     assert 0 < sum(expect) < len(expect)
+
+
+def test_validate_pubkeys_matches_oracle(gpu, oracle, golden):
+    """bls_gpu_validate_pubkeys (Scott's G1 test) vs the oracle's r*P == O KeyValidate:
+    KAT-2 keys, infinity, on-curve points outside G1, bad encodings; 48- and 96-byte forms."""
+    keys = [bytes.fromhex(h) for h in golden["kat2_interop_pubkeys"][:20]]
+    x, outside = 1, []
+    while len(outside) < 6:
+        y = oracle.fp_sqrt((x ** 3 + 4) % oracle.P)
+        if y is not None and not oracle.g1_in_subgroup((x, y)):
+            outside.append((x, y))
+        x += 1
+    keys += [oracle.g1_compress(p_) for p_ in outside]
+    keys += [bytes([0xC0]) + bytes(47), bytes(48), bytes([0xFF]) * 48]
+    expect = [oracle.key_validate(k) for k in keys]
+    assert list(gpu.validate_pubkeys(b"".join(keys), 48)) == expect
+    raw = [oracle.g1_serialize(oracle.g1_decompress(k)[1]) for k in keys[:26]]
+    assert list(gpu.validate_pubkeys(b"".join(raw), 96)) == expect[:26]
