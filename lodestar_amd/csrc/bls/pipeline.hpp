@@ -46,6 +46,9 @@ struct PipeBufs {
   const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs
   const uint32_t* chunk_reqs;
   const uint32_t* indiv_reqs;  // n_indiv
+  const uint32_t* fold_groups; // n_fold [beg, end) pairs: k_fold multiplies f[beg+1..end) into f[beg]
+  uint32_t n_fold;
+  uint32_t fold;               // stride of the folded f's an individual request multiplies (0 or 1: none)
   // intermediates
   G2A* sig;
   int32_t* sig_status;
@@ -280,7 +283,8 @@ BLS_HD void stage_indiv(const PipeBufs& b, uint32_t t) {
     return;
   }
   Fp12 F = fp12_one();
-  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) F = fp12_mul(F, b.f[i]);
+  const uint32_t stride = b.fold > 1 ? b.fold : 1u;
+  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) F = fp12_mul(F, b.f[i]);
   b.indiv_verdict[t] = fp12_is_one(final_exponentiation(F)) ? 1 : 0;
 }
 

@@ -70,9 +70,32 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
   }
   fin_init(env, sh);
   bool first = true;
-  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, first);
+  const uint32_t stride = b.fold > 1 ? b.fold : 1u;  // f's pre-multiplied in groups by k_fold
+  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set(b, env, sh, i, first);
   bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.indiv_verdict[t] = ok ? 1 : 0;
+}
+
+// Fold the f_i of individually verified requests in groups of b.fold consecutive sets
+// (one wavefront per group, groups of all requests in parallel) so k_indiv_coop's
+// sequential product over a large request (a 128-set block call: 127 Fp12 products)
+// shrinks to one product per group.
+__global__ __launch_bounds__(COOP_LANES) void k_fold(PipeBufs b, CoopEnv env) {
+  __shared__ FinShared sh;
+  const uint32_t beg = b.fold_groups[2 * blockIdx.x], end = b.fold_groups[2 * blockIdx.x + 1];
+  if (end - beg < 2) return;
+  fin_init(env, sh);
+  coop_load(sh.frame, FIN_F, reinterpret_cast<const Fp*>(&b.f[beg]), 12);
+  for (uint32_t k = beg + 1; k < end; ++k) {
+    coop_load(sh.frame, FIN_G, reinterpret_cast<const Fp*>(&b.f[k]), 12);
+    coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
+  }
+  if (threadIdx.x < 12) reinterpret_cast<Fp*>(&b.f[beg])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
+}
+
+hipError_t launch_k_fold(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
+  k_fold<<<b.n_fold, COOP_LANES, 0, s>>>(b, env);
+  return hipGetLastError();
 }
 
 // Product tree over Fp12 values (sharded calls): block k multiplies

@@ -27,6 +27,8 @@ hipError_t launch_k_fpm_chain(bls::Fp* io, uint32_t lanes, uint32_t iters, hipSt
 #include "bls/coop.hpp"
 hipError_t launch_k_chunk_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_indiv_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
+hipError_t launch_k_fold(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
+#define BLS_FOLD 16u  // sets per k_fold group
 hipError_t launch_k_coop_probe(const bls::CoopEnv& env, bls::CoopProg pg, uint32_t blocks, uint32_t reps,
                                uint32_t* sink, uint64_t* stamps, hipStream_t s);
 #define FPROD_FAN 64u

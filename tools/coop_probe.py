@@ -17,9 +17,11 @@ progs, _ = gen_coop.build_all()
 kinds = {p.name: [any(op.kind == 1 for op in st) for st in p.steps] for p in progs}
 with GpuContext(0) as g:
     out = {}
-    for name, reps in (("fin_fmul", 200), ("pset_dbl_all", 100), ("pset_add_xr", 100), ("pset_phase2", 3),
-                       ("pset_ml2", 3), ("fin_fe2", 2)):
-        for blocks in (1, 64, 1024):
+    names = sys.argv[1:] or ["fin_fmul:200", "pset3_dbl_all:100", "pset3_add_1111:100", "pset3_phase2:3",
+                             "pset3_ml2:3", "fin_fe2:2"]
+    for item in names:
+        name, reps = item.split(":")[0], int(item.split(":")[1])
+        for blocks in (1, 1024, 3072):
             us, ms = g.coop_probe(name, blocks, reps)
             out[f"{name}@{blocks}"] = {"us_per_step": round(us, 3), "ms_per_run": round(ms / reps, 3)}
         k = np.array(kinds[name])
