@@ -67,7 +67,7 @@ def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3
     FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
-    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"), key=lambda p: p.stat().st_mtime)
+    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"), key=lambda p: p.name)
     for p in reversed(files):
         d = json.loads(p.read_text())
         if kernel in d:

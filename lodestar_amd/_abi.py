@@ -43,6 +43,9 @@ SYMBOLS = (
     "bls_gpu_load_pubkeys",
     "bls_gpu_verify",
     "bls_gpu_aggregate_pubkeys",
+    "bls_gpu_validate_pubkeys",
+    "bls_gpu_partial",
+    "bls_gpu_final_check",
     "bls_gpu_hash_to_g2",
     "bls_gpu_sk_to_pk",
     "bls_gpu_sign",
