@@ -80,7 +80,9 @@ def interop_sk(i: int) -> bytes:
     return v.to_bytes(32, "big")
 
 
-def make_workload(gpu, n_sets: int, rank: int):
+def make_workload(gpu, n_sets: int, rank: int, roots: int = 0):
+    """cfg2: every set signs its own root.  roots > 0: the cfg5 mainnet-epoch shape
+    (SURVEY §8d), consecutive sets in committees sharing `roots` signing roots per call."""
     from lodestar_amd.native import pack_requests
 
     n_keys = n_sets
@@ -89,6 +91,8 @@ def make_workload(gpu, n_sets: int, rank: int):
     codes = gpu.load_pubkeys(pks.tobytes(), 48)
     assert (codes == 0).all()
     msgs = [hashlib.sha256((rank * n_sets + j).to_bytes(8, "little") + b"LODE").digest() for j in range(n_sets)]
+    if roots > 0:
+        msgs = [msgs[(j * roots // n_sets) * (n_sets // roots)] for j in range(n_sets)]
     sigs = gpu.sign(b"".join(interop_sk(j % n_keys) for j in range(n_sets)), b"".join(msgs))
     sets = [([j % n_keys], msgs[j], sigs[j].tobytes()) for j in range(n_sets)]
     batch = pack_requests([(True, [s]) for s in sets])
@@ -138,6 +142,9 @@ def main() -> None:
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=12, help="batches in flight per GPU (contexts/streams)")
+    ap.add_argument("--roots", type=int, default=0,
+                    help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
+    ap.add_argument("--no-dedup", action="store_true", help="hash every set's root (BLS_DEBUG_NO_MSG_DEDUP)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,7 +172,12 @@ def main() -> None:
     # verifyManySignatureSets jobs in flight (multithread/index.ts:199-233).
     ctxs = [GpuContext(local_rank) for _ in range(args.inflight)]
     gpu = ctxs[0]
-    works = [make_workload(c, args.sets, rank) for c in ctxs]
+    works = [make_workload(c, args.sets, rank, args.roots) for c in ctxs]
+    if args.no_dedup:
+        from lodestar_amd._abi import DEBUG_NO_MSG_DEDUP
+
+        for c in ctxs:
+            c.set_debug_flags(DEBUG_NO_MSG_DEDUP)
     batch, call128, _ = works[0]
 
     for c, w in zip(ctxs, works):
@@ -236,8 +248,11 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "u32 (381-bit Fp, 12x32-bit Montgomery limbs)",
             "data": "synthetic: interop keys, sha256 messages, GPU-made signatures",
-            "config": {"workload": "cfg2: 1024 single-pubkey gossip sets per GPU, batchable requests, "
-                                   "random-scalar batch in chunks of 16 requests",
+            "config": {"workload": ("cfg2: 1024 single-pubkey gossip sets per GPU, batchable requests, "
+                                    "random-scalar batch in chunks of 16 requests") if args.roots == 0 else
+                                   (f"cfg5 shape: {args.sets} single-pubkey sets per call over {args.roots} "
+                                    f"committee-shared signing roots, batchable requests"
+                                    + (", root dedup off" if args.no_dedup else "")),
                        "sets_per_step_per_gpu": args.sets, "inflight_batches_per_gpu": args.inflight,
                        "parallelism": f"shard-by-request x{world}"},
             "p50_latency_ms_128": round(statistics.median(lat), 3),

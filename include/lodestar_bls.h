@@ -67,6 +67,7 @@ typedef struct bls_stats {
   uint32_t n_flagged;          /* sets finished by the exact single-lane path */
   double device_ms;            /* device time of the call (HIP events) */
   double stage_ms[8];          /* per stage: h2d, pk, pre (SSWU + sig decode), pset, exact, -, status+chunk, individual */
+  uint32_t n_unique_msgs;      /* distinct signing roots hashed to the curve (== n_sets without dedup) */
 } bls_stats;
 
 typedef struct bls_gpu_ctx bls_gpu_ctx;
@@ -163,6 +164,9 @@ int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint
 /* Test hook: BLS_DEBUG_FORCE_EXACT routes every set through the exact single-lane
  * path (stage_exact_set) instead of the cooperative programs, so parity tests cover both. */
 #define BLS_DEBUG_FORCE_EXACT 1u
+/* Test / bench hook: compute hash_to_field + SSWU per set even when sets share a
+ * signing root (the default dedups them, plan_msg_dedup in bls/pipeline.hpp). */
+#define BLS_DEBUG_NO_MSG_DEDUP 2u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

@@ -56,6 +56,7 @@ SYMBOLS = (
     "bls_gpu_set_debug_flags",
 )
 DEBUG_FORCE_EXACT = 1
+DEBUG_NO_MSG_DEDUP = 2
 
 
 class BlsBatch(ctypes.Structure):
@@ -83,6 +84,7 @@ class BlsStats(ctypes.Structure):
         ("n_flagged", ctypes.c_uint32),
         ("device_ms", ctypes.c_double),
         ("stage_ms", ctypes.c_double * 8),
+        ("n_unique_msgs", ctypes.c_uint32),
     ]
 
 

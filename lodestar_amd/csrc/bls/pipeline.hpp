@@ -42,6 +42,11 @@ struct PipeBufs {
   const uint8_t* sigs;         // n_sets * 96
   const uint32_t* sig_lens;    // nullable
   const uint32_t* seed;        // 8 words
+  // signing-root dedup (nullable; plan_msg_dedup): SSWU points are computed once
+  // per distinct 32-byte root and shared by every set signing that root
+  const uint32_t* msg_uniq;    // n_uniq set indices: the first set of each distinct root
+  const uint32_t* msg_rep;     // n_sets: the set whose SSWU points set i shares
+  uint32_t n_uniq;
   uint32_t scalar_base;        // set i draws r from index scalar_base + i (shards of one call, bls_gpu_partial)
   const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs
   const uint32_t* chunk_reqs;
@@ -174,14 +179,18 @@ BLS_HD void stage_pair_set(const PipeBufs& b, uint32_t i) {
   }
 }
 
-// GPU pre-stage, one lane per task t in [0, 3 n_sets):
-//   t < 2n:  SSWU point q_{t%2} of set t/2 (map_to_curve_sswu_fast; on its rare
-//            false return the set is flagged for the exact path)
-//   t >= 2n: decode signature t - 2n (on-curve, no subgroup test: k_pset does it)
+// GPU pre-stage, one lane per task t in [0, pre_lanes(b)); u = distinct roots
+// (n_uniq with dedup, else n_sets):
+//   t < 2u:  SSWU point q_{t%2} of the set msg_uniq[t/2] (map_to_curve_sswu_fast;
+//            on its rare false return the set is flagged for the exact path)
+//   t >= 2u: decode signature t - 2u (on-curve, no subgroup test: k_pset does it)
+BLS_HD uint32_t pre_roots(const PipeBufs& b) { return b.msg_uniq ? b.n_uniq : b.n_sets; }
+BLS_HD uint32_t pre_lanes(const PipeBufs& b) { return 2 * pre_roots(b) + b.n_sets; }
+
 BLS_HD void stage_pre(const PipeBufs& b, uint32_t t) {
-  const uint32_t n = b.n_sets;
-  if (t < 2 * n) {
-    const uint32_t i = t >> 1;
+  const uint32_t n = b.n_sets, u = pre_roots(b);
+  if (t < 2 * u) {
+    const uint32_t i = b.msg_uniq ? b.msg_uniq[t >> 1] : t >> 1;
     uint32_t w[8];
     msg_words_from_bytes(b.msgs + 32ull * i, w);
     Fp2 u0, u1;
@@ -198,8 +207,8 @@ BLS_HD void stage_pre(const PipeBufs& b, uint32_t t) {
     }
     return;
   }
-  if (t >= 3 * n) return;
-  const uint32_t i = t - 2 * n;
+  if (t >= 2 * u + n) return;
+  const uint32_t i = t - 2 * u;
   G2A s;
   s.inf = true;
   s.x = fp2_zero();
@@ -207,6 +216,18 @@ BLS_HD void stage_pre(const PipeBufs& b, uint32_t t) {
   int32_t code = (b.sig_lens && b.sig_lens[i] != 96) ? BLS_INVALID_SIZE : g2_decompress96(b.sigs + 96ull * i, s);
   b.sig[i] = s;
   b.sig_status[i] = code;
+}
+
+// After stage_pre with dedup: a set whose root is not the first of its kind takes
+// the representative's SSWU points (and its exact-path flag), one lane per
+// (set, Fp word) so the copy is coalesced.
+BLS_HD void stage_qdup(const PipeBufs& b, uint32_t t) {
+  const uint32_t i = t >> 3, k = t & 7;
+  if (!b.msg_rep || i >= b.n_sets) return;
+  const uint32_t r = b.msg_rep[i];
+  if (r == i) return;
+  b.q[8ull * i + k] = b.q[8ull * r + k];
+  if (k == 0 && b.set_flag[r]) b.set_flag[i] = 1u;
 }
 
 // Exact per-set path for sets k_pset flagged: subgroup test, H(m), r pk, r sig and
@@ -292,6 +313,7 @@ BLS_HD void stage_indiv(const PipeBufs& b, uint32_t t) {
 
 // Host-side planning (plain host functions; parsed but not emitted in the device pass).
 #include <stdlib.h>
+#include <string.h>
 #include <vector>
 
 namespace bls {
@@ -330,6 +352,46 @@ static inline void plan_batch(const bls_batch* in, BatchPlan& p) {
     return;
   }
   chunkify_maximize_chunk_size((uint32_t)batchable.size(), 16, p.chunk_off);
+}
+
+// Signing-root dedup for stage_pre: uniq = the first set of each distinct 32-byte
+// root (in set order), rep[i] = that first set for set i.  Committee-shared roots
+// (~512 attesters per root) then pay hash_to_field + SSWU once.
+// Open addressing over a mix of all 32 bytes, so crafted roots cost probes, not
+// wrong answers.  Returns the number of distinct roots.
+static inline uint32_t plan_msg_dedup(const uint8_t* msgs, uint32_t n, std::vector<uint32_t>& uniq,
+                                      std::vector<uint32_t>& rep) {
+  uniq.clear();
+  rep.resize(n);
+  uint32_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
+  std::vector<uint32_t> slot(cap, 0xffffffffu);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* m = msgs + 32ull * i;
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (int w = 0; w < 4; ++w) {
+      uint64_t v;
+      memcpy(&v, m + 8 * w, 8);
+      h = (h ^ v) * 0xff51afd7ed558ccdull;
+      h ^= h >> 32;
+    }
+    uint32_t pos = (uint32_t)h & (cap - 1);
+    for (;;) {
+      const uint32_t j = slot[pos];
+      if (j == 0xffffffffu) {
+        slot[pos] = i;
+        rep[i] = i;
+        uniq.push_back(i);
+        break;
+      }
+      if (memcmp(msgs + 32ull * j, m, 32) == 0) {
+        rep[i] = j;
+        break;
+      }
+      pos = (pos + 1) & (cap - 1);
+    }
+  }
+  return (uint32_t)uniq.size();
 }
 
 // Fill verdicts / stats from chunk results and the individual pass.

@@ -318,4 +318,42 @@ int hs_verify_batch(const bls_batch* in, int32_t* verdicts, bls_stats* stats) {
   return 0;
 }
 
+// Signing-root dedup: plan_msg_dedup + stage_pre (2u map lanes) + stage_qdup must
+// leave every set with the SSWU points and flags the per-set pre-stage gives it.
+// Returns n_uniq, or -1 on a mismatch (q_out gets the deduplicated points).
+int hs_pre_dedup_check(const uint8_t* msgs, uint32_t n, uint32_t* uniq_out, uint32_t* rep_out, uint8_t* q_out) {
+  std::vector<uint32_t> uniq, rep;
+  const uint32_t u = plan_msg_dedup(msgs, n, uniq, rep);
+  std::vector<uint8_t> sigs(96ull * n, 0);
+  std::vector<uint32_t> lens(n, 0);
+  std::vector<G2A> sig(n);
+  std::vector<int32_t> sig_status(n);
+  std::vector<Fp> q_plain(8ull * n), q_dedup(8ull * n);
+  std::vector<uint32_t> flag_plain(n, 0), flag_dedup(n, 0);
+  PipeBufs b;
+  memset(&b, 0, sizeof(b));
+  b.n_sets = n;
+  b.msgs = msgs;
+  b.sigs = sigs.data();
+  b.sig_lens = lens.data();
+  b.sig = sig.data();
+  b.sig_status = sig_status.data();
+  b.q = q_plain.data();
+  b.set_flag = flag_plain.data();
+  for (uint32_t t = 0; t < pre_lanes(b); ++t) stage_pre(b, t);
+  b.q = q_dedup.data();
+  b.set_flag = flag_dedup.data();
+  b.msg_uniq = uniq.data();
+  b.msg_rep = rep.data();
+  b.n_uniq = u;
+  for (uint32_t t = 0; t < pre_lanes(b); ++t) stage_pre(b, t);
+  for (uint32_t t = 0; t < 8 * n; ++t) stage_qdup(b, t);
+  for (uint32_t i = 0; i < u; ++i) uniq_out[i] = uniq[i];
+  for (uint32_t i = 0; i < n; ++i) rep_out[i] = rep[i];
+  memcpy(q_out, q_dedup.data(), sizeof(Fp) * 8ull * n);
+  if (memcmp(q_plain.data(), q_dedup.data(), sizeof(Fp) * 8ull * n) != 0) return -1;
+  if (flag_plain != flag_dedup) return -1;
+  return (int)u;
+}
+
 }  // extern "C"

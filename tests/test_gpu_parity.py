@@ -249,6 +249,46 @@ def test_exact_path_matches_cooperative_path(gpu, oracle, golden, table):
     assert list(v0[:5]) == [1] * 5 and v0[5] == 0
 
 
+@pytest.mark.gpu
+def test_committee_shared_roots_dedup(gpu, oracle, table):
+    """gossip attestations of one committee share a
+    signing root, so hash_to_field + SSWU run once per distinct root (n_unique_msgs).
+    Verdicts match the per-set pre-stage and the exact path, with invalid sets (a
+    signature over another root, a wrong key) mixed into the shared-root chunks."""
+    from lodestar_amd._abi import DEBUG_FORCE_EXACT, DEBUG_NO_MSG_DEDUP
+
+    n = 48
+    roots = [_h(b"committee-root%d" % k) for k in range(3)]
+    sks = _keys(oracle, 16)
+    msgs = [roots[(i * 7) % 3] for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    reqs, expect = [], []
+    for i in range(n):
+        sig, pk = sigs[i].tobytes(), [i % 16]
+        if i == 9:
+            sig = sigs[10].tobytes() if msgs[10] != msgs[9] else sigs[11].tobytes()  # other root
+        if i == 30:
+            pk = [(i + 1) % 16]  # another committee member's key
+        reqs.append((True, [(pk, msgs[i], sig)]))
+        expect.append(0 if i in (9, 30) else 1)
+    reqs.append((False, [([i % 16], msgs[i], sigs[i].tobytes()) for i in range(12)]))  # 1 request, 12 sets, 3 roots
+    expect.append(1)
+    pb = pack_requests(reqs)
+    v0, st0 = gpu.verify_packed(pb)
+    assert list(v0) == expect
+    assert st0.n_unique_msgs == 3
+    results = {}
+    for flags in (DEBUG_NO_MSG_DEDUP, DEBUG_FORCE_EXACT):
+        try:
+            gpu.set_debug_flags(flags)
+            results[flags] = gpu.verify_packed(pb)
+        finally:
+            gpu.set_debug_flags(0)
+    assert list(results[DEBUG_NO_MSG_DEDUP][0]) == expect
+    assert results[DEBUG_NO_MSG_DEDUP][1].n_unique_msgs == n + 12
+    assert list(results[DEBUG_FORCE_EXACT][0]) == expect
+
+
 # ---------------------------------------------------------------------------
 # SURVEY §8e: one call sharded into Fp12 partials + one final exponentiation
 # ---------------------------------------------------------------------------

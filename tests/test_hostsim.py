@@ -186,3 +186,34 @@ def test_pipeline_semantics(hostsim, oracle):
     v, st = _hs_verify(hostsim, bad + [(False, sets[:4]), (False, [])])
     assert v == [1, 1, 1, 0, 1, 1, 1, -8] + [1] * 12 + [1, -10]
     assert st.batch_retries == 1 and st.n_individual == n + 2
+
+
+def test_signing_root_dedup_pre_stage(hostsim):
+    """plan_msg_dedup + stage_pre over distinct roots + stage_qdup give every set the
+    SSWU points of the per-set pre-stage (committee-shared roots)."""
+    import ctypes
+    import hashlib
+
+    import numpy as np
+
+    roots = [hashlib.sha256(b"root%d" % k).digest() for k in range(5)]
+    order = [3, 0, 3, 1, 4, 0, 0, 2, 3, 4, 1, 3]  # ragged multiplicities, first use out of order
+    msgs = b"".join(roots[k] for k in order)
+    n = len(order)
+    uniq = np.zeros(n, np.uint32)
+    rep = np.zeros(n, np.uint32)
+    q = np.zeros(n * 8 * 48, np.uint8)
+    f = hostsim.hs_pre_dedup_check
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    u = f(msgs, n, uniq.ctypes.data, rep.ctypes.data, q.ctypes.data)
+    assert u == 5
+    first = {}
+    for i, k in enumerate(order):
+        first.setdefault(k, i)
+    assert list(uniq[:u]) == sorted(first.values())
+    assert list(rep) == [first[k] for k in order]
+    # all-distinct and all-equal extremes
+    assert f(b"".join(roots), 5, uniq.ctypes.data, rep.ctypes.data, q.ctypes.data) == 5
+    assert f(roots[2] * 7, 7, uniq.ctypes.data, rep.ctypes.data, q.ctypes.data) == 1
+    assert list(rep[:7]) == [0] * 7
