@@ -145,6 +145,8 @@ def main() -> None:
     ap.add_argument("--roots", type=int, default=0,
                     help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
     ap.add_argument("--no-dedup", action="store_true", help="hash every set's root (BLS_DEBUG_NO_MSG_DEDUP)")
+    ap.add_argument("--no-merged-check", action="store_true",
+                    help="one final exponentiation per chunk only (BLS_DEBUG_NO_MERGED_CHECK)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,11 +175,11 @@ def main() -> None:
     ctxs = [GpuContext(local_rank) for _ in range(args.inflight)]
     gpu = ctxs[0]
     works = [make_workload(c, args.sets, rank, args.roots) for c in ctxs]
-    if args.no_dedup:
-        from lodestar_amd._abi import DEBUG_NO_MSG_DEDUP
+    from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK, DEBUG_NO_MSG_DEDUP
 
-        for c in ctxs:
-            c.set_debug_flags(DEBUG_NO_MSG_DEDUP)
+    flags = (DEBUG_NO_MSG_DEDUP if args.no_dedup else 0) | (DEBUG_NO_MERGED_CHECK if args.no_merged_check else 0)
+    for c in ctxs:
+        c.set_debug_flags(flags)
     batch, call128, _ = works[0]
 
     for c, w in zip(ctxs, works):
@@ -252,7 +254,8 @@ def main() -> None:
                                     "random-scalar batch in chunks of 16 requests") if args.roots == 0 else
                                    (f"cfg5 shape: {args.sets} single-pubkey sets per call over {args.roots} "
                                     f"committee-shared signing roots, batchable requests"
-                                    + (", root dedup off" if args.no_dedup else "")),
+                                    + (", root dedup off" if args.no_dedup else ""))
+                                   + (", merged check off" if args.no_merged_check else ""),
                        "sets_per_step_per_gpu": args.sets, "inflight_batches_per_gpu": args.inflight,
                        "parallelism": f"shard-by-request x{world}"},
             "p50_latency_ms_128": round(statistics.median(lat), 3),

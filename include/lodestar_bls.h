@@ -68,6 +68,7 @@ typedef struct bls_stats {
   double device_ms;            /* device time of the call (HIP events) */
   double stage_ms[8];          /* per stage: h2d, pk, pre (SSWU + sig decode), pset, exact, -, status+chunk, individual */
   uint32_t n_unique_msgs;      /* distinct signing roots hashed to the curve (== n_sets without dedup) */
+  uint32_t merged_check;       /* 0 not run, 1 passed (per-chunk checks skipped), 2 failed (chunks checked) */
 } bls_stats;
 
 typedef struct bls_gpu_ctx bls_gpu_ctx;
@@ -167,6 +168,9 @@ int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint
 /* Test / bench hook: compute hash_to_field + SSWU per set even when sets share a
  * signing root (the default dedups them, plan_msg_dedup in bls/pipeline.hpp). */
 #define BLS_DEBUG_NO_MSG_DEDUP 2u
+/* Test / bench hook: skip the merged check (one final exponentiation over every
+ * chunk's sets before the per-chunk ones) and go straight to the chunk verdicts. */
+#define BLS_DEBUG_NO_MERGED_CHECK 4u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

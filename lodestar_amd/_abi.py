@@ -57,6 +57,7 @@ SYMBOLS = (
 )
 DEBUG_FORCE_EXACT = 1
 DEBUG_NO_MSG_DEDUP = 2
+DEBUG_NO_MERGED_CHECK = 4
 
 
 class BlsBatch(ctypes.Structure):
@@ -85,6 +86,7 @@ class BlsStats(ctypes.Structure):
         ("device_ms", ctypes.c_double),
         ("stage_ms", ctypes.c_double * 8),
         ("n_unique_msgs", ctypes.c_uint32),
+        ("merged_check", ctypes.c_uint32),
     ]
 
 

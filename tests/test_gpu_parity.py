@@ -250,6 +250,37 @@ def test_exact_path_matches_cooperative_path(gpu, oracle, golden, table):
 
 
 @pytest.mark.gpu
+def test_merged_check_matches_chunk_verdicts(gpu, oracle, table):
+    """The merged check (one final exponentiation over all chunks' sets) passes only
+    when every chunk would; otherwise the per-chunk verdicts decide, so verdicts and
+    stats equal those of the chunked worker (worker.ts:56-88) with it switched off."""
+    from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK
+
+    n = 48
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"merged%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    good = [(True, [([i % 16], msgs[i], sigs[i].tobytes())]) for i in range(n)]
+    one_bad = list(good)
+    one_bad[20] = (True, [([20 % 16], _h(b"tampered"), sigs[20].tobytes())])
+    err = list(good)
+    err[33] = (True, [([33 % 16], msgs[33], bytes(32))])  # BLST_INVALID_SIZE inside a chunk
+    for reqs, merged_expect in ((good, 1), (one_bad, 2), (err, 2)):
+        pb = pack_requests(reqs)
+        v0, st0 = gpu.verify_packed(pb)
+        try:
+            gpu.set_debug_flags(DEBUG_NO_MERGED_CHECK)
+            v1, st1 = gpu.verify_packed(pb)
+        finally:
+            gpu.set_debug_flags(0)
+        assert list(v0) == list(v1)
+        assert st0.merged_check == merged_expect and st1.merged_check == 0
+        assert (st0.batch_retries, st0.batch_sigs_success, st0.n_chunks) == \
+            (st1.batch_retries, st1.batch_sigs_success, st1.n_chunks)
+    assert list(v0) == [1] * 33 + [-CODE_INVALID_SIZE] + [1] * 14
+
+
+@pytest.mark.gpu
 def test_committee_shared_roots_dedup(gpu, oracle, table):
     """gossip attestations of one committee share a
     signing root, so hash_to_field + SSWU run once per distinct root (n_unique_msgs).
