@@ -40,8 +40,10 @@ sys.path.insert(0, str(ROOT))
 # queues (default 4 on this image), and streams sharing a queue serialise.  Give the
 # in-flight contexts their own queues (set before the HIP runtime initialises; the
 # box exports 4, so raise it rather than default it).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+# 16 batches over 24 queues measured best (tools/gpu_inflight_q.sh: 12/16 384k,
+# 16/24 403k, 20/24 382k sets/s).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 STAGE_NAMES = ["h2d", "k_pk", "k_pre", "k_pset", "k_exact", "-", "k_status+k_chunk", "k_indiv"]
@@ -136,12 +138,12 @@ def cpu_baseline(sample_sets: int = 16, procs: int = 16) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=1024)
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=12, help="batches in flight per GPU (contexts/streams)")
+    ap.add_argument("--inflight", type=int, default=16, help="batches in flight per GPU (contexts/streams)")
     ap.add_argument("--roots", type=int, default=0,
                     help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
     ap.add_argument("--no-dedup", action="store_true", help="hash every set's root (BLS_DEBUG_NO_MSG_DEDUP)")
