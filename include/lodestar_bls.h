@@ -89,8 +89,9 @@ const char* bls_gpu_last_error(const bls_gpu_ctx* ctx);
 /* Load / append trusted validator pubkeys into the device table (Index2PubkeyCache,
  * state-transition/src/cache/pubkeyCache.ts:56-77).  pk_len is 48 (compressed) or 96
  * (uncompressed).  codes (nullable, n entries) receive a per-key decode code; keys
- * are not subgroup-checked (trusted, pubkeyCache.ts:72-75).  Returns the new table
- * size (>= 0) or < 0 on failure. */
+ * are not subgroup-checked (trusted, pubkeyCache.ts:72-75).  All or nothing: when any
+ * key fails to decode, no key is appended (the table keeps its size, so indices stay
+ * aligned across contexts).  Returns the new table size (>= 0) or < 0 on failure. */
 int64_t bls_gpu_load_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes);
 
 /* KeyValidate for n public keys (blst PublicKey.fromBytes(bytes, validate=true) [ext],
@@ -136,6 +137,14 @@ int bls_gpu_final_check(bls_gpu_ctx* ctx, const uint8_t* partials576, uint32_t n
 int bls_gpu_aggregate_pubkeys(bls_gpu_ctx* ctx, const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
                               uint32_t n_sets, uint8_t* out96, int32_t* codes);
 
+/* Signature.fromBytes(bytes, CoordType.affine, validate) ([ext] @chainsafe/blst, as
+ * maybeBatch.ts:23,36 call it): n 96-byte compressed G2 points -> out192 (uncompressed
+ * ZCash order x.c1 || x.c0 || y.c1 || y.c0; the infinity encoding for the point at
+ * infinity) and codes (0, or BLS_CODE_BAD_ENCODING / POINT_NOT_ON_CURVE /
+ * POINT_NOT_IN_GROUP; the subgroup test only when validate != 0). */
+int bls_gpu_g2_decompress(bls_gpu_ctx* ctx, const uint8_t* in96, uint32_t n, int validate, uint8_t* out192,
+                          int32_t* codes);
+
 /* hash_to_G2 with the POP DST for n 32-byte messages; out: n * 192 bytes (uncompressed
  * ZCash order x.c1 || x.c0 || y.c1 || y.c0). */
 int bls_gpu_hash_to_g2(bls_gpu_ctx* ctx, const uint8_t* msgs, uint32_t n, uint8_t* out192);
@@ -171,6 +180,10 @@ int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint
 /* Test / bench hook: skip the merged check (one final exponentiation over every
  * chunk's sets before the per-chunk ones) and go straight to the chunk verdicts. */
 #define BLS_DEBUG_NO_MERGED_CHECK 4u
+/* Test / bench hook: sets per wavefront of the per-set cooperative kernel (1, 2 or 3;
+ * 0 = by call size), so one process can run the same call through every packing. */
+#define BLS_DEBUG_PACK(n) ((uint32_t)(n) << 8)
+#define BLS_DEBUG_PACK_MASK 0x300u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

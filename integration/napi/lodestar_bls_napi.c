@@ -34,6 +34,33 @@
     }                                                               \
   } while (0)
 
+/* One handle per JS verifier context.  Every entry point runs on the JS main thread
+ * (verify_execute only touches ctx on a libuv worker), so the counters need no
+ * locking.  close() while verifies are queued or running only marks the handle; the
+ * last completing verify releases the device context.  Each queued job also holds a
+ * reference to the handle's external, so the GC finalizer cannot run under it. */
+typedef struct {
+  bls_gpu_ctx* ctx;
+  uint32_t inflight;
+  int closed;
+} bls_handle;
+
+static void handle_release_if_idle(bls_handle* h) {
+  if (h->closed && h->inflight == 0 && h->ctx) {
+    bls_gpu_close(h->ctx);
+    h->ctx = NULL;
+  }
+}
+
+static void handle_finalize(napi_env env, void* data, void* hint) {
+  (void)env;
+  (void)hint;
+  bls_handle* h = (bls_handle*)data;
+  h->closed = 1;
+  handle_release_if_idle(h);
+  free(h);
+}
+
 static napi_value js_init(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -45,23 +72,30 @@ static napi_value js_init(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "bls_gpu_init failed (no HIP device?)");
     return NULL;
   }
+  bls_handle* h = (bls_handle*)calloc(1, sizeof(bls_handle));
+  h->ctx = ctx;
   napi_value ext;
-  CHECK(env, napi_create_external(env, ctx, NULL, NULL, &ext));
+  CHECK(env, napi_create_external(env, h, handle_finalize, NULL, &ext));
   return ext;
 }
 
-static bls_gpu_ctx* get_ctx(napi_env env, napi_value v) {
+/* the live handle behind v, or NULL (not a handle, or closed: use after close) */
+static bls_handle* get_handle(napi_env env, napi_value v) {
   void* p = NULL;
-  if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
-  return (bls_gpu_ctx*)p;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) return NULL;
+  bls_handle* h = (bls_handle*)p;
+  return h->closed ? NULL : h;
 }
 
 static napi_value js_close(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bls_gpu_ctx* ctx = get_ctx(env, argv[0]);
-  if (ctx) bls_gpu_close(ctx);
+  bls_handle* h = get_handle(env, argv[0]);
+  if (h) {
+    h->closed = 1;
+    handle_release_if_idle(h);
+  }
   return NULL;
 }
 
@@ -90,11 +124,11 @@ static napi_value js_load_pubkeys(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bls_gpu_ctx* ctx = get_ctx(env, argv[0]);
+  bls_handle* h = get_handle(env, argv[0]);
   void* pks;
   size_t bytes;
   uint32_t pk_len = 48;
-  if (!ctx || view_of(env, argv[1], &pks, &bytes)) {
+  if (!h || view_of(env, argv[1], &pks, &bytes)) {
     napi_throw_type_error(env, NULL, "loadPubkeys(handle, Uint8Array, pkLen)");
     return NULL;
   }
@@ -104,17 +138,19 @@ static napi_value js_load_pubkeys(napi_env env, napi_callback_info info) {
   void* codes;
   CHECK(env, napi_create_arraybuffer(env, 4 * (size_t)(n ? n : 1), &codes, &ab));
   CHECK(env, napi_create_typedarray(env, napi_int32_array, n, ab, 0, &out));
-  if (bls_gpu_load_pubkeys(ctx, (const uint8_t*)pks, n, pk_len, (int32_t*)codes) < 0) {
-    napi_throw_error(env, NULL, bls_gpu_last_error(ctx));
+  if (bls_gpu_load_pubkeys(h->ctx, (const uint8_t*)pks, n, pk_len, (int32_t*)codes) < 0) {
+    napi_throw_error(env, NULL, bls_gpu_last_error(h->ctx));
     return NULL;
   }
   return out;
 }
 
 typedef struct {
+  bls_handle* h;
   bls_gpu_ctx* ctx;
   bls_batch batch;
   napi_ref keep;          /* the request object: keeps the input buffers alive */
+  napi_ref keep_handle;   /* the handle's external: no finalizer while the job is out */
   int32_t* verdicts;
   int rc;
   napi_deferred deferred;
@@ -147,7 +183,10 @@ static void verify_complete(napi_env env, napi_status status, void* data) {
     napi_resolve_deferred(env, j->deferred, out);
   }
   napi_delete_reference(env, j->keep);
+  napi_delete_reference(env, j->keep_handle);
   napi_delete_async_work(env, j->work);
+  j->h->inflight -= 1;
+  handle_release_if_idle(j->h);
   free(j->verdicts);
   free(j);
 }
@@ -162,42 +201,56 @@ static napi_value js_verify(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bls_gpu_ctx* ctx = get_ctx(env, argv[0]);
-  if (!ctx || argc < 2) {
-    napi_throw_type_error(env, NULL, "verify(handle, request)");
+  bls_handle* h = argc >= 2 ? get_handle(env, argv[0]) : NULL;
+  if (!h) {
+    napi_throw_type_error(env, NULL, "verify(handle, request): no live handle (closed?)");
     return NULL;
   }
-  verify_job* j = (verify_job*)calloc(1, sizeof(verify_job));
-  j->ctx = ctx;
   void *ro, *rb, *msg, *sig, *spo, *pki, *pks, *sl, *seed;
   size_t nro, nrb, nmsg, nsig, nspo, npki, npks, nsl, nseed;
   if (prop(env, argv[1], "reqSetOffsets", &ro, &nro) || prop(env, argv[1], "reqBatchable", &rb, &nrb) ||
       prop(env, argv[1], "messages", &msg, &nmsg) || prop(env, argv[1], "signatures", &sig, &nsig) ||
       prop(env, argv[1], "setPkOffsets", &spo, &nspo) || prop(env, argv[1], "pkIndices", &pki, &npki) ||
       prop(env, argv[1], "pubkeys", &pks, &npks) || prop(env, argv[1], "signatureLens", &sl, &nsl) ||
-      prop(env, argv[1], "seed", &seed, &nseed) || nro < 4) {
-    free(j);
+      prop(env, argv[1], "seed", &seed, &nseed) || nro < 4 || !ro) {
     napi_throw_type_error(env, NULL, "verify: bad request object");
     return NULL;
   }
-  j->batch.n_reqs = (uint32_t)(nro / 4 - 1);
-  j->batch.n_sets = ((const uint32_t*)ro)[j->batch.n_reqs];
+  /* every buffer must hold what n_reqs / n_sets say: the library reads exactly that */
+  const uint32_t n_reqs = (uint32_t)(nro / 4 - 1);
+  const uint32_t n_sets = ((const uint32_t*)ro)[n_reqs];
+  const size_t ns = n_sets;
+  int ok = nrb >= n_reqs && nmsg >= 32 * ns && nsig >= 96 * ns && (!sl || nsl >= 4 * ns);
+  if (spo) ok = ok && nspo >= 4 * (ns + 1) && npki >= 4 * (size_t)((const uint32_t*)spo)[n_sets];
+  else ok = ok && pks && npks >= 96 * ns;
+  if (!ok) {
+    napi_throw_range_error(env, NULL, "verify: a buffer is shorter than n_reqs / n_sets require "
+                                      "(pubkeys 96 B, messages 32 B, signatures 96 B per set)");
+    return NULL;
+  }
+  verify_job* j = (verify_job*)calloc(1, sizeof(verify_job));
+  j->h = h;
+  j->ctx = h->ctx;
+  j->batch.n_reqs = n_reqs;
+  j->batch.n_sets = n_sets;
   j->batch.req_set_offsets = (const uint32_t*)ro;
   j->batch.req_batchable = (const uint8_t*)rb;
   j->batch.messages = (const uint8_t*)msg;
   j->batch.signatures = (const uint8_t*)sig;
   j->batch.set_pk_offsets = (const uint32_t*)spo;
   j->batch.pk_indices = (const uint32_t*)pki;
-  j->batch.pubkeys = (const uint8_t*)pks;
+  j->batch.pubkeys = spo ? NULL : (const uint8_t*)pks;
   j->batch.signature_lens = (const uint32_t*)sl;
   j->batch.seed = nseed >= 32 ? (const uint8_t*)seed : NULL;
-  j->verdicts = (int32_t*)calloc(j->batch.n_reqs ? j->batch.n_reqs : 1, 4);
+  j->verdicts = (int32_t*)calloc(n_reqs ? n_reqs : 1, 4);
   napi_value promise, name;
   CHECK(env, napi_create_reference(env, argv[1], 1, &j->keep));
+  CHECK(env, napi_create_reference(env, argv[0], 1, &j->keep_handle));
   CHECK(env, napi_create_promise(env, &j->deferred, &promise));
   CHECK(env, napi_create_string_utf8(env, "lodestar_bls_verify", NAPI_AUTO_LENGTH, &name));
   CHECK(env, napi_create_async_work(env, NULL, name, verify_execute, verify_complete, j, &j->work));
   CHECK(env, napi_queue_async_work(env, j->work));
+  h->inflight += 1;
   return promise;
 }
 

@@ -47,6 +47,7 @@ SYMBOLS = (
     "bls_gpu_partial",
     "bls_gpu_final_check",
     "bls_gpu_hash_to_g2",
+    "bls_gpu_g2_decompress",
     "bls_gpu_sk_to_pk",
     "bls_gpu_sign",
     "bls_gpu_mad_peak",
@@ -58,6 +59,11 @@ SYMBOLS = (
 DEBUG_FORCE_EXACT = 1
 DEBUG_NO_MSG_DEDUP = 2
 DEBUG_NO_MERGED_CHECK = 4
+
+
+def DEBUG_PACK(n: int) -> int:
+    """sets per wavefront of the per-set kernel (BLS_DEBUG_PACK in lodestar_bls.h)"""
+    return n << 8
 
 
 class BlsBatch(ctypes.Structure):
@@ -113,6 +119,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_final_check.restype = i32
         lib.bls_gpu_aggregate_pubkeys.argtypes = [vp, vp, vp, u32, vp, vp]
         lib.bls_gpu_aggregate_pubkeys.restype = i32
+        lib.bls_gpu_g2_decompress.argtypes = [vp, vp, u32, i32, vp, vp]
+        lib.bls_gpu_g2_decompress.restype = i32
         lib.bls_gpu_hash_to_g2.argtypes = [vp, vp, u32, vp]
         lib.bls_gpu_hash_to_g2.restype = i32
         lib.bls_gpu_sk_to_pk.argtypes = [vp, vp, u32, vp]

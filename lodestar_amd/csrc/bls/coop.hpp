@@ -24,7 +24,7 @@ namespace bls {
 #define COOP_OUT_ZCHECK 0xFFFFu
 #define COOP_OUT_NONE 0xFFFEu   // lane idle (kind 0, never written)
 #define COOP_OUT_ZSET 0xFFF0u   // zero-check of packed set s >= 1: 0xFFF0 + s
-#define COOP_MAX_CONSTS 64
+#define COOP_MAX_CONSTS 40  // constants staged per block (tools/gen_coop.py asserts the bank fits)
 
 struct CoopOp {  // 80 bytes, one per lane per step (tools/gen_coop.py:emit)
   uint16_t out;
@@ -58,7 +58,8 @@ struct CoopLdsN {
   uint32_t flag;
 };
 
-#define COOP_FRAME2 512  // the 2-set packed programs (tools/gen_coop.py FRAME2)
+#define COOP_FRAME2 380  // the 2-set packed programs (tools/gen_coop.py FRAME2): with the
+                         // 40-constant bank 20.2 KB of LDS, 8 blocks = 2 wavefronts per SIMD
 #define COOP_FRAME3 640  // the 3-set packed programs (tools/gen_coop.py FRAME3)
 
 // Programs of S sets packed in one wavefront (tools/gen_pset.py build_pset(S)):
@@ -126,6 +127,7 @@ __device__ __forceinline__ void lds_store_fp(Fp* frame, uint32_t slot, const Fp&
 // The same through an explicit LDS (address space 3) pointer: 32-bit addressing with
 // no generic-pointer checks per access (the interpreter converts its frame once).
 typedef unsigned int bls_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int bls_u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) bls_u32x4 LdsU4;
 
 __device__ __forceinline__ Fp lds_load_fp(const LdsU4* base, uint32_t slot) {
@@ -261,50 +263,112 @@ __device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t 
   return acc_reduce(acc, negs);
 }
 
-union CoopOpWords {
-  uint4 w[5];
-  CoopOp op;
+// One lane's op of one step as fetched: the 80-byte CoopOp as 20 raw dwords, loaded
+// with five global (not flat) dwordx4 loads.  Fields are decoded only where the
+// step that owns the op executes, so the loads of the next step's op stay in flight
+// (vmcnt only; flat loads would also hold lgkmcnt and stall every LDS wait).
+struct CoopOpRaw {
+  bls_u32x4 w[4];
+  bls_u32x2 t;  // dwords 16, 17 (cb[4..7]); the 8 pad bytes are never loaded
+};
+typedef __attribute__((address_space(1))) const bls_u32x4 GlobU4;
+typedef __attribute__((address_space(1))) const bls_u32x2 GlobU2;
+
+// Unconditional (every lane, every step), so the compiler can count the loads in
+// flight with vmcnt instead of waiting for them at a control-flow merge.
+__device__ __forceinline__ void coop_fetch(CoopOpRaw& u, const GlobU4* base, uint32_t step, int lane) {
+  const GlobU4* src = base + ((size_t)step * COOP_LANES + lane) * 5;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) u.w[k] = src[k];
+  u.t = *(const GlobU2*)(src + 4);
+}
+
+// dword k (0..19) of the raw op
+__device__ __forceinline__ uint32_t op_word(const CoopOpRaw& u, int k) { return k < 16 ? u.w[k >> 2][k & 3] : u.t[k & 1]; }
+
+// Decoded view of a raw op (CoopOp layout: out u16, kind u8, na u8 | nb u8 ... |
+// a[8] u16 @8 | b[8] u16 @24 | ca[8] i16 @40 | cb[8] i16 @56)
+struct CoopOpView {
+  uint32_t out, kind, na, nb;
+  uint16_t a[8], b[8];
+  int16_t ca[8], cb[8];
 };
 
-__device__ __forceinline__ void coop_fetch(CoopOpWords& u, const uint4* base, uint32_t step, int lane) {
-  const uint4* src = base + ((size_t)step * COOP_LANES + lane) * 5;
+__device__ __forceinline__ CoopOpView coop_decode(const CoopOpRaw& u) {
+  CoopOpView v;
+  const uint32_t w0 = op_word(u, 0), w1 = op_word(u, 1);
+  v.out = w0 & 0xffffu;
+  v.kind = (w0 >> 16) & 0xffu;
+  v.na = w0 >> 24;
+  v.nb = w1 & 0xffu;
 #pragma unroll
-  for (int k = 0; k < 5; ++k) u.w[k] = src[k];
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t wa = op_word(u, 2 + k), wb = op_word(u, 6 + k), wca = op_word(u, 10 + k), wcb = op_word(u, 14 + k);
+    v.a[2 * k] = (uint16_t)wa;
+    v.a[2 * k + 1] = (uint16_t)(wa >> 16);
+    v.b[2 * k] = (uint16_t)wb;
+    v.b[2 * k + 1] = (uint16_t)(wb >> 16);
+    v.ca[2 * k] = (int16_t)wca;
+    v.ca[2 * k + 1] = (int16_t)(wca >> 16);
+    v.cb[2 * k] = (int16_t)wcb;
+    v.cb[2 * k + 1] = (int16_t)(wcb >> 16);
+  }
+  return v;
+}
+
+// Wave-local step boundary.  A block is one wavefront: its LDS operations complete
+// in issue order, so a step needs only its reads to have landed before the writes
+// (and the compiler not to move LDS accesses across) -- no s_barrier.
+__device__ __forceinline__ void coop_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One step for this lane: gather, product, then (after the wave's gathers) write.
+template <bool TIMED>
+__device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, uint32_t* flag, uint64_t* stamp) {
+  const CoopOpView op = coop_decode(raw);
+  Fp r = fp_zero();
+  if (op.kind != 0) {
+    r = coop_lin(op.a, op.ca, op.na, slots);
+    if (op.kind == 1) r = fp_mul_lazy(r, coop_lin(op.b, op.cb, op.nb, slots));
+  }
+  if (TIMED && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+  coop_wave_sync();
+  if (op.kind != 0) {
+    if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
+      if (fp_is_zero_lazy(r)) atomicOr(flag, op.out == COOP_OUT_ZCHECK ? 1u : 1u << (op.out - COOP_OUT_ZSET));
+    } else {
+      lds_store_fp(slots, op.out, r);
+    }
+  }
+  coop_wave_sync();
 }
 
 // Run one program on this block's frame.  cbank: the constant bank staged in LDS
-// (coop_stage_consts).  *flag (LDS) is set when a zero-check op sees zero.  The
-// next step's ops are fetched while the current step computes.
+// (coop_stage_consts).  *flag (LDS) is set when a zero-check op sees zero.  Two op
+// buffers alternate: step s computes from one while step s + 1's ops load into the
+// other.
 template <bool TIMED>
 __device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
                                         uint32_t* flag, uint64_t* stamps) {
   const int lane = threadIdx.x;
-  const uint4* base = reinterpret_cast<const uint4*>(env.ops);
+  const GlobU4* base = (const GlobU4*)(const void*)env.ops;
   if (pg.n == 0) return;
   LdsU4* slots = (LdsU4*)frame;
-  // the next step's ops are in flight while a step computes
-  CoopOpWords cur, n1;
-  coop_fetch(cur, base, pg.first, lane);
-  for (uint32_t s = 0; s < pg.n; ++s) {
+  CoopOpRaw A, B;
+  const uint32_t last = pg.first + pg.n - 1;
+  coop_fetch(A, base, pg.first, lane);
+  for (uint32_t s = 0; s < pg.n; s += 2) {
+    const uint32_t g = pg.first + s;
     if (TIMED && lane == 0) stamps[2 * s] = __builtin_amdgcn_s_memtime();
-    if (s + 1 < pg.n) coop_fetch(n1, base, pg.first + s + 1, lane);
-    const CoopOp& op = cur.op;
-    Fp r = fp_zero();
-    if (op.kind != 0) {
-      r = coop_lin(op.a, op.ca, op.na, slots);
-      if (op.kind == 1) r = fp_mul_lazy(r, coop_lin(op.b, op.cb, op.nb, slots));
-    }
-    if (TIMED && lane == 0) stamps[2 * s + 1] = __builtin_amdgcn_s_memtime();
-    __syncthreads();
-    if (op.kind != 0) {
-      if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
-        if (fp_is_zero_lazy(r)) atomicOr(flag, op.out == COOP_OUT_ZCHECK ? 1u : 1u << (op.out - COOP_OUT_ZSET));
-      } else {
-        lds_store_fp(slots, op.out, r);
-      }
-    }
-    __syncthreads();
-    cur = n1;
+    coop_fetch(B, base, g + 1 <= last ? g + 1 : last, lane);
+    coop_step<TIMED>(A, slots, flag, stamps ? stamps + 2 * s + 1 : nullptr);
+    if (s + 1 >= pg.n) break;
+    if (TIMED && lane == 0) stamps[2 * s + 2] = __builtin_amdgcn_s_memtime();
+    coop_fetch(A, base, g + 2 <= last ? g + 2 : last, lane);
+    coop_step<TIMED>(B, slots, flag, stamps ? stamps + 2 * s + 3 : nullptr);
   }
   if (TIMED && lane == 0) stamps[2 * pg.n] = __builtin_amdgcn_s_memtime();
 }

@@ -48,6 +48,7 @@ struct PipeBufs {
   const uint32_t* msg_rep;     // n_sets: the set whose SSWU points set i shares
   uint32_t n_uniq;
   uint32_t scalar_base;        // set i draws r from index scalar_base + i (shards of one call, bls_gpu_partial)
+  uint32_t pack;               // sets per wavefront of k_pset (0: by call size; BLS_DEBUG_PACK)
   const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs
   const uint32_t* chunk_reqs;
   const uint32_t* indiv_reqs;  // n_indiv
@@ -59,6 +60,11 @@ struct PipeBufs {
   int32_t* sig_status;
   G1J* pk;
   int32_t* pk_status;
+  // raw-pubkey calls: lowest set index whose 96-byte key failed to decode
+  // (0xFFFFFFFF: none).  deserializeSet runs over every request of the worker
+  // message before any verification and throws on the first bad key
+  // (worker.ts:43-46), so the whole call rejects with that key's code.
+  uint32_t* first_bad_pk;
   G2A* H;
   G1J* rpk;
   G2J* rsig;
@@ -95,6 +101,15 @@ BLS_HD uint64_t set_scalar(const uint32_t seed[8], uint32_t i) {
   return r ? r : 1ull;
 }
 
+// *p = min(*p, v) (atomic on the device; the host harness runs lanes one by one)
+BLS_HD void note_min_u32(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicMin(p, v);
+#else
+  if (v < *p) *p = v;
+#endif
+}
+
 BLS_HD void stage_pk(const PipeBufs& b, uint32_t i) {
   if (i >= b.n_sets) return;
   int32_t code = BLS_OK;
@@ -114,6 +129,7 @@ BLS_HD void stage_pk(const PipeBufs& b, uint32_t i) {
     G1A a;
     code = g1_deserialize96(b.pubkeys + 96ull * i, a);
     if (code == BLS_OK) acc = jac_from_aff(a);
+    else if (b.first_bad_pk) note_min_u32(b.first_bad_pk, i);
   }
   b.pk[i] = acc;
   b.pk_status[i] = code;
@@ -261,6 +277,13 @@ BLS_HD void stage_req_status(const PipeBufs& b, uint32_t r) {
   if (r >= b.n_reqs) return;
   uint32_t beg = b.req_off[r], end = b.req_off[r + 1];
   int32_t code = BLS_OK;
+  // a raw key that does not decode rejects every request of the call (worker.ts:45
+  // throws out of verifyManySignatureSets; index.ts:367-374 rejects the whole group)
+  const uint32_t bad = b.first_bad_pk ? *b.first_bad_pk : 0xFFFFFFFFu;
+  if (bad != 0xFFFFFFFFu) {
+    b.req_status[r] = b.pk_status[bad];
+    return;
+  }
   if (beg == end) code = BLS_EMPTY_SET;
   for (uint32_t i = beg; i < end && code == BLS_OK; ++i)
     if (b.pk_status[i] != BLS_OK) code = b.pk_status[i];

@@ -205,9 +205,10 @@ __global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
 }
 
 // Sets per wavefront for a batch: 1 for small batches (latency: one wave per set
-// spreads a small call over more SIMDs), 3 from BLS_PACK_MIN_SETS sets on
-// (throughput).  $BLS_PACK (1, 2 or 3) forces a packing; $BLS_PACK_MIN overrides
-// the threshold.
+// spreads a small call over more SIMDs), 2 from BLS_PACK_MIN_SETS sets on
+// (throughput: the 2-set frame fits 20 KB of LDS, so two wavefronts share each SIMD;
+// the 3-set frame holds one).  $BLS_PACK (1, 2 or 3) forces a packing; $BLS_PACK_MIN
+// overrides the threshold.
 #define BLS_PACK_MIN_SETS 512u
 static uint32_t pack_for(uint32_t n_sets) {
   static const int forced = [] {
@@ -219,11 +220,11 @@ static uint32_t pack_for(uint32_t n_sets) {
     return e ? (uint32_t)strtoul(e, nullptr, 10) : BLS_PACK_MIN_SETS;
   }();
   if (forced >= 1 && forced <= 3) return (uint32_t)forced;
-  return n_sets >= min_sets ? 3u : 1u;
+  return n_sets >= min_sets ? 2u : 1u;
 }
 
 hipError_t launch_k_pset(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
-  const uint32_t S = pack_for(b.n_sets);
+  const uint32_t S = (b.pack >= 1 && b.pack <= 3) ? b.pack : pack_for(b.n_sets);
   if (S == 3 && env.packed[1].ml2.n > 0) {
     k_psetn<3, COOP_FRAME3><<<(b.n_sets + 2) / 3, COOP_LANES, 0, s>>>(b, env);
   } else if (S == 2 && env.packed[0].ml2.n > 0) {

@@ -77,7 +77,12 @@ def pack_requests(requests, seed: bytes | None = None) -> PackedBatch:
                 idx.extend(int(i) for i in pk)
                 idx_offs.append(len(idx))
             else:
-                raw_pks.append(bytes(pk))
+                pkb = bytes(pk)
+                if len(pkb) != 96:
+                    # the worker wire format is the 96-byte uncompressed key (index.ts:126,160);
+                    # the C-ABI reads exactly 96 bytes per set
+                    raise ValueError(f"raw pubkeys are 96 bytes (uncompressed affine), got {len(pkb)}")
+                raw_pks.append(pkb)
             if len(msg) != 32:
                 raise ValueError("signing roots are 32 bytes")
             msgs.append(bytes(msg))
@@ -224,6 +229,17 @@ class GpuContext:
         out = np.zeros(192 * max(n, 1), dtype=np.uint8)
         self._check(self.lib.bls_gpu_hash_to_g2(self._h, _ptr(m), n, _ptr(out)), "bls_gpu_hash_to_g2")
         return out[: 192 * n].reshape(n, 192)
+
+    def g2_decompress(self, sigs96: bytes | np.ndarray, validate: bool = True) -> tuple[np.ndarray, np.ndarray]:
+        """Signature.fromBytes(b, affine, validate) for n 96-byte signatures:
+        (n x 192 uncompressed bytes, n codes) (bls_gpu_g2_decompress)."""
+        s = _u8(sigs96)
+        n = s.size // 96
+        out = np.zeros(192 * max(n, 1), dtype=np.uint8)
+        codes = np.zeros(max(n, 1), dtype=np.int32)
+        self._check(self.lib.bls_gpu_g2_decompress(self._h, _ptr(s), n, 1 if validate else 0, _ptr(out), _ptr(codes)),
+                    "bls_gpu_g2_decompress")
+        return out[: 192 * n].reshape(n, 192), codes[:n]
 
     def sk_to_pk(self, sks: bytes | np.ndarray) -> np.ndarray:
         s = _u8(sks)

@@ -13,10 +13,17 @@ with GPU contexts in place of worker threads:
   signatures are waiting or 100 ms passed since the first (MAX_BUFFERED_SIGS,
   MAX_BUFFER_WAIT_MS); other jobs go straight to the queue.
 * dispatch (runJob / prepareWork, index.ts:290-400): an idle context takes queued
-  jobs up to `max_sets_per_call` signature sets (the reference's 128 by default) and
-  runs one verifyManySignatureSets call (bls_gpu_verify, worker.ts:32-108); per job a
-  verdict resolves the job's future, an error code rejects it with the blst-style
-  message ("BLST_ERROR: BLST_INVALID_SIZE", "Empty signature set", ...).
+  jobs up to `max_sets_per_call` signature sets and runs one verifyManySignatureSets
+  call (bls_gpu_verify, worker.ts:32-108); per job a verdict resolves the job's
+  future, an error code rejects it with the blst-style message ("BLST_ERROR:
+  BLST_INVALID_SIZE", "Empty signature set", ...).  The reference caps a worker
+  message at 128 sets (MAX_SIGNATURE_SETS_PER_JOB, sized for one CPU core); a GPU call
+  wants ~1024 (one call of 128 sets fills 43 of 1024 SIMDs), so the default
+  coalesces queued jobs up to GPU_SETS_PER_CALL.  Verdicts per job are unchanged:
+  the worker chunks a message by request (worker.ts:56) and re-verifies a failing
+  chunk's requests alone, so which jobs share a message changes only batchRetries.
+* metrics: `metrics.bls.aggregatedPubkeys` and the `metrics.blsThreadPool.*` series
+  under the reference's names (lodestar_amd/metrics.py, lodestar.ts:378-446).
 * `close()` (index.ts:176-197) rejects pending jobs with QUEUE_ABORTED.
 
 Sets are `SignatureSet(pubkey, signing_root, signature)` where pubkey is an int
@@ -33,9 +40,11 @@ from dataclasses import dataclass
 from typing import Sequence, Union
 
 from ._abi import ERROR_MESSAGES
+from .metrics import BlsMetrics, get_aggregated_pubkeys_count
 from .native import GpuContext, pack_requests
 
 MAX_SIGNATURE_SETS_PER_JOB = 128   # multithread/index.ts:39
+GPU_SETS_PER_CALL = 1024           # sets per bls_gpu_verify call (cfg2 shape)
 MAX_BUFFERED_SIGS = 32             # multithread/index.ts:48 (flush when >)
 MAX_BUFFER_WAIT_MS = 100           # multithread/index.ts:57
 
@@ -89,7 +98,8 @@ class GpuBlsVerifier:
     """IBlsVerifier on one GPU with `n_contexts` contexts (HIP streams) in flight."""
 
     def __init__(self, device: int = 0, n_contexts: int = 2, verify_all_multi_thread: bool = False,
-                 max_sets_per_call: int = MAX_SIGNATURE_SETS_PER_JOB, pubkeys48: bytes | None = None):
+                 max_sets_per_call: int = GPU_SETS_PER_CALL, pubkeys48: bytes | None = None,
+                 metrics: BlsMetrics | None = None):
         self.verify_all_multi_thread = verify_all_multi_thread
         self.max_sets_per_call = max_sets_per_call
         self._ctxs = [GpuContext(device) for _ in range(n_contexts)]
@@ -103,8 +113,7 @@ class GpuBlsVerifier:
         self._buffer_sigs = 0
         self._buffer_first = 0.0
         self._closed = False
-        self.metrics = {"jobs_started": 0, "sig_sets_started": 0, "batch_retries": 0, "batch_sigs_success": 0,
-                        "success_sig_sets": 0, "error_sig_sets": 0, "main_thread_calls": 0}
+        self.metrics = metrics if metrics is not None else BlsMetrics()
         self._threads = [threading.Thread(target=self._worker, args=(c,), daemon=True) for c in self._ctxs]
         self._timer = threading.Thread(target=self._buffer_timer, daemon=True)
         for t in self._threads:
@@ -113,11 +122,18 @@ class GpuBlsVerifier:
 
     # -- pubkey cache -----------------------------------------------------------
     def load_pubkeys(self, pubkeys48: bytes) -> None:
-        """Append validator pubkeys (48 B compressed) to every context's device table."""
-        for c in self._ctxs:
+        """Append validator pubkeys (48 B compressed) to every context's device table,
+        all or nothing: bls_gpu_load_pubkeys appends no key of a batch that holds an
+        undecodable one, so a failure on the first context leaves every table as it was
+        and validator indices stay aligned across contexts."""
+        codes = self._ctxs[0].load_pubkeys(pubkeys48, 48)
+        if (codes != 0).any():
+            bad = int((codes != 0).argmax())
+            raise BlsError(f"invalid pubkey at batch index {bad} (code {int(codes[bad])}); no key appended")
+        for c in self._ctxs[1:]:
             codes = c.load_pubkeys(pubkeys48, 48)
-            if (codes != 0).any():
-                raise BlsError(f"invalid pubkey at table index {int((codes != 0).argmax())}")
+            if (codes != 0).any():  # same bytes as context 0: cannot happen short of a device fault
+                raise BlsError("pubkey tables diverged across contexts")
 
     # -- IBlsVerifier --------------------------------------------------------------
     def verify_signature_sets(self, sets: Sequence[SignatureSet], batchable: bool = False,
@@ -126,14 +142,18 @@ class GpuBlsVerifier:
 
     def verify_signature_sets_async(self, sets: Sequence[SignatureSet], batchable: bool = False,
                                     verify_on_main_thread: bool = False) -> Future:
+        # pubkeys are aggregated (on the device) whichever branch runs (index.ts:136)
+        self.metrics.bls.aggregatedPubkeys.inc(get_aggregated_pubkeys_count(sets))
         if verify_on_main_thread and not self.verify_all_multi_thread:
             fut: Future = Future()
-            self.metrics["main_thread_calls"] += 1
+            stop = self.metrics.blsThreadPool.mainThreadDurationInThreadPool.start_timer()
             try:
                 with self._main_lock:
                     fut.set_result(self._run_now(list(sets)))
             except Exception as e:  # noqa: BLE001 - the contract rejects with the error
                 fut.set_exception(e)
+            finally:
+                stop()
             return fut
         jobs = [self._queue(chunk, batchable)
                 for chunk in chunkify_maximize_chunk_size(list(sets), MAX_SIGNATURE_SETS_PER_JOB)]
@@ -189,7 +209,7 @@ class GpuBlsVerifier:
             raise BlsError(ERROR_MESSAGES.get(-code, f"BLST_ERROR: {-code}"))
         return code == 1
 
-    def _call(self, ctx: GpuContext, reqs):
+    def _call(self, ctx: GpuContext, reqs, worker_id: int = 0):
         """One bls_gpu_verify; raw and table pubkeys go in separate calls."""
         def is_raw(req):
             return any(isinstance(pk, (bytes, bytearray, memoryview)) for pk, _, _ in req[1])
@@ -198,13 +218,22 @@ class GpuBlsVerifier:
             groups.setdefault(is_raw(r), []).append(k)
         verdicts = [0] * len(reqs)
         stats = None
+        tp = self.metrics.blsThreadPool
         for idx in groups.values():
-            v, stats = ctx.verify_packed(pack_requests([reqs[k] for k in idx]))
+            t0 = time.perf_counter()
+            pb = pack_requests([reqs[k] for k in idx])
+            t1 = time.perf_counter()
+            v, stats = ctx.verify_packed(pb)
+            t2 = time.perf_counter()
             for k, x in zip(idx, v):
                 verdicts[k] = int(x)
-            if stats is not None:
-                self.metrics["batch_retries"] += stats.batch_retries
-                self.metrics["batch_sigs_success"] += stats.batch_sigs_success
+            # the context is the "worker": its time is the call's device time; the
+            # latencies to / from it are the host packing and the verdict hand-back
+            tp.jobsWorkerTime.inc({"workerId": worker_id}, stats.device_ms / 1e3)
+            tp.latencyToWorker.observe(t1 - t0)
+            tp.latencyFromWorker.observe(max(0.0, (t2 - t1) - stats.device_ms / 1e3))
+            tp.batchRetries.inc(stats.batch_retries)
+            tp.batchSigsSuccess.inc(stats.batch_sigs_success)
         return verdicts, stats
 
     def _queue(self, sets: list, batchable: bool) -> _Job:
@@ -251,6 +280,13 @@ class GpuBlsVerifier:
             total += len(j.sets)
         return jobs
 
+    def queue_length(self) -> int:
+        """blsThreadPool.queueLength (index.ts:130, set on collect)."""
+        with self._cv:
+            n = len(self._jobs)
+        self.metrics.blsThreadPool.queueLength.set(n)
+        return n
+
     def _worker(self, ctx: GpuContext):
         while True:
             with self._cv:
@@ -261,18 +297,24 @@ class GpuBlsVerifier:
                 jobs = self._prepare_work()
             if not jobs:
                 continue
-            self.metrics["jobs_started"] += len(jobs)
-            self.metrics["sig_sets_started"] += sum(len(j.sets) for j in jobs)
+            tp = self.metrics.blsThreadPool
+            now = time.monotonic()
+            for j in jobs:
+                tp.jobWaitTime.observe(now - j.added)
+            tp.totalJobsGroupsStarted.inc(1)
+            tp.totalJobsStarted.inc(len(jobs))
+            tp.totalSigSetsStarted.inc(sum(len(j.sets) for j in jobs))
             try:
-                verdicts, _ = self._call(ctx, [(j.batchable, j.sets) for j in jobs])
+                verdicts, _ = self._call(ctx, [(j.batchable, j.sets) for j in jobs], self._ctxs.index(ctx))
             except Exception as e:  # noqa: BLE001 - reject every job of the call
                 for j in jobs:
                     j.future.set_exception(e)
+                tp.errorJobsSignatureSetsCount.inc(sum(len(j.sets) for j in jobs))
                 continue
             for j, code in zip(jobs, verdicts):
                 try:
                     j.future.set_result(self._verdict(code))
-                    self.metrics["success_sig_sets"] += len(j.sets)
+                    tp.successJobsSignatureSetsCount.inc(len(j.sets))
                 except BlsError as e:
                     j.future.set_exception(e)
-                    self.metrics["error_sig_sets"] += len(j.sets)
+                    tp.errorJobsSignatureSetsCount.inc(len(j.sets))

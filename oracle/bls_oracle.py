@@ -834,13 +834,35 @@ def chunkify_maximize_chunk_size(arr, min_per_chunk):
     return [list(arr[i : i + per_chunk]) for i in range(0, len(arr), per_chunk)]
 
 
+def deserialize_set(s):
+    """worker.ts:110-116 deserializeSet: PublicKey.fromBytes(96 B, affine), no validation.
+    A set whose pubkey is already a point (or None = infinity) passes through; raw bytes
+    that do not decode raise BlsError."""
+    pk, msg, sig = s
+    if isinstance(pk, (bytes, bytearray)):
+        code, pt = g1_deserialize(bytes(pk))
+        if code != E_OK:
+            raise BlsError(code)
+        pk = pt
+    return (pk, msg, sig)
+
+
 def verify_many_signature_sets(work_reqs):
     """multithread/worker.ts:32-108.  work_reqs: list of (batchable, sets).  Returns a list of
-    ("success", bool) or ("error", BlsError) per request, plus (batchRetries, batchSigsSuccess)."""
+    ("success", bool) or ("error", BlsError) per request, plus (batchRetries, batchSigsSuccess).
+
+    deserializeSet runs over every request before any verification and outside any try
+    (worker.ts:43-46): one raw pubkey that does not decode throws out of the worker call,
+    and the pool rejects every job of that message with the error (index.ts:367-374) --
+    so every request gets ("error", e) and the counters are meaningless (0, 0)."""
     results = [None] * len(work_reqs)
     batch_retries = 0
     batch_sigs_success = 0
     batchable, non_batchable = [], []
+    try:
+        work_reqs = [(b, [deserialize_set(s) for s in sets]) for b, sets in work_reqs]
+    except BlsError as e:
+        return [("error", e)] * len(results), 0, 0
     for i, (is_batchable, sets) in enumerate(work_reqs):
         (batchable if is_batchable else non_batchable).append((i, sets))
     if batchable:

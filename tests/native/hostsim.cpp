@@ -280,6 +280,8 @@ int hs_verify_batch(const bls_batch* in, int32_t* verdicts, bls_stats* stats) {
   b.sig_status = sig_status.data();
   b.pk = pk.data();
   b.pk_status = pk_status.data();
+  uint32_t first_bad_pk = 0xFFFFFFFFu;
+  if (in->pubkeys && !in->set_pk_offsets) b.first_bad_pk = &first_bad_pk;
   b.H = H.data();
   b.rpk = rpk.data();
   b.rsig = rsig.data();

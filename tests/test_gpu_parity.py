@@ -18,6 +18,8 @@ from lodestar_amd._abi import (
     CODE_EMPTY_SET,
     CODE_INVALID_SIZE,
     CODE_PK_IS_INFINITY,
+    CODE_POINT_NOT_IN_GROUP,
+    CODE_POINT_NOT_ON_CURVE,
     CODE_ZERO_SIGNATURE,
 )
 from lodestar_amd.native import pack_requests
@@ -175,10 +177,25 @@ def test_verify_raw_pubkeys(gpu, oracle, golden):
     sigs = gpu.sign(b"".join(sks), b"".join(msgs))
     raw = [oracle.g1_serialize(oracle.sk_to_pk(int.from_bytes(s, "big"))) for s in sks]
     sets = [(raw[i], msgs[i], sigs[i].tobytes()) for i in range(3)]
-    bad_pk = bytes([0x80]) + raw[0][1:]
-    reqs = [(False, sets), (True, sets[:1]), (True, sets[1:]), (False, [(bad_pk, msgs[0], sigs[0].tobytes())])]
+    reqs = [(False, sets), (True, sets[:1]), (True, sets[1:])]
     v, _ = gpu.verify_packed(pack_requests(reqs))
-    assert list(v) == [1, 1, 1, -CODE_BAD_ENCODING]
+    assert list(v) == [1, 1, 1]
+    # deserializeSet maps every request of the worker message before verifying and
+    # throws on the first undecodable key (worker.ts:43-46); the pool then rejects
+    # every job of that message (index.ts:367-374): all four requests reject.
+    bad_pk = bytes([0x80]) + raw[0][1:]          # compression flag on a 96-byte key
+    off_curve = raw[1][:48] + raw[2][48:]         # (x1, y2): not on the curve
+    for bad, code in ((bad_pk, CODE_BAD_ENCODING), (off_curve, CODE_POINT_NOT_ON_CURVE)):
+        reqs = [(False, sets), (True, sets[:1]), (True, sets[1:]), (False, [(bad, msgs[0], sigs[0].tobytes())])]
+        v, _ = gpu.verify_packed(pack_requests(reqs))
+        assert list(v) == [-code] * 4
+        want, _, _ = oracle.verify_many_signature_sets(reqs)
+        assert [-r[1].code for r in want] == list(v)
+    # two bad keys: the first in request order names the error
+    reqs = [(True, sets[:1]), (True, [(off_curve, msgs[0], sigs[0].tobytes())]),
+            (True, [(bad_pk, msgs[0], sigs[0].tobytes())])]
+    v, _ = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [-CODE_POINT_NOT_ON_CURVE] * 3
 
 
 def test_verify_batch_with_injected_invalid(gpu, oracle, table):
@@ -500,3 +517,162 @@ def test_validate_pubkeys_matches_oracle(gpu, oracle, golden):
     assert list(gpu.validate_pubkeys(b"".join(keys), 48)) == expect
     raw = [oracle.g1_serialize(oracle.g1_decompress(k)[1]) for k in keys[:26]]
     assert list(gpu.validate_pubkeys(b"".join(raw), 96)) == expect[:26]
+
+
+# ---------------------------------------------------------------------------
+# The headline call (cfg2) and the epoch shape (cfg5) at full size, with invalid sets
+# in every position that matters: chunk boundaries (chunks of 16 requests,
+# worker.ts:17,56) and every slot of a packed wavefront (1, 2 or 3 sets per
+# wavefront, kernels/k_pset.hip), through every packing, the merged check on / off
+# and the exact path.  Reference: worker.ts:54-98, multithread.test.ts:89-106.
+# ---------------------------------------------------------------------------
+def _decode_case(golden, name):
+    return bytes.fromhex(next(c["bytes"] for c in golden["sig_decode"] if c["name"] == name))
+
+
+def _expected_stats(expect, n_chunk=16):
+    """batch_retries / batch_sigs_success of the chunked worker for single-set requests
+    (a chunk with any non-1 verdict is retried)."""
+    chunks = [expect[i:i + n_chunk] for i in range(0, len(expect), n_chunk)]
+    retries = sum(1 for c in chunks if any(v != 1 for v in c))
+    ok = sum(len(c) for c in chunks if all(v == 1 for v in c))
+    return retries, ok
+
+
+def _run_all_paths(gpu, pb):
+    """(verdicts, stats) of one call through: packings 1/2/3 (merged check on), the
+    packing chosen by size with the merged check off, and the exact path."""
+    from lodestar_amd._abi import DEBUG_FORCE_EXACT, DEBUG_NO_MERGED_CHECK, DEBUG_PACK
+
+    out = {}
+    for name, flags in (("auto", 0), ("pack1", DEBUG_PACK(1)), ("pack2", DEBUG_PACK(2)), ("pack3", DEBUG_PACK(3)),
+                        ("no_merged", DEBUG_NO_MERGED_CHECK), ("exact", DEBUG_FORCE_EXACT)):
+        try:
+            gpu.set_debug_flags(flags)
+            out[name] = gpu.verify_packed(pb)
+        finally:
+            gpu.set_debug_flags(0)
+    return out
+
+
+def test_cfg2_1024_call_with_invalid_sets(gpu, oracle, golden, table):
+    """cfg2: 1024 single-set batchable requests in one call (64 chunks of 16).  Invalid
+    sets straddle chunk boundaries and sit in every wavefront slot: wrong message, wrong
+    key, a 32-byte signature, an on-curve point outside G2, the infinity signature,
+    undecodable bytes.  Every path gives the reference verdicts and worker stats."""
+    n = 1024
+    sks = _keys(oracle, 100)
+    msgs = [_h(b"cfg2-%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 100] for i in range(n)), b"".join(msgs))
+    sets = [([i % 100], msgs[i], sigs[i].tobytes()) for i in range(n)]
+    inf_sig = bytes([0xC0]) + bytes(95)
+    bad = {
+        15: ("msg", 0), 16: ("key", 0), 17: ("size", -CODE_INVALID_SIZE),            # chunk 0 / 1 boundary
+        31: ("group", -CODE_POINT_NOT_IN_GROUP), 32: ("inf", -CODE_ZERO_SIGNATURE),  # chunk 1 / 2
+        100: ("msg", 0), 101: ("msg", 0), 102: ("key", 0),                           # slots 1,2,0 of 3-packs
+        511: ("curve", -CODE_POINT_NOT_ON_CURVE), 512: ("enc", -CODE_BAD_ENCODING),  # mid-call boundary
+        700: ("inf", -CODE_ZERO_SIGNATURE), 701: ("group", -CODE_POINT_NOT_IN_GROUP),
+        1021: ("key", 0), 1022: ("size", -CODE_INVALID_SIZE), 1023: ("msg", 0),      # last chunk, last slots
+    }
+    reqs, expect = [], []
+    for i, (pk, m, sig) in enumerate(sets):
+        kind, code = bad.get(i, (None, 1))
+        if kind == "msg":
+            m = _h(b"tampered%d" % i)
+        elif kind == "key":
+            pk = [(i + 1) % 100]
+        elif kind == "size":
+            sig = sig[:32]
+        elif kind == "group":
+            sig = _decode_case(golden, "not_in_group")
+        elif kind == "curve":
+            sig = _decode_case(golden, "not_on_curve")
+        elif kind == "enc":
+            sig = _decode_case(golden, "x_ge_p")
+        elif kind == "inf":
+            sig = inf_sig
+        reqs.append((True, [(pk, m, sig)]))
+        expect.append(code)
+    pb = pack_requests(reqs)
+    retries, ok = _expected_stats(expect)
+    res = _run_all_paths(gpu, pb)
+    for name, (v, st) in res.items():
+        assert list(v) == expect, name
+        assert (st.n_chunks, st.batch_retries, st.batch_sigs_success) == (64, retries, ok), name
+    assert res["auto"][1].merged_check == 2 and res["no_merged"][1].merged_check == 0
+    # every set that decodes goes through the exact path (the 4 decode failures never reach it)
+    assert res["exact"][1].n_flagged == n - 4
+    # the same call all-valid: the merged check passes on every packing
+    good = pack_requests([(True, [s]) for s in sets])
+    for name, (v, st) in _run_all_paths(gpu, good).items():
+        assert list(v) == [1] * n, name
+        assert st.batch_retries == 0 and st.batch_sigs_success == n, name
+        assert st.merged_check == (0 if name == "no_merged" else 1), name
+
+
+def test_cfg5_shape_two_roots_with_invalid(gpu, oracle, table):
+    """cfg5 shape: 1024 attestations of two committees sharing two signing
+    roots, with invalid sets (a signature over the other root, a wrong key, an
+    undecodable signature) in both committees; verdicts equal with root dedup on / off,
+    every packing and the exact path."""
+    from lodestar_amd._abi import DEBUG_NO_MSG_DEDUP
+
+    n = 1024
+    roots = [_h(b"epoch-root-a"), _h(b"epoch-root-b")]
+    sks = _keys(oracle, 100)
+    msgs = [roots[i * 2 // n] for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 100] for i in range(n)), b"".join(msgs))
+    reqs, expect = [], []
+    for i in range(n):
+        pk, sig, code = [i % 100], sigs[i].tobytes(), 1
+        if i in (3, 600):            # signature over the other committee's root
+            sig, code = sigs[n - 1 - i].tobytes(), 0
+        if i in (257, 1000):         # another validator's key
+            pk, code = [(i + 7) % 100], 0
+        if i == 513:                 # undecodable
+            sig, code = bytes(96), -CODE_BAD_ENCODING
+        reqs.append((True, [(pk, msgs[i], sig)]))
+        expect.append(code)
+    pb = pack_requests(reqs)
+    res = _run_all_paths(gpu, pb)
+    try:
+        gpu.set_debug_flags(DEBUG_NO_MSG_DEDUP)
+        res["no_dedup"] = gpu.verify_packed(pb)
+    finally:
+        gpu.set_debug_flags(0)
+    retries, ok = _expected_stats(expect)
+    for name, (v, st) in res.items():
+        assert list(v) == expect, name
+        assert (st.batch_retries, st.batch_sigs_success) == (retries, ok), name
+    assert res["auto"][1].n_unique_msgs == 2 and res["no_dedup"][1].n_unique_msgs == n
+
+
+def test_kat3_mainnet_points_gpu_decode(gpu, golden, oracle, table):
+    """KAT-3: the real mainnet G2 points of backfill/blocks.json through the GPU decoder:
+    bit-exact uncompressed coordinates and G2 membership (bls_gpu_g2_decompress), then
+    through the verify path's own decode + psi subgroup test (k_pre + k_pset, every
+    packing): a decodable in-group point that is not this set's signature gives false,
+    never an error code."""
+    pts = golden["kat3_g2_points"]
+    comp = b"".join(bytes.fromhex(p["compressed"]) for p in pts)
+    out, codes = gpu.g2_decompress(comp, validate=True)
+    assert list(codes) == [0] * len(pts)
+    assert [o.tobytes().hex() for o in out] == [p["uncompressed"] for p in pts]
+    # the oracle-derived negatives through the same entry point
+    cases = golden["sig_decode"]
+    _, codes = gpu.g2_decompress(b"".join(bytes.fromhex(c["bytes"]) for c in cases), validate=True)
+    assert list(codes) == [c["code"] for c in cases]
+    # verify path: 1-set requests, and one large batchable call so the packed kernels run
+    sks = _keys(oracle, 1)
+    m = _h(b"kat3")
+    reqs = [(False, [([0], m, bytes.fromhex(p["compressed"]))]) for p in pts]
+    v, _ = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == [0] * len(pts)
+    sig = gpu.sign(sks[0], m)[0].tobytes()
+    big = [(True, [([0], m, sig)])] * 600
+    for k, p in enumerate(pts):
+        big[37 * k + 5] = (True, [([0], m, bytes.fromhex(p["compressed"]))])
+    pb = pack_requests(big)
+    want = [0 if (i - 5) % 37 == 0 and (i - 5) // 37 < len(pts) else 1 for i in range(600)]
+    for name, (v, _) in _run_all_paths(gpu, pb).items():
+        assert list(v) == want, name

@@ -188,6 +188,28 @@ def test_pipeline_semantics(hostsim, oracle):
     assert st.batch_retries == 1 and st.n_individual == n + 2
 
 
+def test_deserialize_set_rejects_whole_call(hostsim, oracle):
+    """worker.ts:43-46: deserializeSet maps every request of a worker message before any
+    verification, outside the try; one raw key that does not decode throws, and the pool
+    rejects every job of the message (index.ts:367-374).  The kernels' stage bodies and
+    the oracle agree on that (the first bad key in request order names the error)."""
+    sk = oracle.interop_secret_key(0)
+    pk = oracle.g1_serialize(oracle.sk_to_pk(sk))
+    msg = hashlib.sha256(b"deser").digest()
+    sig = oracle.g2_compress(oracle.sign(sk, msg))
+    good = (pk, msg, sig)
+    flag_bit = bytes([0x80]) + pk[1:]                         # compressed flag on a 96-byte key
+    off_curve = pk[:48] + (int.from_bytes(pk[48:], "big") ^ 1).to_bytes(48, "big")
+    for reqs, code in (
+        ([(True, [good]), (False, [good, (flag_bit, msg, sig)]), (False, [])], oracle.E_BAD_ENCODING),
+        ([(True, [(off_curve, msg, sig)]), (True, [(flag_bit, msg, sig)])], oracle.E_POINT_NOT_ON_CURVE),
+    ):
+        v, _ = _hs_verify(hostsim, reqs)
+        assert v == [-code] * len(reqs)
+        want, retries, ok = oracle.verify_many_signature_sets(reqs)
+        assert [-r[1].code for r in want] == v and (retries, ok) == (0, 0)
+
+
 def test_signing_root_dedup_pre_stage(hostsim):
     """plan_msg_dedup + stage_pre over distinct roots + stage_qdup give every set the
     SSWU points of the per-set pre-stage (committee-shared roots)."""

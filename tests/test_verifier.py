@@ -88,8 +88,30 @@ def test_large_call_split_into_jobs(verifier, oracle):
     msgs = [hashlib.sha256(b"big%d" % i).digest() for i in range(n)]
     sigs = verifier._main.sign(sks, b"".join(msgs))
     sets = [SignatureSet(i % 100, msgs[i], sigs[i].tobytes()) for i in range(n)]
-    started = verifier.metrics["jobs_started"]
+    tp = verifier.metrics.blsThreadPool
+    started, sigs = tp.totalJobsStarted.get(), tp.totalSigSetsStarted.get()
     assert verifier.verify_signature_sets(sets, batchable=True) is True
-    assert verifier.metrics["jobs_started"] - started == 2
+    assert tp.totalJobsStarted.get() - started == 2
+    assert tp.totalSigSetsStarted.get() - sigs == n
     sets[150] = SignatureSet(sets[150].pubkey, msgs[0], sets[150].signature)
     assert verifier.verify_signature_sets(sets) is False
+
+
+@pytest.mark.gpu
+def test_metrics_reference_series(verifier, sets3):
+    """metrics.bls.aggregatedPubkeys counts the keys of aggregate sets (index.ts:136,
+    utils.ts:18-26) on both branches; the pool series move as index.ts:317-366 moves them."""
+    m = verifier.metrics
+    agg0 = m.bls.aggregatedPubkeys.get()
+    ok0 = m.blsThreadPool.successJobsSignatureSetsCount.get()
+    agg_set = SignatureSet([0, 1], sets3[0].signing_root, sets3[0].signature)
+    assert verifier.verify_signature_sets([agg_set] + sets3) is False
+    assert verifier.verify_signature_sets([agg_set], verify_on_main_thread=True) is False
+    assert m.bls.aggregatedPubkeys.get() - agg0 == 4
+    assert m.blsThreadPool.successJobsSignatureSetsCount.get() - ok0 == 4
+    assert m.blsThreadPool.mainThreadDurationInThreadPool.count() >= 1
+    assert m.blsThreadPool.jobWaitTime.count() >= 1
+    assert verifier.queue_length() == 0
+    text = m.expose()
+    assert "lodestar_bls_aggregated_pubkeys_total" in text
+    assert 'lodestar_bls_thread_pool_time_seconds_sum{workerId="' in text
