@@ -29,7 +29,7 @@ from circuits import (  # noqa: E402
 
 X_ABS = 0xD201000000010000
 FRAME = 256
-FRAME2 = 512   # frame of the 2-set programs (kernels/k_pset.hip, CoopLdsN<COOP_FRAME2>)
+FRAME2 = 380   # frame of the 2-set programs (kernels/k_pset.hip, CoopLdsN<COOP_FRAME2>; 2 waves/SIMD)
 FRAME3 = 640   # frame of the 3-set programs (CoopLdsN<COOP_FRAME3>)
 MONT_R = 1 << 384
 
@@ -460,7 +460,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                 steps_bin += struct.pack("<HBBB3x8H8H8h8h8x", out, kind, len(a), len(b),
                                          *refs(a), *refs(b), *cfs(a), *cfs(b))
         first += len(pg.steps)
-    assert len(consts.vals) <= 64, "constant bank exceeds COOP_MAX_CONSTS"
+    assert len(consts.vals) <= 40, "constant bank exceeds COOP_MAX_CONSTS"
     header = struct.pack("<4sIIII", b"BLSC", 1, len(consts.vals), len(progs), first)
     cbin = b"".join(_le_limbs(v * MONT_R % P) for v in consts.vals)
     path.write_bytes(header + cbin + bytes(table) + bytes(steps_bin))
