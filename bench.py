@@ -2,23 +2,36 @@
 """Benchmark of the MI355X BLS signature-set verifier (BASELINE.json metric:
 "BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch").
 
-Workload per step (BASELINE.json configs[1], cfg2): one verifyManySignatureSets call of
-1024 gossip-attestation sets, each its own batchable single-pubkey request (as
+Workload (BASELINE.json configs[1], cfg2): verifyManySignatureSets calls of 1024
+gossip-attestation sets, each its own batchable single-pubkey request (as
 multithread/index.ts:260-275 buffers them), pubkeys resident in the device table
 (index2pubkey, pubkeyCache.ts:56-77), random-scalar batch verification in chunks of
-16 requests (worker.ts:17,56) -- every stage (decompress + subgroup check,
-hash_to_G2, scalar muls, Miller loops, final exponentiations) runs inside the timed
-step.  Inputs are synthetic: interop keys sk_i = LE(sha256(LE32(i))) mod r
+16 requests (worker.ts:17,56); every stage (decompress + subgroup check, hash_to_G2,
+scalar muls, Miller loops, final exponentiations) runs inside the timed region.
+Inputs are synthetic: interop keys sk_i = LE(sha256(LE32(i))) mod r
 (state-transition/src/util/interop.ts:19-22), messages sha256(LE64(j) || "LODE"),
 signatures made on the GPU before timing.
 
-Multi-GPU (torchrun, one process per GPU): each rank verifies its own 1024 sets (shard
-by request, no data-path collective: scaling "weak"); value = all ranks' sets / max
-over ranks of the timed region.
+A step is one call on each of the `--inflight` verifier contexts (one HIP stream
+each), i.e. inflight x 1024 sets: the contexts start together (a barrier) and each
+runs exactly `--steps` calls back to back, as the reference's worker pool keeps one
+message per worker in flight (multithread/index.ts:199-233).  value = all sets / the
+timed region, so it is steady-state whatever --steps is.
+
+Multi-GPU (torchrun, one process per GPU):
+  --mode cfg2 (default): each rank verifies its own calls (shard by request, no
+      data-path collective; scaling "weak"); value = all ranks' sets / max rank time.
+  --mode sharded: cfg4/cfg5 shape -- ONE call of (sets x world) sets split across
+      the ranks (lodestar_amd.shard.verify_call_sharded): per rank an Fp12 partial of
+      its shard, an all-gather of 588-byte records over RCCL/xGMI, one final
+      exponentiation; a step is one such call.
+  --mode napi: the same cfg2 workload driven through the N-API addon and the JS
+      GpuBlsVerifier (integration/js), one verifySignatureSets([set], {batchable})
+      per set, as gossip validation calls it (N = 1 only).
 
 Also reported: p50 latency of one non-batchable 128-set call (cfg1 shape), the
 roofline of the dominant kernel against the measured v_mad_u64_u32 peak, and the CPU
-baseline (the oracle, rank 0, N = 1 only, bounded sample).
+baseline (the C++ restatement under oracle/cpu on the host cores, rank 0, N = 1).
 """
 from __future__ import annotations
 
@@ -26,8 +39,12 @@ import argparse
 import hashlib
 import json
 import os
+import platform
+import shutil
 import statistics
+import subprocess
 import sys
+import tempfile
 import threading
 import time
 from pathlib import Path
@@ -38,10 +55,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 # One HIP stream per in-flight batch; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
 # queues (default 4 on this image), and streams sharing a queue serialise.  Give the
-# in-flight contexts their own queues (set before the HIP runtime initialises; the
-# box exports 4, so raise it rather than default it).
-# 16 batches over 24 queues measured best (tools/gpu_inflight_q.sh: 12/16 384k,
-# 16/24 403k, 20/24 382k sets/s).
+# in-flight contexts their own queues (set before the HIP runtime initialises).
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
     os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
@@ -49,32 +63,51 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 STAGE_NAMES = ["h2d", "k_pk", "k_pre", "k_pset", "k_exact", "-", "k_status+k_chunk", "k_indiv"]
 X_ABS = 0xD201000000010000
 MADS_PER_FPM = 288   # 12x12 limb products + 12x12 reduction products per Montgomery product
+METRIC = "BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch"
 
 
-def pset_products_per_set() -> float:
-    """Expected Fp products k_pset executes per set (program MUL ops from
-    lodestar_amd/_native/coop_programs.json; r's bits are uniform)."""
+def pack_of(n_sets: int) -> int:
+    """Sets per wavefront k_pset runs for a call of n_sets (kernels/k_pset.hip pack_for)."""
+    forced = int(os.environ.get("BLS_PACK", "0") or 0)
+    if forced in (1, 2, 3):
+        return forced
+    return 2 if n_sets >= int(os.environ.get("BLS_PACK_MIN", "512")) else 1
+
+
+def pset_products_per_set(S: int) -> float:
+    """Expected Fp products the per-set kernel executes per set with S sets per
+    wavefront (program MUL ops from lodestar_amd/_native/coop_programs.json; r's bits
+    uniform, so each of the 2^S r-masks of an addition step is equally likely)."""
     pg = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
     m = {k: v["mul_ops"] for k, v in pg.items()}
-    n = m["pset_prep"] + m["pset_dbl_r"] + 0.5 * m["pset_add_r"] + 63 * m["pset_dbl_all"]
+    if S == 1:
+        n = m["pset_prep"] + m["pset_dbl_r"] + 0.5 * m["pset_add_r"] + 63 * m["pset_dbl_all"]
+        for i in range(62, -1, -1):
+            n += (0.5 * m["pset_add_xr"] + 0.5 * m["pset_add_x"]) if (X_ABS >> i) & 1 else 0.5 * m["pset_add_r"]
+        return n + m["pset_phase2"] + m["pset_norm2"] + m["pset_affine2"] + m["pset_ml2"]
+    p = f"pset{S}_"
+
+    def add(xb):
+        progs = [f"{p}add_{xb}{r:0{S}b}" for r in range(1 << S) if xb or r]
+        return sum(m[q] for q in progs) / (1 << S)
+
+    n = m[p + "prep"] + m[p + "dbl_r"] + add(0) + 63 * m[p + "dbl_all"]
     for i in range(62, -1, -1):
-        if (X_ABS >> i) & 1:
-            n += 0.5 * m["pset_add_xr"] + 0.5 * m["pset_add_x"]
-        else:
-            n += 0.5 * m["pset_add_r"]
-    return n + m["pset_phase2"] + m["pset_norm2"] + m["pset_affine2"] + m["pset_ml2"]
+        n += add((X_ABS >> i) & 1)
+    n += m[p + "phase2"] + m[p + "norm2"] + m[p + "affine2"] + m[p + "ml2"]
+    return n / S
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3
-    FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
-    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"), key=lambda p: p.name)
+def pmc_summary(kernel_prefix: str):
+    """The newest committed SQ-counter summary for the kernel (profiles/r*_pmc_*.json,
+    rocprofv3 --pmc passes; tools/pmc_summary.py), or None."""
+    files = sorted((ROOT / "profiles").glob("r*_pmc_k_pset*.json"), key=lambda p: p.name)
     for p in reversed(files):
         d = json.loads(p.read_text())
-        if kernel in d:
-            return int(d[kernel]["hbm_bytes_per_launch"]), p.name
-    return None, None
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(kernel_prefix):
+                return {**v, "source": p.name}
+    return None
 
 
 def interop_sk(i: int) -> bytes:
@@ -84,7 +117,9 @@ def interop_sk(i: int) -> bytes:
 
 def make_workload(gpu, n_sets: int, rank: int, roots: int = 0):
     """cfg2: every set signs its own root.  roots > 0: the cfg5 mainnet-epoch shape
-    (SURVEY §8d), consecutive sets in committees sharing `roots` signing roots per call."""
+    (SURVEY §8d), consecutive sets in committees sharing `roots` signing roots per call.
+    Returns (batch, call128, sets, raw96): the packed cfg2 call, a 128-set non-batchable
+    call (cfg1 shape), the sets (table indices), the 96-byte uncompressed keys."""
     from lodestar_amd.native import pack_requests
 
     n_keys = n_sets
@@ -97,53 +132,151 @@ def make_workload(gpu, n_sets: int, rank: int, roots: int = 0):
         msgs = [msgs[(j * roots // n_sets) * (n_sets // roots)] for j in range(n_sets)]
     sigs = gpu.sign(b"".join(interop_sk(j % n_keys) for j in range(n_sets)), b"".join(msgs))
     sets = [([j % n_keys], msgs[j], sigs[j].tobytes()) for j in range(n_sets)]
+    raw96, _ = gpu.aggregate_pubkeys([[j % n_keys] for j in range(n_sets)])
     batch = pack_requests([(True, [s]) for s in sets])
     call128 = pack_requests([(False, sets[:128])])
-    return batch, call128, sets
+    return batch, call128, sets, raw96
 
 
-def _oracle_batch(args) -> float:
-    """One worker of the CPU baseline: build `n` sets with the oracle, then time
-    verifySignatureSetsMaybeBatch over them (seconds)."""
-    from oracle import bls_oracle as O
+# ---------------------------------------------------------------------------
+# CPU baseline: the C++ restatement under oracle/cpu ("not blst"), host cores
+# ---------------------------------------------------------------------------
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
 
-    n, base = args
-    sks = [int.from_bytes(interop_sk(base + i), "big") for i in range(n)]
-    msgs = [hashlib.sha256((base + j).to_bytes(8, "little") + b"LODE").digest() for j in range(n)]
-    sigs = [O.g2_compress(O.sign(s, m)) for s, m in zip(sks, msgs)]
-    pks = [O.sk_to_pk(s) for s in sks]
+
+def cpu_baseline(sets, raw96, threads: int = 16, seconds: float = 10.0, latency_runs: int = 20) -> dict:
+    """The reference's CPU path restated in C++ (oracle/cpu/bls_cpu.cpp): a worker pool
+    of `threads` OS threads, each running verifyManySignatureSets on messages of 128
+    single-set batchable requests (the pool's MAX_SIGNATURE_SETS_PER_JOB = 128,
+    index.ts:39; chunks of 16 requests, worker.ts:17,56) back to back for `seconds`
+    -> cfg2 sets/s; and cfg1: one message holding one non-batchable request of 128
+    sets on one core, `latency_runs` runs -> p50 / p99 ms."""
+    import ctypes
+
+    from lodestar_amd._abi import BlsBatch
+    from lodestar_amd.native import _ptr, pack_requests
+
+    lib = ctypes.CDLL(str(ROOT / "oracle" / "cpu" / "libbls_cpu.so"))
+    lib.cpu_pool_throughput.argtypes = [ctypes.POINTER(BlsBatch), ctypes.c_int, ctypes.c_double,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
+    lib.cpu_message_latency.argtypes = [ctypes.POINTER(BlsBatch), ctypes.c_int, ctypes.c_void_p]
+    raw_sets = [(raw96[i], m, s) for i, (_, m, s) in enumerate(sets[:128])]
+
+    def batch_of(pb):
+        b = BlsBatch()
+        b.n_sets, b.n_reqs = pb.n_sets, pb.n_reqs
+        keep = []
+        for f in ("req_set_offsets", "req_batchable", "messages", "signatures", "pubkeys", "set_pk_offsets",
+                  "pk_indices", "signature_lens"):
+            a = getattr(pb, f)
+            keep.append(a)
+            setattr(b, f, _ptr(a))
+        return b, keep
+
+    job, k1 = batch_of(pack_requests([(True, [s]) for s in raw_sets]))
+    rate, msgs = ctypes.c_double(), ctypes.c_uint32()
+    rc = lib.cpu_pool_throughput(ctypes.byref(job), threads, seconds, ctypes.byref(rate), ctypes.byref(msgs))
+    assert rc == 0, "CPU baseline verification failed"
+    call, k2 = batch_of(pack_requests([(False, raw_sets)]))
+    ms = np.zeros(latency_runs, dtype=np.float64)
+    assert lib.cpu_message_latency(ctypes.byref(call), latency_runs, _ptr(ms)) == 0
+    return {"value": round(rate.value, 1), "unit": "sets/s", "cores": threads, "kind": "port",
+            "impl": "C++ restatement of the reference worker pool, not blst (oracle/cpu/bls_cpu.cpp: 6x64-bit "
+                    "Montgomery words, shared-squaring Miller loops, sum of r_i sig_i, one final exp per chunk)",
+            "cpu": _cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"cfg2: {threads} worker threads x messages of 128 batchable single-set requests for "
+                      f"{seconds:.0f} s ({msgs.value} messages); cfg1: one 128-set non-batchable request on one "
+                      f"core x {latency_runs}",
+            "cfg1_p50_ms_128": round(float(np.percentile(ms, 50)), 2),
+            "cfg1_p99_ms_128": round(float(np.percentile(ms, 99)), 2)}
+
+
+# ---------------------------------------------------------------------------
+# modes
+# ---------------------------------------------------------------------------
+def timed_calls(ctxs, batches, steps: int):
+    """Every context runs `steps` calls of its batch back to back, all starting at one
+    barrier; returns (elapsed s, mean stage_ms, all verdicts valid)."""
+    n = len(ctxs)
+    start = threading.Barrier(n + 1)
+    stage_sum = np.zeros(8)
+    ok = [True]
+    lock = threading.Lock()
+
+    def worker(i):
+        start.wait()
+        acc = np.zeros(8)
+        good = True
+        for _ in range(steps):
+            v, st = ctxs[i].verify_packed(batches[i])
+            good = good and bool((v == 1).all())
+            acc += np.array(st.stage_ms[:])
+        with lock:
+            stage_sum[:] += acc
+            ok[0] = ok[0] and good
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    start.wait()
     t0 = time.perf_counter()
-    ok = O.verify_signature_sets_maybe_batch(list(zip(pks, msgs, sigs)))
-    dt = time.perf_counter() - t0
-    assert ok
-    return dt
+    for t in th:
+        t.join()
+    return time.perf_counter() - t0, stage_sum / max(1, steps * n), ok[0]
 
 
-def cpu_baseline(sample_sets: int = 16, procs: int = 16) -> dict:
-    """Oracle (pure-Python restatement, oracle/bls_oracle.py) timed on the host:
-    `procs` processes (the box's CPU share is 16 cores), each verifying its own
-    random-scalar batch of `sample_sets` sets; value = all sets / the slowest worker's
-    verification time (input construction is outside the timed part)."""
-    import multiprocessing as mp
+def run_sharded(be, sets, seed, steps, warmup, dist, device):
+    """--mode sharded: `steps` calls, each ONE call of every rank's sets (world x sets),
+    verified as one random-scalar batch through verify_call_sharded with the partial
+    backend `be` (GpuPartialBackend on the GPU box).  Returns (elapsed s, sets per call)."""
+    from lodestar_amd.shard import verify_call_sharded
 
-    procs = max(1, min(procs, os.cpu_count() or 1))
-    with mp.get_context("spawn").Pool(procs) as pool:
-        times = pool.map(_oracle_batch, [(sample_sets, 1000 * k) for k in range(procs)])
-    total = sample_sets * procs
-    return {"value": round(total / max(times), 3), "unit": "sets/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x {sample_sets} single-pubkey sets, one random-scalar batch each "
-                      f"(verifySignatureSetsMaybeBatch), slowest {max(times):.1f} s, pure-Python oracle"}
+    for _ in range(warmup):
+        ok, _ = verify_call_sharded(sets, seed, be, dist, device, localize=False)
+        assert ok is True, "sharded warm-up call failed"
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ok, _ = verify_call_sharded(sets, seed, be, dist, device, localize=False)
+        assert ok is True, "sharded call failed inside the timed region"
+    if dist is not None:
+        dist.barrier()
+    return time.perf_counter() - t0, len(sets)
+
+
+def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int) -> dict:
+    """--mode napi: integration/js/benchNapi.js in a child Node process (the GPU is not
+    touched by this process meanwhile)."""
+    node = shutil.which("node")
+    if node is None:
+        raise SystemExit("--mode napi needs node")
+    env = dict(os.environ, UV_THREADPOOL_SIZE=str(max(4, inflight + 2)))
+    out = subprocess.run([node, str(ROOT / "integration" / "js" / "benchNapi.js"), str(work_file), str(steps),
+                          str(inflight), str(n_sets)], capture_output=True, text=True, env=env, timeout=1200)
+    if out.returncode != 0:
+        raise SystemExit(f"benchNapi.js failed: {out.stderr[-2000:]}")
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=1024)
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=16, help="batches in flight per GPU (contexts/streams)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--inflight", type=int, default=16, help="calls in flight per GPU (contexts / HIP streams)")
+    ap.add_argument("--mode", choices=("cfg2", "sharded", "napi"), default="cfg2")
     ap.add_argument("--roots", type=int, default=0,
                     help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
     ap.add_argument("--no-dedup", action="store_true", help="hash every set's root (BLS_DEBUG_NO_MSG_DEDUP)")
@@ -154,12 +287,13 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    dist, device = None, None
     if world > 1:
         import torch
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)
+        device = f"cuda:{local_rank}"
         dist.init_process_group("nccl")
 
     def barrier_sync():
@@ -169,121 +303,145 @@ def main() -> None:
             dist.barrier()
             torch.cuda.synchronize()
 
-    from lodestar_amd.native import GpuContext
-
-    # `inflight` verifier contexts (one HIP stream each) fed by one host thread each:
-    # batches overlap on the GPU the way the reference's worker pool keeps several
-    # verifyManySignatureSets jobs in flight (multithread/index.ts:199-233).
-    ctxs = [GpuContext(local_rank) for _ in range(args.inflight)]
-    gpu = ctxs[0]
-    works = [make_workload(c, args.sets, rank, args.roots) for c in ctxs]
     from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK, DEBUG_NO_MSG_DEDUP
-
-    flags = (DEBUG_NO_MSG_DEDUP if args.no_dedup else 0) | (DEBUG_NO_MERGED_CHECK if args.no_merged_check else 0)
-    for c in ctxs:
-        c.set_debug_flags(flags)
-    batch, call128, _ = works[0]
-
-    for c, w in zip(ctxs, works):
-        for _ in range(args.warmup):
-            v, _ = c.verify_packed(w[0])
-            assert (v == 1).all(), "warm-up verification failed"
-
-    stage_sum = np.zeros(8)
-    stage_n = [0]
-    failures = []
-    lock = threading.Lock()
-    share = [args.steps // args.inflight + (1 if i < args.steps % args.inflight else 0) for i in range(args.inflight)]
-
-    def worker(i):
-        for _ in range(share[i]):
-            v, st = ctxs[i].verify_packed(works[i][0])
-            if not (v == 1).all():
-                failures.append(i)
-            with lock:
-                stage_sum[:] += np.array(st.stage_ms[:])
-                stage_n[0] += 1
-
-    threads = [threading.Thread(target=worker, args=(i,)) for i in range(args.inflight)]
-    barrier_sync()
-    t0 = time.perf_counter()
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if failures:
-        raise SystemExit("verification failed inside the timed region")
+    from lodestar_amd.native import GpuContext
     from lodestar_amd.shard import global_throughput
 
-    value, elapsed = global_throughput(args.sets * args.steps, elapsed, dist, device=f"cuda:{local_rank}")
+    flags = (DEBUG_NO_MSG_DEDUP if args.no_dedup else 0) | (DEBUG_NO_MERGED_CHECK if args.no_merged_check else 0)
+    inflight = args.inflight if args.mode == "cfg2" else 1
+    ctxs = [GpuContext(local_rank) for _ in range(inflight)]
+    gpu = ctxs[0]
+    works = [make_workload(c, args.sets, rank, args.roots) for c in ctxs]
+    for c in ctxs:
+        c.set_debug_flags(flags)
+    batch, call128, sets, raw96 = works[0]
+    S = pack_of(args.sets)
+    extra = {}
 
-    # p50 latency of one 128-set non-batchable call (cfg1 shape)
-    lat = []
-    for _ in range(args.latency_runs):
-        t1 = time.perf_counter()
-        v, _ = gpu.verify_packed(call128)
-        lat.append((time.perf_counter() - t1) * 1e3)
-        assert v[0] == 1
+    if args.mode == "cfg2":
+        for c, w in zip(ctxs, works):
+            for _ in range(args.warmup):
+                v, _ = c.verify_packed(w[0])
+                assert (v == 1).all(), "warm-up verification failed"
+        barrier_sync()
+        elapsed, stage_ms, ok = timed_calls(ctxs, [w[0] for w in works], args.steps)
+        barrier_sync()
+        if not ok:
+            raise SystemExit("verification failed inside the timed region")
+        local_sets = args.sets * args.steps * inflight
+        value, elapsed = global_throughput(local_sets, elapsed, dist, device=device)
+        workload = ("cfg2: 1024 single-pubkey gossip sets per call, batchable requests, random-scalar batch in "
+                    "chunks of 16 requests" if args.roots == 0 else
+                    f"cfg5 shape: {args.sets} single-pubkey sets per call over {args.roots} committee-shared signing "
+                    "roots, batchable requests" + (", root dedup off" if args.no_dedup else ""))
+        workload += ", merged check off" if args.no_merged_check else ""
+        config = {"workload": workload, "sets_per_call": args.sets, "calls_in_flight_per_gpu": inflight,
+                  "sets_per_step_per_gpu": args.sets * inflight, "parallelism": f"shard-by-request x{world}"}
+        scaling = "weak"
+    elif args.mode == "sharded":
+        # the call: every rank's sets (each rank made its own keys/messages; the call's
+        # pubkeys travel raw, as the worker wire format, index.ts:160)
+        mine = [(raw96[i], m, s) for i, (_, m, s) in enumerate(sets)]
+        all_sets = mine
+        if dist is not None:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, mine)
+            all_sets = [s for part in gathered for s in part]
+        seed = hashlib.sha256(b"sharded-bench").digest()
+        from lodestar_amd.shard import GpuPartialBackend
 
-    # roofline of the dominant kernel, k_pset (VALU integer multiply-add bound).
-    # stage_ms: per batch while batches overlap (a launch waits for CUs the other
-    # streams hold); the roofline uses the kernel's solo launch time: the same batch
-    # on one stream with the device otherwise idle (HIP events on that stream).
-    stage_ms = stage_sum / max(stage_n[0], 1)
-    dom = "k_pset"
-    solo = []
-    for _ in range(5):
-        _, st = gpu.verify_packed(batch)
-        solo.append(st.stage_ms[STAGE_NAMES.index(dom)])
-    dom_ms = statistics.median(solo)
-    shared_ms = stage_ms[STAGE_NAMES.index(dom)]
-    fpm_set = pset_products_per_set()
-    mads = fpm_set * MADS_PER_FPM * args.sets
-    achieved = mads / (dom_ms * 1e-3) / 1e12
-    peak_rate, _ = gpu.mad_peak()
-    traffic, traffic_src = pmc_traffic("k_psetn" if args.sets >= 512 else "k_pset")
-    peak = peak_rate / 1e12
+        elapsed_local, total = run_sharded(GpuPartialBackend(gpu), all_sets, seed, args.steps, args.warmup, dist,
+                                           device)
+        value, elapsed = global_throughput(total * args.steps / world, elapsed_local, dist, device=device)
+        stage_ms = np.zeros(8)
+        config = {"workload": f"cfg4/cfg5 sharded call: one call of {total} single-pubkey sets split over {world} "
+                              "GPU(s); per-rank Fp12 Miller-loop partial, all-gather of 588-byte records, one final "
+                              "exponentiation", "sets_per_call": total, "sets_per_step_per_gpu": args.sets,
+                  "parallelism": f"sharded-call x{world}"}
+        scaling = "weak"
+    else:  # napi
+        if world > 1:
+            raise SystemExit("--mode napi runs on one GPU")
+        with tempfile.TemporaryDirectory() as td:
+            wf = Path(td) / "work.json"
+            pks48 = gpu.sk_to_pk(b"".join(interop_sk(i) for i in range(args.sets))).tobytes()
+            wf.write_text(json.dumps({"pubkeys48": pks48.hex(),
+                                      "sets": [{"idx": pk[0], "msg": m.hex(), "sig": s.hex()} for pk, m, s in sets]}))
+            # the ctypes number on the same box, for the within-20% check
+            for c, w in zip(ctxs, works):
+                c.verify_packed(w[0])
+            for c in ctxs:
+                c.close()
+            ctxs = []
+            res = run_napi(wf, args.steps, args.inflight, args.sets)
+        value, elapsed = res["sets_per_s"], res["elapsed_s"]
+        stage_ms = np.zeros(8)
+        extra["napi"] = res
+        config = {"workload": "cfg2 through the N-API addon + JS GpuBlsVerifier: one verifySignatureSets([set], "
+                              "{batchable: true}) per set, buffered and coalesced into GPU calls",
+                  "sets_per_step_per_gpu": args.sets * args.inflight, "contexts": args.inflight,
+                  "parallelism": "napi x1"}
+        scaling = "weak"
 
+    out = None
     if rank == 0:
-        out = {
-            "metric": "BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch",
-            "value": round(value, 2),
-            "unit": "sets/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32 (381-bit Fp, 12x32-bit Montgomery limbs)",
-            "data": "synthetic: interop keys, sha256 messages, GPU-made signatures",
-            "config": {"workload": ("cfg2: 1024 single-pubkey gossip sets per GPU, batchable requests, "
-                                    "random-scalar batch in chunks of 16 requests") if args.roots == 0 else
-                                   (f"cfg5 shape: {args.sets} single-pubkey sets per call over {args.roots} "
-                                    f"committee-shared signing roots, batchable requests"
-                                    + (", root dedup off" if args.no_dedup else ""))
-                                   + (", merged check off" if args.no_merged_check else ""),
-                       "sets_per_step_per_gpu": args.sets, "inflight_batches_per_gpu": args.inflight,
-                       "parallelism": f"shard-by-request x{world}"},
-            "p50_latency_ms_128": round(statistics.median(lat), 3),
-            "stage_ms": {k: round(float(x), 3) for k, x in zip(STAGE_NAMES, stage_ms)},
-            "roofline": {"bound": "valu", "kernel": dom, "achieved": round(achieved, 4), "peak": round(peak, 3),
-                         "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5), "traffic": traffic,
-                         "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
-                                         f"{traffic_src})" if traffic else None,
-                         "work": f"{fpm_set:.0f} Fp products/set x {MADS_PER_FPM} MAD x {args.sets} sets "
-                                 f"per launch, {dom_ms:.3f} ms/launch (HIP events, median of 5 solo launches "
-                                 f"on one stream; {shared_ms:.3f} ms while {args.inflight} batches overlap)",
-                         "device_achieved": round(value * fpm_set * MADS_PER_FPM / 1e12, 4),
-                         "device_frac": round(value * fpm_set * MADS_PER_FPM / 1e12 / peak, 5),
-                         "device_note": "whole-job sets/s x k_pset MADs per set: the device-wide useful "
-                                        "MAD rate of the per-set kernel"},
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline()
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 3),
+               "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
+               "dtype": "u32 (381-bit Fp, 12x32-bit Montgomery limbs)",
+               "data": "synthetic: interop keys, sha256 messages, GPU-made signatures", "config": config}
+        out.update(extra)
+
+    if args.mode != "napi":
+        # p50 latency of one 128-set non-batchable call (cfg1 shape)
+        lat = []
+        for _ in range(args.latency_runs):
+            t1 = time.perf_counter()
+            v, _ = gpu.verify_packed(call128)
+            lat.append((time.perf_counter() - t1) * 1e3)
+            assert v[0] == 1
+        # roofline of the dominant kernel, the per-set cooperative kernel (VALU integer
+        # multiply-add bound).  achieved = the device-wide useful MAD rate of that kernel in
+        # the timed region: sets/s per GPU x its MADs per set (launches overlap across the
+        # in-flight streams, so wall time per launch = timed region / launches); the solo
+        # launch time of one call is reported beside it.
+        fpm_set = pset_products_per_set(S)
+        mad_set = fpm_set * MADS_PER_FPM
+        solo = []
+        for _ in range(5):
+            _, st = gpu.verify_packed(batch)
+            solo.append(st.stage_ms[STAGE_NAMES.index("k_pset")])
+        solo_ms = statistics.median(solo)
+        peak_rate, _ = gpu.mad_peak()
+        peak = peak_rate / 1e12
+        per_gpu = value / world
+        achieved = per_gpu * mad_set / 1e12
+        if rank == 0:
+            pmc = pmc_summary(f"k_psetn<{S}" if S > 1 else "k_pset")
+            roof = {"bound": "valu", "kernel": f"k_psetn<{S}>" if S > 1 else "k_pset", "achieved": round(achieved, 4),
+                    "peak": round(peak, 3), "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5),
+                    "traffic": None,
+                    "work": f"{fpm_set:.0f} Fp products/set x {MADS_PER_FPM} MAD ({S} sets per wavefront) x "
+                            f"{per_gpu:.0f} sets/s per GPU (timed region; launch wall time = region / launches)",
+                    "solo_launch_ms": round(solo_ms, 3),
+                    "solo_achieved": round(args.sets * mad_set / (solo_ms * 1e-3) / 1e12, 4),
+                    "peak_note": "measured: bls_gpu_mad_peak, every CU at 8 waves/SIMD"}
+            if pmc:
+                wc = pmc.get("SQ_WAVE_CYCLES")
+                roof["pmc"] = {"source": pmc["source"],
+                               "valu_issue_frac": round(pmc["SQ_ACTIVE_INST_VALU"] / wc, 3) if wc else None,
+                               "wait_frac": round(pmc["SQ_WAIT_ANY"] / wc, 3) if wc else None,
+                               "waves_per_simd": pmc.get("waves_per_simd"),
+                               "valu_insts_per_wave": round(pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"]),
+                               "note": pmc.get("note")}
+                roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+            out["p50_latency_ms_128"] = round(statistics.median(lat), 3)
+            out["stage_ms"] = {k: round(float(x), 3) for k, x in zip(STAGE_NAMES, stage_ms)}
+            out["roofline"] = roof
+            if world == 1 and not args.no_cpu_baseline and args.mode == "cfg2":
+                out["cpu_baseline"] = cpu_baseline(sets, raw96, seconds=args.cpu_seconds,
+                                                   latency_runs=args.latency_runs)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     for c in ctxs:
         c.close()

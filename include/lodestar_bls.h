@@ -120,12 +120,17 @@ int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* batch, int32_t* verdicts, 
  * with r_i drawn from the call's shared seed at index set_index_base + i, so the
  * scalars of all shards are distinct draws of one batch.  batch->seed must be set
  * (the same 32 bytes on every rank).  out576 receives P_rank as 12 Fp (opaque device
- * form: 12 x 48-byte Montgomery limbs; only bls_gpu_final_check reads it).  status:
- * 0 if every set decoded, else -(code) of the first failing request in order -- the
- * whole call then rejects (rule 2 of SURVEY §8a) and out576 is undefined.
- * The shard must hold >= 1 set. */
+ * form: 12 x 48-byte Montgomery limbs; only bls_gpu_final_check reads it).  The shard is
+ * verified with the rules of a multi-set call (no single-set rules, even for a 1-set
+ * shard).  status: 0 if every set decoded, else -(code) of the shard's first error in
+ * the reference's order -- class 0 a pubkey that does not decode / aggregate
+ * (deserializeSet, worker.ts:45), class 1 a signature that does not decode
+ * (maybeBatch.ts:19-24), class 2 an infinity pubkey -- and err_info (nullable,
+ * 2 words) receives {class, shard-local set index} (class 3: none) so the ranks can
+ * pick the call's first error; the whole call then rejects (rule 2 of SURVEY §8a) and
+ * out576 is undefined.  The shard must hold >= 1 set. */
 int bls_gpu_partial(bls_gpu_ctx* ctx, const bls_batch* batch, uint32_t set_index_base, uint8_t* out576,
-                    int32_t* status, bls_stats* stats);
+                    int32_t* status, uint32_t* err_info, bls_stats* stats);
 
 /* The combine step after the all-gather: *verdict = 1 iff FE(prod_k partials[k]) == 1,
  * one final exponentiation for the whole call (n >= 1 partials of 576 bytes). */

@@ -1,0 +1,54 @@
+"use strict";
+/**
+ * bench.py --mode napi: the cfg2 workload through the N-API addon and GpuBlsVerifier,
+ * driven the way gossip validation drives IBlsVerifier (one
+ * verifySignatureSets([set], {batchable: true}) per attestation,
+ * chain/validation/attestation.ts:138).  A step submits inflight x nSets such calls;
+ * two steps are kept outstanding so the contexts never wait for the JS side.
+ *
+ *   node benchNapi.js work.json steps inflight nSets   -> one JSON line
+ */
+const fs = require("fs");
+const {GpuBlsVerifier} = require("./gpuBlsVerifier.js");
+
+async function main() {
+  const [file, stepsS, inflightS, nSetsS] = process.argv.slice(2);
+  const steps = Number(stepsS);
+  const inflight = Number(inflightS);
+  const nSets = Number(nSetsS);
+  const data = JSON.parse(fs.readFileSync(file, "utf8"));
+  const sets = data.sets.map((s) => ({
+    pubkeyIndices: [s.idx],
+    signingRoot: Buffer.from(s.msg, "hex"),
+    signature: Buffer.from(s.sig, "hex"),
+  }));
+  const pool = new GpuBlsVerifier({contexts: inflight});
+  pool.loadPubkeys(Buffer.from(data.pubkeys48, "hex"));
+  const per = inflight * nSets;
+  const step = () => {
+    const ps = new Array(per);
+    for (let k = 0; k < per; k++) ps[k] = pool.verifySignatureSets([sets[k % nSets]], {batchable: true});
+    return Promise.all(ps);
+  };
+  const check = (r) => {
+    for (const v of r) if (v !== true) throw Error("a valid set did not verify");
+  };
+  check(await step()); // warm-up
+  const t0 = process.hrtime.bigint();
+  const pending = [];
+  for (let s = 0; s < steps; s++) {
+    pending.push(step());
+    if (pending.length >= 2) check(await pending.shift());
+  }
+  for (const p of pending) check(await p);
+  const dt = Number(process.hrtime.bigint() - t0) / 1e9;
+  const st = pool.stats;
+  await pool.close();
+  console.log(JSON.stringify({sets_per_s: (steps * per) / dt, elapsed_s: dt, steps, sets_per_step: per,
+                              gpu_calls: st.jobGroupsStarted, jobs: st.jobsStarted}));
+}
+
+main().catch((e) => {
+  console.error("benchNapi failed:", e && e.stack);
+  process.exit(1);
+});

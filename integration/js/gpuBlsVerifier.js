@@ -147,6 +147,10 @@ class GpuBlsVerifier {
         if (timer) timer();
       }
     }
+    if (sets.length > 0 && sets.length <= MAX_SIGNATURE_SETS_PER_JOB) {
+      // one job (chunkifyMaximizeChunkSize gives one chunk): skip the Promise.all
+      return (await this._queue({batchable: Boolean(opts.batchable), sets})) === true;
+    }
     const results = await Promise.all(
       chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((chunk) =>
         this._queue({batchable: Boolean(opts.batchable), sets: chunk})

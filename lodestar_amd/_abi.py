@@ -113,7 +113,7 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_verify.restype = i32
         lib.bls_gpu_validate_pubkeys.argtypes = [vp, vp, u32, u32, vp]
         lib.bls_gpu_validate_pubkeys.restype = i32
-        lib.bls_gpu_partial.argtypes = [vp, ctypes.POINTER(BlsBatch), u32, vp, vp, ctypes.POINTER(BlsStats)]
+        lib.bls_gpu_partial.argtypes = [vp, ctypes.POINTER(BlsBatch), u32, vp, vp, vp, ctypes.POINTER(BlsStats)]
         lib.bls_gpu_partial.restype = i32
         lib.bls_gpu_final_check.argtypes = [vp, vp, u32, vp]
         lib.bls_gpu_final_check.restype = i32

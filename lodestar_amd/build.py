@@ -107,6 +107,18 @@ def build_hostsim(verbose: bool = True) -> Path:
     return out
 
 
+def build_cpu_baseline(verbose: bool = True) -> Path:
+    """The C++ CPU baseline under oracle/cpu (benchmark / test infrastructure, "not
+    blst"; oracle/cpu/bls_cpu.cpp), next to its source: bench.py's cpu_baseline leg
+    loads it on the GPU box's host cores."""
+    out = ROOT / "oracle" / "cpu" / "libbls_cpu.so"
+    cmd = ["make", "-s", "-C", str(ROOT / "oracle" / "cpu")]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_napi(verbose: bool = True) -> Path | None:
     """N-API addon (integration/napi/lodestar_bls_napi.c) over the C-ABI, next to the
     library; skipped when the Node headers are absent."""
@@ -132,3 +144,4 @@ if __name__ == "__main__":
     build(jobs=int(sys.argv[1]) if len(sys.argv) > 1 else None)
     build_napi()
     build_hostsim()
+    build_cpu_baseline()

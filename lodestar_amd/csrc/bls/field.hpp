@@ -21,6 +21,7 @@
 #pragma once
 
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -163,32 +164,73 @@ BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
   return r;
 }
 #else
+// Host build (CPU test harness and the CPU baseline under oracle/): the 12 x 32-bit
+// little-endian limbs are the bytes of 6 x 64-bit little-endian words, so the CPU
+// works on 64-bit words with unsigned __int128 carries (x86-64 host only).
+static_assert(sizeof(Fp) == 48, "Fp is 6 x 64-bit words on the host");
+static inline void fp_w_load(const Fp& a, uint64_t w[6]) { memcpy(w, a.l, 48); }
+static inline Fp fp_w_store(const uint64_t w[6]) {
+  Fp r;
+  memcpy(r.l, w, 48);
+  return r;
+}
+static const uint64_t BLS_P64[6] = {0xb9feffffffffaaabull, 0x1eabfffeb153ffffull, 0x6730d2a0f6b0f624ull,
+                                    0x64774b84f38512bfull, 0x4b1ba7b6434bacd7ull, 0x1a0111ea397fe69aull};
+#define BLS_NP0_64 0x89f3fffcfffcfffdull  // -p^-1 mod 2^64
+
+// s - p when s >= p (s < 2p)
+static inline void fp_w_reduce(uint64_t s[6]) {
+  uint64_t d[6];
+  unsigned __int128 br = 0;
+  for (int i = 0; i < 6; ++i) {
+    const unsigned __int128 t = (unsigned __int128)s[i] - BLS_P64[i] - (uint64_t)br;
+    d[i] = (uint64_t)t;
+    br = (t >> 64) & 1;
+  }
+  if (!br) memcpy(s, d, 48);
+}
+
 // Reduce a value < 2p to [0, p).
-BLS_HD Fp fp_reduce_once(const Fp& s) {
-  Fp d;
-  uint32_t borrow = fp_sub_p(s, d);
-  return fp_select(borrow != 0, s, d);
+BLS_HD Fp fp_reduce_once(const Fp& a) {
+  uint64_t s[6];
+  fp_w_load(a, s);
+  fp_w_reduce(s);
+  return fp_w_store(s);
 }
 
 BLS_HD Fp fp_add(const Fp& a, const Fp& b) {
-  Fp s;
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) s.l[i] = addc32(a.l[i], b.l[i], c, &c);
-  return fp_reduce_once(s);  // a + b < 2p < 2^382: no carry out
+  uint64_t x[6], y[6];
+  fp_w_load(a, x);
+  fp_w_load(b, y);
+  unsigned __int128 c = 0;
+  for (int i = 0; i < 6; ++i) {
+    c += (unsigned __int128)x[i] + y[i];
+    x[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  fp_w_reduce(x);  // a + b < 2p < 2^382: no carry out
+  return fp_w_store(x);
 }
 
 BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
-  Fp d;
-  uint32_t borrow = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) d.l[i] = subc32(a.l[i], b.l[i], borrow, &borrow);
-  // if a < b add p back
-  uint32_t mask = 0u - borrow;
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) d.l[i] = addc32(d.l[i], p_limb(i) & mask, c, &c);
-  return d;
+  uint64_t x[6], y[6];
+  fp_w_load(a, x);
+  fp_w_load(b, y);
+  unsigned __int128 br = 0;
+  for (int i = 0; i < 6; ++i) {
+    const unsigned __int128 t = (unsigned __int128)x[i] - y[i] - (uint64_t)br;
+    x[i] = (uint64_t)t;
+    br = (t >> 64) & 1;
+  }
+  if (br) {  // a < b: add p back
+    unsigned __int128 c = 0;
+    for (int i = 0; i < 6; ++i) {
+      c += (unsigned __int128)x[i] + BLS_P64[i];
+      x[i] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  return fp_w_store(x);
 }
 #endif
 
@@ -367,35 +409,41 @@ __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_m
 __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cols<true>(a, b); }
 BLS_NOINLINE Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
 #else
-// Host build (test harness): Montgomery product a*b/R mod p, CIOS with the no-carry
-// optimisation (valid because p's top limb 0x1a0111ea < 2^31 - 1).  Inputs < p, output < p.
-BLS_NOINLINE Fp fp_mul(Fp a, Fp b) {
+// Host build: Montgomery product a*b/R mod p (R = 2^384) over 6 x 64-bit words,
+// separated operand scanning (the 36 partial products of a*b first, then the word-by-
+// word reduction), unsigned __int128 products.  Inputs < p, output < p.
+BLS_HD Fp fp_mul(const Fp& a, const Fp& b) {
   BLS_COUNT_FPM();
-  uint32_t t[12];
-#pragma unroll
-  for (int j = 0; j < 12; ++j) t[j] = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const uint32_t bi = b.l[i];
-    uint64_t A = (uint64_t)a.l[0] * bi + t[0];
-    const uint32_t m = (uint32_t)A * BLS_NP0;
-    uint64_t C = (uint64_t)m * p_limb(0) + (uint32_t)A;
-    A >>= 32;
-    C >>= 32;
-#pragma unroll
-    for (int j = 1; j < 12; ++j) {
-      A = (uint64_t)a.l[j] * bi + t[j] + A;
-      C = (uint64_t)m * p_limb(j) + (uint32_t)A + C;
-      t[j - 1] = (uint32_t)C;
-      A >>= 32;
-      C >>= 32;
+  typedef unsigned __int128 u128;
+  uint64_t x[6], y[6], t[13];
+  fp_w_load(a, x);
+  fp_w_load(b, y);
+  for (int k = 0; k < 13; ++k) t[k] = 0;
+  for (int i = 0; i < 6; ++i) {
+    uint64_t c = 0;
+    for (int j = 0; j < 6; ++j) {
+      const u128 v = (u128)x[i] * y[j] + t[i + j] + c;
+      t[i + j] = (uint64_t)v;
+      c = (uint64_t)(v >> 64);
     }
-    t[11] = (uint32_t)(C + A);
+    t[i + 6] = c;
   }
-  Fp r;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) r.l[j] = t[j];
-  return fp_reduce_once(r);
+  for (int i = 0; i < 6; ++i) {
+    const uint64_t m = t[i] * BLS_NP0_64;
+    uint64_t c = 0;
+    for (int j = 0; j < 6; ++j) {
+      const u128 v = (u128)m * BLS_P64[j] + t[i + j] + c;
+      t[i + j] = (uint64_t)v;
+      c = (uint64_t)(v >> 64);
+    }
+    for (int k = i + 6; k < 13 && c; ++k) {
+      const u128 v = (u128)t[k] + c;
+      t[k] = (uint64_t)v;
+      c = (uint64_t)(v >> 64);
+    }
+  }
+  fp_w_reduce(t + 6);  // t < 2p
+  return fp_w_store(t + 6);
 }
 BLS_HD Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul(a, b); }
 BLS_HD Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul(a, b); }

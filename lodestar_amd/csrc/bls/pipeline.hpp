@@ -49,6 +49,8 @@ struct PipeBufs {
   uint32_t n_uniq;
   uint32_t scalar_base;        // set i draws r from index scalar_base + i (shards of one call, bls_gpu_partial)
   uint32_t pack;               // sets per wavefront of k_pset (0: by call size; BLS_DEBUG_PACK)
+  uint32_t multi_set_rules;    // a shard of a larger call (bls_gpu_partial): no 1-set rules
+  uint8_t* pk_inf;             // n_sets (nullable): 1 = the set's (aggregate) pubkey is infinity
   const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs
   const uint32_t* chunk_reqs;
   const uint32_t* indiv_reqs;  // n_indiv
@@ -133,6 +135,7 @@ BLS_HD void stage_pk(const PipeBufs& b, uint32_t i) {
   }
   b.pk[i] = acc;
   b.pk_status[i] = code;
+  if (b.pk_inf) b.pk_inf[i] = (code == BLS_OK && jac_is_inf(acc)) ? 1 : 0;
 }
 
 BLS_HD void stage_sig(const PipeBufs& b, uint32_t i) {
@@ -290,7 +293,7 @@ BLS_HD void stage_req_status(const PipeBufs& b, uint32_t r) {
   for (uint32_t i = beg; i < end && code == BLS_OK; ++i)
     if (b.sig_status[i] != BLS_OK) code = b.sig_status[i];
   if (code == BLS_OK) {
-    if (end - beg == 1) {
+    if (end - beg == 1 && !b.multi_set_rules) {
       if (b.sig[beg].inf) code = BLS_ZERO_SIGNATURE;
       else if (jac_is_inf(b.pk[beg])) code = BLS_PK_IS_INFINITY;
     } else {

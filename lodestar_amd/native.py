@@ -184,19 +184,23 @@ class GpuContext:
         self._check(rc, "bls_gpu_verify")
         return verdicts[: pb.n_reqs], stats
 
-    def partial(self, pb: PackedBatch, set_index_base: int) -> tuple[bytes | None, int, BlsStats]:
+    def partial(self, pb: PackedBatch, set_index_base: int):
         """Miller-loop partial of this shard of a sharded call (bls_gpu_partial):
-        (576 opaque bytes or None on a decode error, status 0 / -code, stats)."""
+        (576 opaque bytes or None on an error, status 0 / -code, (class, shard-local set
+        index) of the error or None, stats)."""
         if pb.seed is None:
             raise ValueError("a sharded call needs the call's shared 32-byte seed")
         b, _keep = self._batch_struct(pb)
         out = np.zeros(576, dtype=np.uint8)
         status = ctypes.c_int32(0)
+        err = np.zeros(2, dtype=np.uint32)
         stats = BlsStats()
         rc = self.lib.bls_gpu_partial(self._h, ctypes.byref(b), set_index_base, _ptr(out), ctypes.byref(status),
-                                      ctypes.byref(stats))
+                                      _ptr(err), ctypes.byref(stats))
         self._check(rc, "bls_gpu_partial")
-        return (out.tobytes() if status.value == 0 else None), status.value, stats
+        if status.value == 0:
+            return out.tobytes(), 0, None, stats
+        return None, status.value, (int(err[0]), int(err[1])), stats
 
     def final_check(self, partials: list[bytes]) -> bool:
         """FE(prod partials) == 1: the one final exponentiation of a sharded call."""

@@ -39,7 +39,7 @@ def global_throughput(local_sets: int, local_elapsed_s: float, dist=None, device
 # ---------------------------------------------------------------------------
 # One call split across GPUs (the north_star's "each GPU reduces its shard to an
 # Fp12 partial, the partials are combined over RCCL/xGMI, and one final
-# exponentiation follows").  The exchange is a 580-byte all-gather per rank.
+# exponentiation follows").  The exchange is a 588-byte all-gather per rank.
 # ---------------------------------------------------------------------------
 PARTIAL_BYTES = 576
 
@@ -63,23 +63,39 @@ class GpuPartialBackend:
         self.gpu = gpu
 
     def partial(self, sets, set_index_base: int, seed: bytes):
+        """(576-byte partial or None, status 0 / -code, (class, shard-local index) or None)"""
         from .native import pack_requests
 
-        part, status, _ = self.gpu.partial(pack_requests([(True, sets)], seed=seed), set_index_base)
-        return part, status
+        part, status, err, _ = self.gpu.partial(pack_requests([(True, sets)], seed=seed), set_index_base)
+        return part, status, err
 
     def final_check(self, partials: list[bytes]) -> bool:
         return self.gpu.final_check(partials)
+
+
+RECORD_BYTES = 12 + PARTIAL_BYTES   # int32 status, int32 error class, uint32 call index, Fp12 partial
+
+
+def first_error(records) -> int:
+    """The call's rejection code from the ranks' (status, class, call index) triples:
+    the lowest error class first (0 a pubkey that does not decode / aggregate, 1 a
+    signature that does not decode, 2 an infinity pubkey -- the order in which the
+    reference's worker meets them, worker.ts:45 then maybeBatch.ts:19-24), then the
+    lowest index in the call; 0 if no rank failed."""
+    bad = [(cls, idx, st) for st, cls, idx in records if st < 0]
+    return min(bad)[2] if bad else 0
 
 
 def verify_call_sharded(sets, seed: bytes, backend, dist=None, device=None, localize: bool = True):
     """verifySignatureSets on ONE call whose sets are spread over the ranks.
 
     Semantics: an undecodable set rejects the call with its code (the
-    first failing set in call order wins); otherwise the verdict is the random-scalar
-    batch check of all sets (maybeBatch.ts:18-25), done as one final exponentiation
-    over the product of the ranks' Miller-loop partials.  Every rank passes the whole
-    call's `sets` (each uses only its contiguous shard) and the same 32-byte `seed`.
+    first error in the reference's order, `first_error`); otherwise the verdict is the
+    random-scalar batch check of all sets (maybeBatch.ts:18-25), done as one final
+    exponentiation over the product of the ranks' Miller-loop partials.  Every shard is
+    verified with the rules of a multi-set call, so a sharded call gives the verdict of
+    the same call unsharded.  Every rank passes the whole call's `sets` (each uses only
+    its contiguous shard) and the same 32-byte `seed`.
 
     Returns (verdict, info): verdict True / False, or a negative error code;
     info["bad_shards"] lists the ranks whose own partial fails its final
@@ -92,19 +108,22 @@ def verify_call_sharded(sets, seed: bytes, backend, dist=None, device=None, loca
     if n < 2:
         raise ValueError("a sharded call needs >= 2 sets (1-set calls take the non-batched path)")
     beg, end = shard_bounds(n, world)[rank]
-    rec = np.zeros(4 + PARTIAL_BYTES, dtype=np.uint8)
-    rec[:4] = np.frombuffer(np.int32(1).tobytes(), dtype=np.uint8)  # 1 = empty shard
+    rec = np.zeros(RECORD_BYTES, dtype=np.uint8)
+    head = np.array([1, 3, 0], dtype=np.int32)  # status 1 = empty shard
     if end > beg:
-        part, status = backend.partial(sets[beg:end], beg, seed)
-        rec[:4] = np.frombuffer(np.int32(status).tobytes(), dtype=np.uint8)
+        part, status, err = backend.partial(sets[beg:end], beg, seed)
+        head[0] = status
+        if err is not None:
+            head[1], head[2] = err[0], beg + err[1]
         if part is not None:
-            rec[4:] = np.frombuffer(part, dtype=np.uint8)
+            rec[12:] = np.frombuffer(part, dtype=np.uint8)
+    rec[:12] = head.view(np.uint8)
     recs = _all_gather_bytes(rec, dist, device) if world > 1 else [rec]
-    statuses = [int(np.frombuffer(r[:4].tobytes(), dtype=np.int32)[0]) for r in recs]
-    for st in statuses:                       # ranks hold the call in order
-        if st < 0:
-            return st, {"bad_shards": []}
-    partials = [r[4:].tobytes() for r, st in zip(recs, statuses) if st == 0]
+    heads = [np.frombuffer(r[:12].tobytes(), dtype=np.int32) for r in recs]
+    code = first_error([(int(h[0]), int(h[1]), int(h[2])) for h in heads])
+    if code < 0:
+        return code, {"bad_shards": []}
+    partials = [r[12:].tobytes() for r, h in zip(recs, heads) if int(h[0]) == 0]
     # one final exponentiation for the whole call (rank 0), verdict broadcast
     ok = backend.final_check(partials) if rank == 0 else False
     if world > 1:
@@ -112,8 +131,8 @@ def verify_call_sharded(sets, seed: bytes, backend, dist=None, device=None, loca
     info = {"bad_shards": []}
     if not ok and localize:
         mine = 1
-        if statuses[rank] == 0:
-            mine = int(backend.final_check([recs[rank][4:].tobytes()]))
+        if int(heads[rank][0]) == 0:
+            mine = int(backend.final_check([recs[rank][12:].tobytes()]))
         flags = _all_gather_bytes(np.array([mine], dtype=np.uint8), dist, device) if world > 1 else [[mine]]
         info["bad_shards"] = [k for k, f in enumerate(flags) if int(f[0]) == 0]
     return ok, info

@@ -350,7 +350,7 @@ def test_sharded_partials_final_check(gpu, oracle, table):
     def partials(ss):
         out = []
         for beg, end in bounds:
-            p, st, _ = gpu.partial(pack_requests([(True, ss[beg:end])], seed=seed), beg)
+            p, st, _, _ = gpu.partial(pack_requests([(True, ss[beg:end])], seed=seed), beg)
             assert st == 0
             out.append(p)
         return out
@@ -371,8 +371,8 @@ def test_sharded_partials_final_check(gpu, oracle, table):
     enc = list(sets)
     enc[4] = (enc[4][0], enc[4][1], b"\x00" * 96)
     beg, end = bounds[1]
-    p, st, _ = gpu.partial(pack_requests([(True, enc[beg:end])], seed=seed), beg)
-    assert p is None and st == -CODE_BAD_ENCODING
+    p, st, err, _ = gpu.partial(pack_requests([(True, enc[beg:end])], seed=seed), beg)
+    assert p is None and st == -CODE_BAD_ENCODING and err == (1, 4 - beg)
 
 
 def _sharded_gpu_rank(rank, world, port, sets, q):
@@ -406,12 +406,14 @@ def test_sharded_call_two_ranks(gpu, oracle):
     raw = [oracle.g1_serialize(oracle.sk_to_pk(int.from_bytes(s, "big"))) for s in sks]
     good = [(raw[i], msgs[i], sigs[i].tobytes()) for i in range(6)]
     bad = good[:1] + [(raw[1], msgs[2], sigs[1].tobytes())] + good[2:]
+    two_inf = [good[0], (raw[1], msgs[1], bytes([0xC0]) + bytes(95))]
+    order = [(raw[0], msgs[0], bytes(32))] + good[1:5] + [(bytes([0x80]) + raw[5][1:], msgs[5], sigs[5].tobytes())]
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad], q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad, two_inf, order], q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=100) for _ in procs)
@@ -421,6 +423,8 @@ def test_sharded_call_two_ranks(gpu, oracle):
     for r in (0, 1):
         assert res[r][0] == (True, {"bad_shards": []})
         assert res[r][1] == (False, {"bad_shards": [0]})
+        assert res[r][2] == (False, {"bad_shards": []}) or res[r][2][0] is False   # infinity sig, 1-set shards
+        assert res[r][3][0] == -CODE_BAD_ENCODING                                  # pubkey error beats signature
 
 
 # ---------------------------------------------------------------------------

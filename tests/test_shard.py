@@ -97,18 +97,31 @@ class OraclePartialBackend:
         return r or 1
 
     def partial(self, sets, base, seed):
+        """(partial, status, (class, local index)) with multi-set rules, first error of
+        the lowest class: 0 pubkey decode, 1 signature decode, 2 infinity pubkey."""
         O = self.O
-        f = O.F12_ONE
-        for k, (pk96, msg, sig) in enumerate(sets):
+        decoded = []
+        for k, (pk96, _, _) in enumerate(sets):
+            code, pk = O.g1_deserialize(pk96)
+            if code != O.E_OK:
+                return None, -code, (0, k)
+            decoded.append(pk)
+        sigs = []
+        for k, (_, _, sig) in enumerate(sets):
             try:
-                s = O.signature_from_bytes(sig, validate=True)
+                sigs.append(O.signature_from_bytes(sig, validate=True))
             except O.BlsError as e:
-                return None, -e.code
-            _, pk = O.g1_deserialize(pk96)
+                return None, -e.code, (1, k)
+        for k, pk in enumerate(decoded):
+            if pk is None:
+                return None, -O.E_PK_IS_INFINITY, (2, k)
+        f = O.F12_ONE
+        for k, ((_, msg, _), pk, s) in enumerate(zip(sets, decoded, sigs)):
             r = self._scalar(seed, base + k)
             f = O.f12_mul(f, O.miller_loop(O.E1.mul(pk, r), O.hash_to_g2(msg)))
-            f = O.f12_mul(f, O.miller_loop(O.E1.neg(O.G1), O.E2.mul(s, r)))
-        return b"".join(v.to_bytes(48, "big") for c in f for v in c), 0
+            if s is not None:
+                f = O.f12_mul(f, O.miller_loop(O.E1.neg(O.G1), O.E2.mul(s, r)))
+        return b"".join(v.to_bytes(48, "big") for c in f for v in c), 0, None
 
     def final_check(self, partials):
         O = self.O
@@ -131,7 +144,14 @@ def _sharded_cases():
     good = list(zip(pks, msgs, sigs))
     wrong_msg = good[:3] + [(pks[3], msgs[0], sigs[3])]          # invalid set in rank 1's shard
     bad_enc = good[:1] + [(pks[1], msgs[1], b"\x00" * 96)] + good[2:]  # undecodable (no compression flag)
-    return {"good": good, "wrong_msg": wrong_msg, "bad_enc": bad_enc}
+    # the unsharded call decides these, not the shards' own rules
+    inf_sig = bytes([0xC0]) + bytes(95)
+    two_inf = [good[0], (pks[1], msgs[1], inf_sig)]               # 1-set shards: false, not ZERO_SIGNATURE
+    bad_pk = bytes([0x80]) + pks[3][1:]
+    order = [(pks[0], msgs[0], sigs[0][:32])] + good[1:3] + [(bad_pk, msgs[3], sigs[3])]
+    inf_pk = good[:2] + [(O.g1_serialize(None), msgs[2], sigs[2]), good[3]]
+    return {"good": good, "wrong_msg": wrong_msg, "bad_enc": bad_enc, "two_inf": two_inf, "order": order,
+            "inf_pk": inf_pk}
 
 
 def _sharded_rank(rank, world, port, q):
@@ -170,3 +190,62 @@ def test_gloo_world2_sharded_call_partials():
         assert out["good"] == (True, {"bad_shards": []})
         assert out["wrong_msg"] == (False, {"bad_shards": [1]})
         assert out["bad_enc"][0] == -O.E_BAD_ENCODING
+        # a 2-set call over 2 ranks with an infinity signature: the multi-set verdict
+        # (false), as unsharded (oracle verify_multiple), not the 1-set ZERO_SIGNATURE
+        assert out["two_inf"][0] is False
+        # a signature error in rank 0's shard and a pubkey error in rank 1's: the pubkey
+        # error wins (deserializeSet runs first, worker.ts:45)
+        assert out["order"][0] == -O.E_BAD_ENCODING
+        assert out["inf_pk"][0] == -O.E_PK_IS_INFINITY
+
+
+def test_first_error_order():
+    from lodestar_amd.shard import first_error
+
+    assert first_error([(0, 3, 0), (0, 3, 0)]) == 0
+    assert first_error([(-8, 1, 0), (-2, 0, 7)]) == -2         # pubkey class before signature class
+    assert first_error([(-3, 1, 9), (-8, 1, 4)]) == -8         # same class: lower call index
+    assert first_error([(-6, 2, 1), (-1, 1, 5)]) == -1
+
+
+# ---------------------------------------------------------------------------
+# bench.py --mode sharded, dry run: the bench's own timed loop (run_sharded) and
+# max-over-ranks reduction over gloo with two ranks; only the per-rank partial backend
+# is the oracle's (no GPU here).
+# ---------------------------------------------------------------------------
+def _bench_sharded_rank(rank, world, port, q):
+    import hashlib
+
+    import torch.distributed as dist
+
+    import bench
+    from lodestar_amd.shard import global_throughput
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sets = _sharded_cases()["good"]
+    seed = hashlib.sha256(b"sharded-bench").digest()
+    elapsed, total = bench.run_sharded(OraclePartialBackend(), sets, seed, 1, 0, dist, None)
+    value, emax = global_throughput(total * 1 / world, elapsed, dist)
+    q.put((rank, total, value, emax, elapsed))
+    dist.destroy_process_group()
+
+
+def test_bench_sharded_mode_gloo_world2():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_sharded_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    emax = max(r[4] for r in res)
+    for _, total, value, e, _ in res:
+        assert total == 4
+        assert e == pytest.approx(emax)
+        assert value == pytest.approx(4 / emax)
