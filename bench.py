@@ -252,15 +252,16 @@ def run_sharded(be, sets, seed, steps, warmup, dist, device):
     return time.perf_counter() - t0, len(sets)
 
 
-def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int) -> dict:
+def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int, per_call: int = 1) -> dict:
     """--mode napi: integration/js/benchNapi.js in a child Node process (the GPU is not
-    touched by this process meanwhile)."""
+    touched by this process meanwhile); per_call sets per verifySignatureSets call."""
     node = shutil.which("node")
     if node is None:
         raise SystemExit("--mode napi needs node")
     env = dict(os.environ, UV_THREADPOOL_SIZE=str(max(4, inflight + 2)))
     out = subprocess.run([node, str(ROOT / "integration" / "js" / "benchNapi.js"), str(work_file), str(steps),
-                          str(inflight), str(n_sets)], capture_output=True, text=True, env=env, timeout=1200)
+                          str(inflight), str(n_sets), str(per_call)], capture_output=True, text=True, env=env,
+                         timeout=1200)
     if out.returncode != 0:
         raise SystemExit(f"benchNapi.js failed: {out.stderr[-2000:]}")
     return json.loads(out.stdout.strip().splitlines()[-1])
@@ -373,10 +374,13 @@ def main() -> None:
             for c in ctxs:
                 c.close()
             ctxs = []
-            res = run_napi(wf, args.steps, args.inflight, args.sets)
+            batched = run_napi(wf, args.steps, args.inflight, args.sets, args.sets)
+            res = run_napi(wf, args.steps, args.inflight, args.sets, 1)
         value, elapsed = res["sets_per_s"], res["elapsed_s"]
         stage_ms = np.zeros(8)
-        extra["napi"] = res
+        extra["napi"] = {"per_set_calls": res, "calls_of_1024_sets": batched,
+                         "note": "per-set calls: one JS promise per attestation, bound by the Node main thread; "
+                                 "calls of 1024 sets (sync / block-import shape): bound by the GPU"}
         config = {"workload": "cfg2 through the N-API addon + JS GpuBlsVerifier: one verifySignatureSets([set], "
                               "{batchable: true}) per set, buffered and coalesced into GPU calls",
                   "sets_per_step_per_gpu": args.sets * args.inflight, "contexts": args.inflight,

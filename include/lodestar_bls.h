@@ -142,6 +142,16 @@ int bls_gpu_final_check(bls_gpu_ctx* ctx, const uint8_t* partials576, uint32_t n
 int bls_gpu_aggregate_pubkeys(bls_gpu_ctx* ctx, const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
                               uint32_t n_sets, uint8_t* out96, int32_t* codes);
 
+/* G2 signature aggregation for the op pools:
+ * Signature.aggregate(sigs.map((s) => Signature.fromBytes(s, undefined, true))) for each
+ * of n_lists lists (aggregatedAttestationPool.ts:320-327 aggregateInto,
+ * syncContributionAndProofPool.ts:181-185, syncCommitteeMessagePool.ts:122-129).
+ * List l holds the 96-byte compressed signatures [list_offsets[l], list_offsets[l+1]).
+ * out96: n_lists compressed sums; codes: 0, BLS_CODE_EMPTY_AGGREGATE for an empty list,
+ * or the code of the list's first signature that does not decode / is outside G2. */
+int bls_gpu_aggregate_signatures(bls_gpu_ctx* ctx, const uint8_t* sigs96, const uint32_t* list_offsets,
+                                 uint32_t n_lists, uint8_t* out96, int32_t* codes);
+
 /* Signature.fromBytes(bytes, CoordType.affine, validate) ([ext] @chainsafe/blst, as
  * maybeBatch.ts:23,36 call it): n 96-byte compressed G2 points -> out192 (uncompressed
  * ZCash order x.c1 || x.c0 || y.c1 || y.c0; the infinity encoding for the point at

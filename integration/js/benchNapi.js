@@ -1,12 +1,13 @@
 "use strict";
 /**
  * bench.py --mode napi: the cfg2 workload through the N-API addon and GpuBlsVerifier,
- * driven the way gossip validation drives IBlsVerifier (one
+ * driven the way gossip validation drives IBlsVerifier (setsPerCall = 1: one
  * verifySignatureSets([set], {batchable: true}) per attestation,
- * chain/validation/attestation.ts:138).  A step submits inflight x nSets such calls;
- * two steps are kept outstanding so the contexts never wait for the JS side.
+ * chain/validation/attestation.ts:138) or the way sync / block import does (calls of
+ * setsPerCall sets, sync/range/range.ts:191-214).  A step submits inflight x nSets
+ * sets; two steps are kept outstanding so the contexts never wait for the JS side.
  *
- *   node benchNapi.js work.json steps inflight nSets   -> one JSON line
+ *   node benchNapi.js work.json steps inflight nSets [setsPerCall]   -> one JSON line
  */
 const fs = require("fs");
 const {GpuBlsVerifier} = require("./gpuBlsVerifier.js");
@@ -16,6 +17,7 @@ async function main() {
   const steps = Number(stepsS);
   const inflight = Number(inflightS);
   const nSets = Number(nSetsS);
+  const perCall = Number(process.argv[6] || 1);
   const data = JSON.parse(fs.readFileSync(file, "utf8"));
   const sets = data.sets.map((s) => ({
     pubkeyIndices: [s.idx],
@@ -25,11 +27,13 @@ async function main() {
   const pool = new GpuBlsVerifier({contexts: inflight});
   pool.loadPubkeys(Buffer.from(data.pubkeys48, "hex"));
   const per = inflight * nSets;
-  const step = () => {
-    const ps = new Array(per);
-    for (let k = 0; k < per; k++) ps[k] = pool.verifySignatureSets([sets[k % nSets]], {batchable: true});
-    return Promise.all(ps);
-  };
+  const calls = [];
+  for (let k = 0; k < per; k += perCall) {
+    const c = [];
+    for (let j = k; j < Math.min(per, k + perCall); j++) c.push(sets[j % nSets]);
+    calls.push(c);
+  }
+  const step = () => Promise.all(calls.map((c) => pool.verifySignatureSets(c, {batchable: true})));
   const check = (r) => {
     for (const v of r) if (v !== true) throw Error("a valid set did not verify");
   };
@@ -45,6 +49,7 @@ async function main() {
   const st = pool.stats;
   await pool.close();
   console.log(JSON.stringify({sets_per_s: (steps * per) / dt, elapsed_s: dt, steps, sets_per_step: per,
+                              sets_per_call: perCall,
                               gpu_calls: st.jobGroupsStarted, jobs: st.jobsStarted}));
 }
 

@@ -20,7 +20,8 @@
  */
 const path = require("path");
 
-const addon = require(path.join(__dirname, "..", "..", "lodestar_amd", "_native", "lodestar_bls.node"));
+const ADDON_PATH = path.join(__dirname, "..", "..", "lodestar_amd", "_native", "lodestar_bls.node");
+let defaultAddon = null;
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:39
 const GPU_SETS_PER_CALL = 1024; // sets per bls_gpu_verify call (cfg2 shape)
@@ -115,11 +116,16 @@ class GpuBlsVerifier {
     this.blsVerifyAllMultiThread = Boolean(opts.blsVerifyAllMultiThread);
     this.maxSetsPerCall = opts.maxSetsPerCall || GPU_SETS_PER_CALL;
     this.metrics = opts.metrics || null; // {bls: {...}, blsThreadPool: {...}} with the reference's names
+    // the N-API addon (opts.addon: a stand-in with the same four functions, for host-side tests)
+    this.addon = opts.addon || (defaultAddon = defaultAddon || require(ADDON_PATH));
+    const addon = this.addon;
     this.ctxs = [];
     // `inflight`: calls queued or running on the context (the main-thread path may
     // share context 0 with a pool job; the library serialises calls per context)
     for (let i = 0; i < contexts; i++) this.ctxs.push({handle: addon.init(device), inflight: 0, id: i});
-    this.jobs = [];
+    this.jobs = []; // queue: jobs[jobsHead..] are pending
+    this.jobsHead = 0;
+    this.runScheduled = false;
     this.bufferedJobs = null;
     this.closed = false;
     this.stats = {jobsStarted: 0, sigSetsStarted: 0, jobGroupsStarted: 0, batchRetries: 0};
@@ -129,47 +135,74 @@ class GpuBlsVerifier {
    * All or nothing (bls_gpu_load_pubkeys appends no key of a batch holding a bad one). */
   loadPubkeys(pks48) {
     this.ctxs.forEach((c, i) => {
-      const codes = addon.loadPubkeys(c.handle, pks48, 48);
+      const codes = this.addon.loadPubkeys(c.handle, pks48, 48);
       const bad = codes.findIndex((x) => x !== 0);
       if (bad >= 0) throw Error(i === 0 ? `invalid pubkey at batch index ${bad}; no key appended` : "pubkey tables diverged");
     });
   }
 
-  /** IBlsVerifier.verifySignatureSets (index.ts:134-174) */
-  async verifySignatureSets(sets, opts = {}) {
+  /** IBlsVerifier.verifySignatureSets (index.ts:134-174).  Returns a Promise<boolean>. */
+  verifySignatureSets(sets, opts = {}) {
     if (this.metrics) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
     if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
       // "don't buffer": one non-batchable request now (verifySignatureSetsMaybeBatch)
       const timer = this.metrics && this.metrics.blsThreadPool.mainThreadDurationInThreadPool.startTimer();
-      try {
-        return this._settle(await this._call(this.ctxs[0], [{batchable: false, sets}]), 0);
-      } finally {
-        if (timer) timer();
-      }
+      return this._call(this.ctxs[0], [{batchable: false, sets}]).then(
+        (v) => {
+          if (timer) timer();
+          return this._settle(v, 0);
+        },
+        (e) => {
+          if (timer) timer();
+          throw e;
+        }
+      );
     }
     if (sets.length > 0 && sets.length <= MAX_SIGNATURE_SETS_PER_JOB) {
-      // one job (chunkifyMaximizeChunkSize gives one chunk): skip the Promise.all
-      return (await this._queue({batchable: Boolean(opts.batchable), sets})) === true;
+      // one job (chunkifyMaximizeChunkSize gives one chunk); the job resolves to the
+      // boolean verdict, so it is the call's result
+      return this._queue({batchable: Boolean(opts.batchable), sets});
     }
-    const results = await Promise.all(
+    return Promise.all(
       chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((chunk) =>
         this._queue({batchable: Boolean(opts.batchable), sets: chunk})
       )
-    );
-    if (results.length === 0) throw Error("Empty results array");
-    return results.every((v) => v === true);
+    ).then((results) => {
+      if (results.length === 0) throw Error("Empty results array");
+      return results.every((v) => v === true);
+    });
+  }
+
+  /**
+   * state-transition verifySignatureSet (src/util/signatureSets.ts:24-38) on the GPU,
+   * synchronous like the reference (which blocks the main thread in blst): one
+   * non-batchable request of one set (single, or aggregate with pubkeyIndices of length
+   * > 1 = verifyAggregate), true / false, throwing the blst-style error when the
+   * signature does not decode (Signature.fromBytes(sig, undefined, true)).
+   */
+  verifySignatureSetSync(set) {
+    return this._settle(this.addon.verifySync(this.ctxs[0].handle, packRequests([{batchable: false, sets: [set]}])), 0);
+  }
+
+  /** verifySignatureSet over many sets in one GPU call (e.g. every inline check of a
+   * block when batch verification is off): per-set booleans; a set that does not decode
+   * throws, as its own verifySignatureSet would. */
+  verifySignatureSetsEachSync(sets) {
+    const v = this.addon.verifySync(this.ctxs[0].handle, packRequests(sets.map((s) => ({batchable: false, sets: [s]}))));
+    return sets.map((_, i) => this._settle(v, i));
   }
 
   /** IBlsVerifier.close (index.ts:176-197): abort queued jobs, wait for calls in flight */
   async close() {
     this.closed = true;
     if (this.bufferedJobs) clearTimeout(this.bufferedJobs.timeout);
-    const pending = this.jobs.concat(this.bufferedJobs ? this.bufferedJobs.jobs : []);
+    const pending = this.jobs.slice(this.jobsHead).concat(this.bufferedJobs ? this.bufferedJobs.jobs : []);
     this.jobs = [];
+    this.jobsHead = 0;
     this.bufferedJobs = null;
     for (const j of pending) j.reject(Error("QUEUE_ABORTED"));
     while (this.ctxs.some((c) => c.inflight > 0)) await new Promise((r) => setTimeout(r, 5));
-    for (const c of this.ctxs) addon.close(c.handle);
+    for (const c of this.ctxs) this.addon.close(c.handle);
     this.ctxs = [];
   }
 
@@ -183,7 +216,7 @@ class GpuBlsVerifier {
     if (this.closed && this.ctxs.length === 0) throw Error("QUEUE_ABORTED");
     ctx.inflight++;
     try {
-      return await addon.verify(ctx.handle, packRequests(jobs));
+      return await this.addon.verify(ctx.handle, packRequests(jobs));
     } finally {
       ctx.inflight--;
     }
@@ -193,29 +226,48 @@ class GpuBlsVerifier {
   _queue(workReq) {
     if (this.closed) return Promise.reject(Error("QUEUE_ABORTED"));
     return new Promise((resolve, reject) => {
-      const job = {resolve, reject, workReq, addedTimeMs: Date.now()};
-      if (workReq.batchable) {
-        if (!this.bufferedJobs) {
-          this.bufferedJobs = {jobs: [], sigCount: 0, timeout: setTimeout(() => this._runBufferedJobs(), MAX_BUFFER_WAIT_MS)};
+      // the job is its own BlsWorkReq ({batchable, sets}) plus the promise handlers
+      const job = {resolve, reject, batchable: workReq.batchable, sets: workReq.sets,
+                   addedTimeMs: this.metrics ? Date.now() : 0};
+      if (job.batchable) {
+        let buf = this.bufferedJobs;
+        if (!buf) {
+          buf = this.bufferedJobs = {jobs: [], sigCount: 0, timeout: setTimeout(() => this._runBufferedJobs(), MAX_BUFFER_WAIT_MS)};
         }
-        this.bufferedJobs.jobs.push(job);
-        this.bufferedJobs.sigCount += workReq.sets.length;
-        if (this.bufferedJobs.sigCount > MAX_BUFFERED_SIGS) {
-          clearTimeout(this.bufferedJobs.timeout);
+        buf.jobs.push(job);
+        buf.sigCount += job.sets.length;
+        if (buf.sigCount > MAX_BUFFERED_SIGS) {
+          clearTimeout(buf.timeout);
           this._runBufferedJobs();
         }
       } else {
         this.jobs.push(job);
-        setTimeout(() => this._runJob(), 0);
+        this._scheduleRun();
       }
     });
   }
 
+  /** setTimeout(runJob, 0) (index.ts:282,409), at most one pending at a time */
+  _scheduleRun() {
+    if (this.runScheduled) return;
+    this.runScheduled = true;
+    setTimeout(() => {
+      this.runScheduled = false;
+      this._runJob();
+    }, 0);
+  }
+
   _runBufferedJobs() {
-    if (this.bufferedJobs) {
-      this.jobs.push(...this.bufferedJobs.jobs);
+    const buf = this.bufferedJobs;
+    if (buf) {
+      if (this.jobsHead >= this.jobs.length) {
+        this.jobs = buf.jobs; // queue empty: take the buffer's array as the queue
+        this.jobsHead = 0;
+      } else {
+        for (const j of buf.jobs) this.jobs.push(j);
+      }
       this.bufferedJobs = null;
-      setTimeout(() => this._runJob(), 0);
+      this._scheduleRun();
     }
   }
 
@@ -224,23 +276,29 @@ class GpuBlsVerifier {
   async _runJob() {
     if (this.closed) return;
     const ctx = this.ctxs.find((c) => c.inflight === 0);
-    if (!ctx || this.jobs.length === 0) return;
-    const isRaw = (j) => j.workReq.sets.some((s) => s.pubkey !== undefined);
-    const kind = isRaw(this.jobs[0]);
+    if (!ctx || this.jobsHead >= this.jobs.length) return;
+    const isRaw = (j) => j.sets[0] !== undefined && j.sets[0].pubkey !== undefined;
+    const kind = isRaw(this.jobs[this.jobsHead]);
     const jobs = [];
-    const rest = [];
+    const skipped = [];
     let total = 0;
-    while (this.jobs.length > 0) {
-      const j = this.jobs.shift();
-      if (total < this.maxSetsPerCall && isRaw(j) === kind) {
+    while (this.jobsHead < this.jobs.length && total < this.maxSetsPerCall) {
+      const j = this.jobs[this.jobsHead];
+      this.jobs[this.jobsHead++] = undefined;
+      if (isRaw(j) === kind) {
         jobs.push(j);
-        total += j.workReq.sets.length;
+        total += j.sets.length;
       } else {
-        rest.push(j);
-        if (total >= this.maxSetsPerCall) break;
+        skipped.push(j); // other pubkey form: a later call
       }
     }
-    this.jobs = rest.concat(this.jobs);
+    if (skipped.length > 0) {
+      this.jobs = skipped.concat(this.jobs.slice(this.jobsHead));
+      this.jobsHead = 0;
+    } else if (this.jobsHead > 4096 && this.jobsHead * 2 > this.jobs.length) {
+      this.jobs = this.jobs.slice(this.jobsHead);
+      this.jobsHead = 0;
+    }
     const tp = this.metrics && this.metrics.blsThreadPool;
     this.stats.jobGroupsStarted += 1;
     this.stats.jobsStarted += jobs.length;
@@ -251,34 +309,36 @@ class GpuBlsVerifier {
       tp.totalJobsStarted.inc(jobs.length);
       tp.totalSigSetsStarted.inc(total);
     }
-    if (this.jobs.length > 0) setTimeout(() => this._runJob(), 0); // another idle context may take the rest
+    if (this.jobsHead < this.jobs.length) this._scheduleRun(); // another idle context may take the rest
     let verdicts;
     const t0 = process.hrtime.bigint();
     try {
-      verdicts = await this._call(ctx, jobs.map((j) => j.workReq));
+      verdicts = await this._call(ctx, jobs);
     } catch (e) {
       for (const j of jobs) j.reject(e);
       if (tp) tp.errorJobsSignatureSetsCount.inc(total);
-      setTimeout(() => this._runJob(), 0);
+      this._scheduleRun();
       return;
     }
     if (tp) tp.jobsWorkerTime.inc({workerId: ctx.id}, Number(process.hrtime.bigint() - t0) / 1e9);
     let ok = 0;
     let err = 0;
-    jobs.forEach((j, i) => {
-      try {
-        j.resolve(this._settle(verdicts, i));
-        ok += j.workReq.sets.length;
-      } catch (e) {
-        j.reject(e);
-        err += j.workReq.sets.length;
+    for (let i = 0; i < jobs.length; i++) {
+      const j = jobs[i];
+      const code = verdicts[i];
+      if (code >= 0) {
+        j.resolve(code === 1);
+        ok += j.sets.length;
+      } else {
+        j.reject(Error(ERROR_MESSAGES[-code] || `BLST_ERROR: ${-code}`));
+        err += j.sets.length;
       }
-    });
+    }
     if (tp) {
       tp.successJobsSignatureSetsCount.inc(ok);
       tp.errorJobsSignatureSetsCount.inc(err);
     }
-    setTimeout(() => this._runJob(), 0);
+    this._scheduleRun();
   }
 }
 

@@ -50,6 +50,15 @@ async function main() {
   const wrong = Object.assign({}, sets[1], {signingRoot: sets[0].signingRoot});
   out.wrongMessage = await pool.verifySignatureSets(sets.concat([wrong]));
   out.empty = await pool.verifySignatureSets([]).then(() => "resolved", (e) => e.message);
+  // state-transition verifySignatureSet, synchronous (signatureSets.ts:24-38)
+  out.stfSync = [sets[0], wrong, invalid].map((s) => {
+    try {
+      return pool.verifySignatureSetSync(s);
+    } catch (e) {
+      return e.message;
+    }
+  });
+  out.stfEach = pool.verifySignatureSetsEachSync([sets[0], wrong, sets[2]]);
   await pool.close();
   assert.ok(true);
   console.log(JSON.stringify(out));

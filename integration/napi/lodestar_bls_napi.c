@@ -8,6 +8,7 @@
  *   verify(handle, {reqSetOffsets, reqBatchable, messages, signatures,
  *                   setPkOffsets?, pkIndices?, pubkeys?, signatureLens?, seed?})
  *          -> Promise<Int32Array verdicts>   (1 valid, 0 invalid, -code error)
+ *   verifySync(handle, request) -> Int32Array   (the same on the calling thread)
  *   close(handle)
  *
  * verify runs bls_gpu_verify on a libuv worker thread (napi_async_work): the JS
@@ -197,24 +198,17 @@ static int prop(napi_env env, napi_value obj, const char* name, void** data, siz
   return view_of(env, v, data, bytes);
 }
 
-static napi_value js_verify(napi_env env, napi_callback_info info) {
-  size_t argc = 2;
-  napi_value argv[2];
-  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bls_handle* h = argc >= 2 ? get_handle(env, argv[0]) : NULL;
-  if (!h) {
-    napi_throw_type_error(env, NULL, "verify(handle, request): no live handle (closed?)");
-    return NULL;
-  }
+/* Parse and check a request object into a bls_batch (buffers stay owned by the object). */
+static int parse_request(napi_env env, napi_value req, bls_batch* b) {
   void *ro, *rb, *msg, *sig, *spo, *pki, *pks, *sl, *seed;
   size_t nro, nrb, nmsg, nsig, nspo, npki, npks, nsl, nseed;
-  if (prop(env, argv[1], "reqSetOffsets", &ro, &nro) || prop(env, argv[1], "reqBatchable", &rb, &nrb) ||
-      prop(env, argv[1], "messages", &msg, &nmsg) || prop(env, argv[1], "signatures", &sig, &nsig) ||
-      prop(env, argv[1], "setPkOffsets", &spo, &nspo) || prop(env, argv[1], "pkIndices", &pki, &npki) ||
-      prop(env, argv[1], "pubkeys", &pks, &npks) || prop(env, argv[1], "signatureLens", &sl, &nsl) ||
-      prop(env, argv[1], "seed", &seed, &nseed) || nro < 4 || !ro) {
+  if (prop(env, req, "reqSetOffsets", &ro, &nro) || prop(env, req, "reqBatchable", &rb, &nrb) ||
+      prop(env, req, "messages", &msg, &nmsg) || prop(env, req, "signatures", &sig, &nsig) ||
+      prop(env, req, "setPkOffsets", &spo, &nspo) || prop(env, req, "pkIndices", &pki, &npki) ||
+      prop(env, req, "pubkeys", &pks, &npks) || prop(env, req, "signatureLens", &sl, &nsl) ||
+      prop(env, req, "seed", &seed, &nseed) || nro < 4 || !ro) {
     napi_throw_type_error(env, NULL, "verify: bad request object");
-    return NULL;
+    return -1;
   }
   /* every buffer must hold what n_reqs / n_sets say: the library reads exactly that */
   const uint32_t n_reqs = (uint32_t)(nro / 4 - 1);
@@ -226,23 +220,39 @@ static napi_value js_verify(napi_env env, napi_callback_info info) {
   if (!ok) {
     napi_throw_range_error(env, NULL, "verify: a buffer is shorter than n_reqs / n_sets require "
                                       "(pubkeys 96 B, messages 32 B, signatures 96 B per set)");
+    return -1;
+  }
+  memset(b, 0, sizeof(*b));
+  b->n_reqs = n_reqs;
+  b->n_sets = n_sets;
+  b->req_set_offsets = (const uint32_t*)ro;
+  b->req_batchable = (const uint8_t*)rb;
+  b->messages = (const uint8_t*)msg;
+  b->signatures = (const uint8_t*)sig;
+  b->set_pk_offsets = (const uint32_t*)spo;
+  b->pk_indices = (const uint32_t*)pki;
+  b->pubkeys = spo ? NULL : (const uint8_t*)pks;
+  b->signature_lens = (const uint32_t*)sl;
+  b->seed = nseed >= 32 ? (const uint8_t*)seed : NULL;
+  return 0;
+}
+
+static napi_value js_verify(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_handle* h = argc >= 2 ? get_handle(env, argv[0]) : NULL;
+  if (!h) {
+    napi_throw_type_error(env, NULL, "verify(handle, request): no live handle (closed?)");
     return NULL;
   }
+  bls_batch b;
+  if (parse_request(env, argv[1], &b)) return NULL;
   verify_job* j = (verify_job*)calloc(1, sizeof(verify_job));
   j->h = h;
   j->ctx = h->ctx;
-  j->batch.n_reqs = n_reqs;
-  j->batch.n_sets = n_sets;
-  j->batch.req_set_offsets = (const uint32_t*)ro;
-  j->batch.req_batchable = (const uint8_t*)rb;
-  j->batch.messages = (const uint8_t*)msg;
-  j->batch.signatures = (const uint8_t*)sig;
-  j->batch.set_pk_offsets = (const uint32_t*)spo;
-  j->batch.pk_indices = (const uint32_t*)pki;
-  j->batch.pubkeys = spo ? NULL : (const uint8_t*)pks;
-  j->batch.signature_lens = (const uint32_t*)sl;
-  j->batch.seed = nseed >= 32 ? (const uint8_t*)seed : NULL;
-  j->verdicts = (int32_t*)calloc(n_reqs ? n_reqs : 1, 4);
+  j->batch = b;
+  j->verdicts = (int32_t*)calloc(b.n_reqs ? b.n_reqs : 1, 4);
   napi_value promise, name;
   CHECK(env, napi_create_reference(env, argv[1], 1, &j->keep));
   CHECK(env, napi_create_reference(env, argv[0], 1, &j->keep_handle));
@@ -254,12 +264,38 @@ static napi_value js_verify(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+/* verifySync(handle, request) -> Int32Array: the same call on the calling thread, for the
+ * synchronous state-transition path (verifySignatureSet, state-transition
+ * src/util/signatureSets.ts:24-38), which blocks the main thread as blst's verify does. */
+static napi_value js_verify_sync(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_handle* h = argc >= 2 ? get_handle(env, argv[0]) : NULL;
+  if (!h) {
+    napi_throw_type_error(env, NULL, "verifySync(handle, request): no live handle (closed?)");
+    return NULL;
+  }
+  bls_batch b;
+  if (parse_request(env, argv[1], &b)) return NULL;
+  napi_value ab, out;
+  void* dst;
+  CHECK(env, napi_create_arraybuffer(env, 4 * (size_t)(b.n_reqs ? b.n_reqs : 1), &dst, &ab));
+  CHECK(env, napi_create_typedarray(env, napi_int32_array, b.n_reqs, ab, 0, &out));
+  if (bls_gpu_verify(h->ctx, &b, (int32_t*)dst, NULL) != 0) {
+    napi_throw_error(env, NULL, bls_gpu_last_error(h->ctx));
+    return NULL;
+  }
+  return out;
+}
+
 static napi_value module_init(napi_env env, napi_value exports) {
   napi_property_descriptor d[] = {
       {"init", NULL, js_init, NULL, NULL, NULL, napi_default, NULL},
       {"close", NULL, js_close, NULL, NULL, NULL, napi_default, NULL},
       {"loadPubkeys", NULL, js_load_pubkeys, NULL, NULL, NULL, napi_default, NULL},
       {"verify", NULL, js_verify, NULL, NULL, NULL, napi_default, NULL},
+      {"verifySync", NULL, js_verify_sync, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
   return exports;

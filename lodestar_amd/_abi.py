@@ -48,6 +48,7 @@ SYMBOLS = (
     "bls_gpu_final_check",
     "bls_gpu_hash_to_g2",
     "bls_gpu_g2_decompress",
+    "bls_gpu_aggregate_signatures",
     "bls_gpu_sk_to_pk",
     "bls_gpu_sign",
     "bls_gpu_mad_peak",
@@ -121,6 +122,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_aggregate_pubkeys.restype = i32
         lib.bls_gpu_g2_decompress.argtypes = [vp, vp, u32, i32, vp, vp]
         lib.bls_gpu_g2_decompress.restype = i32
+        lib.bls_gpu_aggregate_signatures.argtypes = [vp, vp, vp, u32, vp, vp]
+        lib.bls_gpu_aggregate_signatures.restype = i32
         lib.bls_gpu_hash_to_g2.argtypes = [vp, vp, u32, vp]
         lib.bls_gpu_hash_to_g2.restype = i32
         lib.bls_gpu_sk_to_pk.argtypes = [vp, vp, u32, vp]

@@ -19,6 +19,8 @@ hipError_t launch_k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk
 hipError_t launch_k_pre(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_exact(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_hash_to_g2(const uint8_t* msgs, uint32_t n, uint8_t* out192, hipStream_t s);
+hipError_t launch_k_sig_aggregate(const uint8_t* in96, uint32_t n, const uint32_t* off, uint32_t n_lists,
+                                  bls::G2A* pts, int32_t* sig_codes, uint8_t* out96, int32_t* codes, hipStream_t s);
 hipError_t launch_k_g2_decompress(const uint8_t* in96, uint32_t n, int validate, uint8_t* out192, int32_t* codes,
                                   hipStream_t s);
 hipError_t launch_k_sk_to_pk(const uint8_t* sks, uint32_t n, uint8_t* out48, hipStream_t s);

@@ -245,6 +245,27 @@ class GpuContext:
                     "bls_gpu_g2_decompress")
         return out[: 192 * n].reshape(n, 192), codes[:n]
 
+    def aggregate_signatures(self, sig_lists) -> tuple[list[bytes], np.ndarray]:
+        """Signature.aggregate over lists of 96-byte signatures (each decoded with
+        validate=true): (compressed sums, codes) (bls_gpu_aggregate_signatures)."""
+        offs, flat = [0], []
+        for lst in sig_lists:
+            for sig in lst:
+                b = bytes(sig)
+                if len(b) != 96:
+                    raise ValueError("signatures are 96 bytes (compressed G2)")
+                flat.append(b)
+            offs.append(len(flat))
+        n_lists = len(sig_lists)
+        o = np.array(offs, dtype=np.uint32)
+        buf = np.frombuffer(b"".join(flat), dtype=np.uint8).copy() if flat else np.zeros(96, np.uint8)
+        out = np.zeros(96 * max(n_lists, 1), dtype=np.uint8)
+        codes = np.zeros(max(n_lists, 1), dtype=np.int32)
+        self._check(self.lib.bls_gpu_aggregate_signatures(self._h, _ptr(buf), _ptr(o), n_lists, _ptr(out),
+                                                          _ptr(codes)), "bls_gpu_aggregate_signatures")
+        raw = out.tobytes()
+        return [raw[96 * i: 96 * i + 96] for i in range(n_lists)], codes[:n_lists]
+
     def sk_to_pk(self, sks: bytes | np.ndarray) -> np.ndarray:
         s = _u8(sks)
         n = s.size // 32

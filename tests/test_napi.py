@@ -20,9 +20,9 @@ pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node
 
 def test_addon_exports():
     code = ("const a = require(process.argv[1]);"
-            "console.log(JSON.stringify(['init','close','loadPubkeys','verify'].map(k => typeof a[k])))")
+            "console.log(JSON.stringify(['init','close','loadPubkeys','verify','verifySync'].map(k => typeof a[k])))")
     out = subprocess.run([NODE, "-e", code, str(ADDON)], capture_output=True, text=True, timeout=60, check=True)
-    assert json.loads(out.stdout) == ["function"] * 4
+    assert json.loads(out.stdout) == ["function"] * 5
 
 
 @pytest.mark.gpu
@@ -45,3 +45,20 @@ def test_js_pool_matches_reference_tests(gpu, golden, oracle, tmp_path):
     assert "BLST_INVALID_SIZE" in r["firstInvalid"]
     assert r["wrongMessage"] is False
     assert r["empty"] == "Empty signature set"
+    # state-transition verifySignatureSet through verifySync (signatureSets.ts:24-38)
+    assert r["stfSync"] == [True, False, "BLST_ERROR: BLST_INVALID_SIZE"]
+    assert r["stfEach"] == [True, False, True]
+
+
+def test_js_adapter_host_side():
+    """The adapter's queueing with a stand-in addon (no GPU): per-set gossip calls are
+    buffered (>32 sigs / 100 ms) and coalesced into calls of up to 1024 sets, verdicts
+    map back to their calls, an error code rejects only its own call, close() waits for
+    calls in flight and rejects queued jobs."""
+    out = subprocess.run([NODE, str(ROOT / "integration" / "js" / "adapterTest.js")], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["verdicts_ok"] and r["max_call_sets"] == 1024 and 4 <= r["calls"] <= 6
+    assert r["rejected"] == "BLST_ERROR: BLST_INVALID_SIZE" and r["others_true"]
+    assert r["closed"] == "QUEUE_ABORTED" and r["inflight_at_close"] == 0
