@@ -199,6 +199,11 @@ int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint
  * 0 = by call size), so one process can run the same call through every packing. */
 #define BLS_DEBUG_PACK(n) ((uint32_t)(n) << 8)
 #define BLS_DEBUG_PACK_MASK 0x300u
+/* Test / bench hook: force the aggregated-signature path (per-set chains one lane per
+ * set, e(-g1, sum r_i sig_i) once per chunk, single-pair cooperative Miller loops) or
+ * the all-cooperative per-set path; default: by call size (>= 512 sets: aggregated). */
+#define BLS_DEBUG_SIGAGG_ON 8u
+#define BLS_DEBUG_SIGAGG_OFF 16u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

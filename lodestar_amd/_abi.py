@@ -60,6 +60,8 @@ SYMBOLS = (
 DEBUG_FORCE_EXACT = 1
 DEBUG_NO_MSG_DEDUP = 2
 DEBUG_NO_MERGED_CHECK = 4
+DEBUG_SIGAGG_ON = 8
+DEBUG_SIGAGG_OFF = 16
 
 
 def DEBUG_PACK(n: int) -> int:

@@ -404,10 +404,18 @@ __device__ __forceinline__ Fp fp_sqr_cols(const Fp& a) {
   u.l[11] = (uint32_t)L[23];
   return fp_reduce_once(u);
 }
-BLS_NOINLINE Fp fp_sqr_dev(Fp a) { return fp_sqr_cols(a); }
+// BLS_FP_INLINE (a kernel TU that defines it before the includes): the product is
+// inlined at every use instead of called -- no call boundary for the register
+// allocator (k_chain's point chains keep their operands in registers)
+#ifdef BLS_FP_INLINE
+#define BLS_FP_MUL_ATTR static __device__ __forceinline__
+#else
+#define BLS_FP_MUL_ATTR BLS_NOINLINE
+#endif
+BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_sqr_cols(a); }
 __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul_cols<false>(a, b); }
 __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cols<true>(a, b); }
-BLS_NOINLINE Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
+BLS_FP_MUL_ATTR Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
 #else
 // Host build: Montgomery product a*b/R mod p (R = 2^384) over 6 x 64-bit words,
 // separated operand scanning (the 36 partial products of a*b first, then the word-by-

@@ -29,6 +29,14 @@
 
 namespace bls {
 
+// Aggregated-signature path (bls_gpu.hip): k_chain -> k_gsum / k_vset -> k_mln hand-off
+// per set, CHAIN_WORDS Fp: HQ = affine H(m) (x.c0, x.c1, y.c0, y.c1), RP = [r] pk
+// (G1 Jacobian), RS = [r] sig (G2 Jacobian x.c0, x.c1, y.c0, y.c1, z.c0, z.c1).
+// A group's virtual set (index n_sets + chunk, n_sets + n_chunks + individual
+// request) holds HQ = affine(sum of the group's RS) and RP = -g1.
+enum : int { CH_HQ = 0, CH_RP = 4, CH_RS = 7, CHAIN_WORDS = 13 };
+enum : uint32_t { CHAIN_ST_NOT_IN_G2 = 1u, CHAIN_ST_H_INF = 2u, CHAIN_ST_RP_INF = 4u };
+
 struct PipeBufs {
   uint32_t n_sets, n_reqs, n_chunks, n_indiv;
   // inputs
@@ -73,6 +81,16 @@ struct PipeBufs {
   Fp12* f;
   int32_t* req_status;
   Fp* q;               // n_sets * 8: the two SSWU points on E2' (x.c0, x.c1, y.c0, y.c1) per set
+  // aggregated-signature path (sigagg = 1): f_i = ML(r_i pk_i, H_i) only, and per group
+  // (chunk / individually verified request) one virtual set f = ML(-g1, sum r_i sig_i)
+  // at n_sets + chunk / n_sets + n_chunks + t, multiplied in by the chunk, individual,
+  // merged and partial products (kernels/k_fin.hip).  Sets the exact path finishes
+  // keep both pairings in their own f_i and are left out of the sums.
+  uint32_t sigagg;
+  Fp* chain;             // (n_sets + virtual) * CHAIN_WORDS (layout: CH_*)
+  uint32_t* chain_live;  // n_sets + virtual: 1 = k_mln runs this set's Miller loop
+  uint32_t* chain_st;    // n_sets: CHAIN_ST_* bits from k_chain's roles
+  const uint32_t* gsets; // set indices of the groups being summed, group-major (k_gsum level 0)
   uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
   uint32_t* flag_count;  // 1 word: sets flagged by the cooperative kernel (GPU path)
   // outputs

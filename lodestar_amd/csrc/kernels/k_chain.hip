@@ -1,0 +1,199 @@
+// Per-set scalar chains of the aggregated-signature path, one lane per set (SIMT):
+// everything of a set's work except its Miller loop.
+//
+//   in_group = psi(sig) == [x] sig         (Scott's G2 test: Signature.fromBytes(.., true),
+//                                           maybeBatch.ts:23,36)
+//   P  = iso(q0) + iso(q1)                 (Jacobian isogeny, no inversion)
+//   H  = clear_cofactor(P), affine         (RFC 9380 Budroni-Pintore, one inversion)
+//   RP = [r] pk,  RS = [r] sig             (the 64-bit batch scalar of
+//                                           verifyMultipleSignatures, [ext] blst)
+//
+// The batch equation prod e(r_i pk_i, H_i) * e(-g1, sum r_i sig_i) == 1 is then
+// evaluated as the reference's blst does it: one Miller loop per set for
+// (RP, H) (k_mln, cooperative) and ONE per group for (-g1, sum RS) (k_gsum sums
+// the RS of a chunk / request, k_vset turns the sum into a virtual set for k_mln).
+//
+// These are narrow, strictly sequential double-and-add chains (about 6k Fp products
+// per set: 3 G2 chains over |x|, one over r, one G1 chain over r): one lane per set
+// keeps all 64 lanes busy, where the cooperative interpreter filled 20..50 of 64
+// lanes per step with them.  The point formulas are curve.hpp's complete ones
+// (infinity and doubling branches), so no addition needs the exact path; the set
+// goes to k_exact only for an infinity signature, an SSWU input k_pre flagged,
+// H = O, or [r] pk = O (a pubkey outside G1).
+//
+// Output per live set (b.chain, CH_* layout); b.chain_live[i] = 1 (k_chain_done).  A
+// set whose request errors (decode status, infinity pubkey) or whose signature is
+// outside G2 gets f_i = 1 and is not live (not summed, no Miller loop).
+#define BLS_FP_INLINE 1
+#include "../launchers.hpp"
+
+using namespace bls;
+
+namespace {
+
+// 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3) into Jacobian coordinates:
+// x = xn / xd, y = y' yn / yd  ->  Z = xd yd, X = xn xd yd^2, Y = y' yn xd^3 yd^2.
+// A zero denominator gives Z = 0, the point at infinity (iso_map_g2's convention).
+__device__ G2J iso_map_jac(const Fp2& x, const Fp2& y) {
+  Fp2 xn = c_iso_xnum_3();
+  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_2());
+  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_1());
+  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_0());
+  Fp2 xd = fp2_add(x, c_iso_xden_1());
+  xd = fp2_add(fp2_mul(xd, x), c_iso_xden_0());
+  Fp2 yn = c_iso_ynum_3();
+  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_2());
+  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_1());
+  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_0());
+  Fp2 yd = fp2_add(x, c_iso_yden_2());
+  yd = fp2_add(fp2_mul(yd, x), c_iso_yden_1());
+  yd = fp2_add(fp2_mul(yd, x), c_iso_yden_0());
+  const Fp2 yd2 = fp2_sqr(yd);
+  const Fp2 xd2 = fp2_sqr(xd);
+  G2J r;
+  r.z = fp2_mul(xd, yd);
+  r.x = fp2_mul(fp2_mul(xn, xd), yd2);
+  r.y = fp2_mul(fp2_mul(fp2_mul(y, yn), fp2_mul(xd2, xd)), yd2);
+  if (fp2_is_zero(r.z)) return jac_infinity<Fp2>();
+  return r;
+}
+
+// One out-of-line copy of each chain (called for A, U, C and RS on G2, RP on G1):
+// the double-and-add body is large, so the kernel keeps a single instance of it.
+__device__ __noinline__ void g2_mul_u64(G2J* out, const G2J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
+__device__ __noinline__ void g1_mul_u64(G1J* out, const G1J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
+// out-of-line general addition for the handful of additions outside the chains
+__device__ __noinline__ void g2_add(G2J* out, const G2J* a, const G2J* b) { *out = jac_add(*a, *b); }
+
+__device__ G2J g2_add_v(const G2J& a, const G2J& b) {
+  G2J r;
+  g2_add(&r, &a, &b);
+  return r;
+}
+
+__device__ G2J g2_mul_x(const G2J& p) {  // [x]P = -[|x|]P
+  G2J r;
+  g2_mul_u64(&r, &p, (uint64_t)BLS_X_ABS);
+  return jac_neg(r);
+}
+
+__device__ void store_one(Fp12* f) {
+  Fp* d = reinterpret_cast<Fp*>(f);
+  d[0] = c_one();
+#pragma unroll
+  for (int k = 1; k < 12; ++k) d[k] = fp_zero();
+}
+
+__device__ void flag_exact(const PipeBufs& b, uint32_t i) {
+  b.set_flag[i] = 1u;
+  atomicAdd(b.flag_count, 1u);
+}
+
+}  // namespace
+
+// the set needs no chains: its request errors on its status (f_i = 1), or the exact
+// path takes it (infinity signature, SSWU flag from k_pre)
+__device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
+  return b.pk_status[i] != BLS_OK || b.sig_status[i] != BLS_OK || jac_is_inf(b.pk[i]) || b.sig[i].inf ||
+         b.set_flag[i];
+}
+
+// Four roles per set, one wavefront per (role, 64 sets), so a call of n sets runs
+// 4 n / 64 wavefronts and its latency is the longest chain, not their sum:
+//   role 0  H = clear_cofactor(iso(q0) + iso(q1)) -> HQ (affine)   ~2.9k Fp products
+//   role 1  psi(sig) == [x] sig                                     ~1.3k
+//   role 2  RS = [r] sig                                            ~1.9k
+//   role 3  RP = [r] pk                                             ~1.0k
+// Results that decide the set's fate go to b.chain_st (k_chain_done reads them).
+__global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks_per_role) {
+  const uint32_t role = blockIdx.x / blocks_per_role;
+  const uint32_t i = (blockIdx.x % blocks_per_role) * BLS_BLOCK + threadIdx.x;
+  if (i >= b.n_sets || chain_skip(b, i)) return;
+  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
+  if (role == 0) {
+    // H = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P), P = iso(q0) + iso(q1)
+    const Fp* q = b.q + 8ull * i;
+    const G2J P =
+        g2_add_v(iso_map_jac(Fp2{q[0], q[1]}, Fp2{q[2], q[3]}), iso_map_jac(Fp2{q[4], q[5]}, Fp2{q[6], q[7]}));
+    const G2J t1 = g2_mul_x(P);
+    const G2J t2 = g2_psi(P);
+    G2J t3 = g2_psi(g2_psi(jac_dbl(P)));
+    t3 = g2_add_v(t3, jac_neg(t2));
+    t3 = g2_add_v(t3, g2_mul_x(g2_add_v(t1, t2)));
+    t3 = g2_add_v(t3, jac_neg(t1));
+    const G2J Hj = g2_add_v(t3, jac_neg(P));
+    if (jac_is_inf(Hj)) {
+      atomicOr(&b.chain_st[i], CHAIN_ST_H_INF);
+      return;
+    }
+    // HQ = affine H: one Fp inversion (binary GCD) of N(Z)
+    const Fp ni = fp_inv_gcd(fp_add(fp_sqr(Hj.z.c0), fp_sqr(Hj.z.c1)));
+    const Fp2 zi = Fp2{fp_mul(Hj.z.c0, ni), fp_neg(fp_mul(Hj.z.c1, ni))};
+    const Fp2 zi2 = fp2_sqr(zi);
+    const Fp2 hx = fp2_mul(Hj.x, zi2);
+    const Fp2 hy = fp2_mul(Hj.y, fp2_mul(zi2, zi));
+    o[CH_HQ + 0] = hx.c0;
+    o[CH_HQ + 1] = hx.c1;
+    o[CH_HQ + 2] = hy.c0;
+    o[CH_HQ + 3] = hy.c1;
+  } else if (role == 1) {
+    const G2J sj = jac_from_aff(b.sig[i]);
+    if (!jac_eq(g2_psi(sj), g2_mul_x(sj))) atomicOr(&b.chain_st[i], CHAIN_ST_NOT_IN_G2);
+  } else if (role == 2) {
+    const G2J sj = jac_from_aff(b.sig[i]);
+    G2J RS;
+    g2_mul_u64(&RS, &sj, set_scalar(b.seed, b.scalar_base + i));
+    o[CH_RS + 0] = RS.x.c0;
+    o[CH_RS + 1] = RS.x.c1;
+    o[CH_RS + 2] = RS.y.c0;
+    o[CH_RS + 3] = RS.y.c1;
+    o[CH_RS + 4] = RS.z.c0;
+    o[CH_RS + 5] = RS.z.c1;
+  } else {
+    G1J RP;
+    const G1J pk = b.pk[i];
+    g1_mul_u64(&RP, &pk, set_scalar(b.seed, b.scalar_base + i));
+    if (jac_is_inf(RP)) {
+      atomicOr(&b.chain_st[i], CHAIN_ST_RP_INF);
+      return;
+    }
+    o[CH_RP + 0] = RP.x;
+    o[CH_RP + 1] = RP.y;
+    o[CH_RP + 2] = RP.z;
+  }
+}
+
+// One lane per set after the four roles: the set's fate.
+__global__ __launch_bounds__(BLS_BLOCK) void k_chain_done(PipeBufs b) {
+  const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (i >= b.n_sets) return;
+  b.chain_live[i] = 0u;
+  if (b.pk_status[i] != BLS_OK || b.sig_status[i] != BLS_OK || jac_is_inf(b.pk[i])) {
+    store_one(&b.f[i]);  // the request errors on its status; f_i is unused
+    return;
+  }
+  if (b.sig[i].inf || b.set_flag[i]) {
+    flag_exact(b, i);
+    return;
+  }
+  const uint32_t st = b.chain_st[i];
+  if (st & CHAIN_ST_NOT_IN_G2) {  // psi(sig) != [x] sig: Signature.fromBytes(.., validate) throws
+    b.sig_status[i] = BLS_POINT_NOT_IN_GROUP;
+    store_one(&b.f[i]);
+    return;
+  }
+  if (st) {  // H = O or [r] pk = O: the exact path's complete formulas decide
+    flag_exact(b, i);
+    return;
+  }
+  b.chain_live[i] = 1u;
+}
+
+hipError_t launch_k_chain(const PipeBufs& b, hipStream_t s) {
+  const uint32_t nb = bls_grid_for(b.n_sets);
+  hipError_t e = hipMemsetAsync(b.chain_st, 0, sizeof(uint32_t) * b.n_sets, s);
+  if (e != hipSuccess) return e;
+  k_chain<<<4 * nb, BLS_BLOCK, 0, s>>>(b, nb);
+  k_chain_done<<<nb, BLS_BLOCK, 0, s>>>(b);
+  return hipGetLastError();
+}

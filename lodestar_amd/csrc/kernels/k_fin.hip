@@ -4,8 +4,9 @@
 //                 (worker.ts:56-88: random-scalar batch over the chunk's sets)
 //   k_indiv_coop  one task per request verified on its own
 //                 (failed chunks' requests and non-batchable requests, worker.ts:91-98)
-// Task: F = prod f_i (each f_i already holds both pairings of its set, k_pset),
-//       verdict = (FE(F) == 1).
+// Task: F = prod f_i, verdict = (FE(F) == 1).  Each f_i holds both pairings of its
+// set (k_pset), or (aggregated-signature path, b.sigagg) only e(r pk, H) and the task
+// multiplies in its group's virtual set ML(-g1, sum r_i sig_i).
 #include "../launchers.hpp"
 #include "../bls/coop.hpp"
 
@@ -55,6 +56,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv e
     const uint32_t r = b.chunk_reqs[k];
     for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, first);
   }
+  if (b.sigagg) fin_accumulate_set(b, env, sh, b.n_sets + c, first);  // ML(-g1, sum of the chunk's r sig)
   bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.chunk_ok[c] = ok ? 1 : 0;
 }
@@ -72,6 +74,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
   bool first = true;
   const uint32_t stride = b.fold > 1 ? b.fold : 1u;  // f's pre-multiplied in groups by k_fold
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set(b, env, sh, i, first);
+  if (b.sigagg) fin_accumulate_set(b, env, sh, b.n_sets + b.n_chunks + t, first);  // the request's own sum
   bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.indiv_verdict[t] = ok ? 1 : 0;
 }

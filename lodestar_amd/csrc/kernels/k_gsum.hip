@@ -1,0 +1,94 @@
+// Signature side of the aggregated-signature path (after k_chain.hip):
+//
+//   k_gsum  segmented sums of RS_i = [r_i] sig_i, one lane per segment of at most
+//           GSUM_FAN points (G2 Jacobian, complete additions).  Level 0 reads the
+//           sets listed in b.gsets (group-major) from b.chain, skipping sets that are
+//           not live (error status, outside G2, finished by the exact path, whose f_i
+//           already holds its own signature pairing); each later level sums the
+//           previous level's outputs.  Segments never straddle groups, so after the
+//           last level there is one sum per group (bls_gpu.hip plan_gsum).
+//   k_vset  one lane per group: the sum becomes the group's virtual set for k_mln,
+//           HQ = affine(sum) (one inversion), RP = -g1, so that its f is
+//           ML(-g1, sum r_i sig_i) -- the single signature Miller loop blst's
+//           verifyMultipleSignatures runs per batch.  A sum at infinity gives f = 1.
+#define BLS_FP_INLINE 1
+#include "../launchers.hpp"
+
+using namespace bls;
+
+namespace {
+
+__device__ __noinline__ void g2_add_p(G2J* acc, const G2J* p) { *acc = jac_add(*acc, *p); }
+
+__device__ G2J chain_rs(const PipeBufs& b, uint32_t i) {
+  const Fp* c = b.chain + (size_t)CHAIN_WORDS * i + CH_RS;
+  G2J p;
+  p.x = Fp2{c[0], c[1]};
+  p.y = Fp2{c[2], c[3]};
+  p.z = Fp2{c[4], c[5]};
+  return p;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_gsum(PipeBufs b, const uint32_t* seg, uint32_t n_seg, const G2J* in,
+                                                    G2J* out) {
+  const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (k >= n_seg) return;
+  const uint32_t beg = seg[2 * k], end = seg[2 * k + 1];
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t j = beg; j < end; ++j) {
+    G2J p;
+    if (in) {
+      p = in[j];
+    } else {
+      const uint32_t i = b.gsets[j];
+      if (!b.chain_live[i]) continue;
+      p = chain_rs(b, i);
+    }
+    g2_add_p(&acc, &p);
+  }
+  out[k] = acc;
+}
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_vset(PipeBufs b, const G2J* sums, uint32_t n_groups, uint32_t vbase) {
+  const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (g >= n_groups) return;
+  const uint32_t v = vbase + g;
+  const G2J s = sums[g];
+  if (jac_is_inf(s)) {  // nothing to pair (every set errored, or the sum cancels): f = 1
+    b.chain_live[v] = 0u;
+    Fp* d = reinterpret_cast<Fp*>(&b.f[v]);
+    d[0] = c_one();
+#pragma unroll
+    for (int k = 1; k < 12; ++k) d[k] = fp_zero();
+    return;
+  }
+  const Fp ni = fp_inv_gcd(fp_add(fp_sqr(s.z.c0), fp_sqr(s.z.c1)));
+  const Fp2 zi = Fp2{fp_mul(s.z.c0, ni), fp_neg(fp_mul(s.z.c1, ni))};
+  const Fp2 zi2 = fp2_sqr(zi);
+  const Fp2 x = fp2_mul(s.x, zi2);
+  const Fp2 y = fp2_mul(s.y, fp2_mul(zi2, zi));
+  Fp* o = b.chain + (size_t)CHAIN_WORDS * v;
+  o[CH_HQ + 0] = x.c0;
+  o[CH_HQ + 1] = x.c1;
+  o[CH_HQ + 2] = y.c0;
+  o[CH_HQ + 3] = y.c1;
+  o[CH_RP + 0] = c_g1_x();
+  o[CH_RP + 1] = c_g1_negy();
+  o[CH_RP + 2] = c_one();
+  b.chain_live[v] = 1u;
+}
+
+hipError_t launch_k_gsum(const PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const G2J* in, G2J* out,
+                         hipStream_t s) {
+  if (n_seg == 0) return hipSuccess;
+  k_gsum<<<bls_grid_for(n_seg), BLS_BLOCK, 0, s>>>(b, seg, n_seg, in, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_k_vset(const PipeBufs& b, const G2J* sums, uint32_t n_groups, uint32_t vbase, hipStream_t s) {
+  if (n_groups == 0) return hipSuccess;
+  k_vset<<<bls_grid_for(n_groups), BLS_BLOCK, 0, s>>>(b, sums, n_groups, vbase);
+  return hipGetLastError();
+}

@@ -204,6 +204,45 @@ __global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
       reinterpret_cast<Fp*>(&b.f[i0 + s])[lane] = coop_get(sh.frame, PSN_SLOTS * s + PS_F + lane);
 }
 
+// Single-pair Miller loops of the aggregated-signature path (after k_chain.hip and
+// k_gsum.hip's k_vset): S sets per wavefront, f_i = ML(RP_i, HQ_i) for the sets in
+// [first, first + count) that are live (real sets: RP = [r] pk, HQ = H(m); a group's
+// virtual set: RP = -g1, HQ = sum r sig).  Frame per packed set s (tools/gen_pset.py
+// build_ml1, ML1_SLOTS = 19): RP at 19 s + 0..2, HQ at 19 s + 3..6, F at 19 s + 7..18.
+// A part of the wave with no live set borrows the first live set's inputs.
+enum : int { ML1_SLOTS = 19, ML1_RP = 0, ML1_HQ = 3, ML1_F = 7 };
+
+template <int S, class Lds>
+__global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count) {
+  __shared__ Lds sh;
+  const CoopProg& ml = S == 1 ? env.ml1_1 : env.ml1_4;
+  const int lane = threadIdx.x;
+  const uint32_t i0 = first + (uint32_t)S * blockIdx.x, end = first + count;
+  bool live[S];
+  int first_live = -1;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const uint32_t i = i0 + s;
+    live[s] = i < end && b.chain_live[i];
+    if (live[s] && first_live < 0) first_live = s;
+  }
+  if (first_live < 0) return;
+  coop_stage_consts(env, sh.cbank);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const uint32_t i = i0 + (live[s] ? s : first_live), o = ML1_SLOTS * s;
+    const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
+    if (lane < 3) lds_store_fp(sh.frame, o + ML1_RP + lane, ch[CH_RP + lane]);
+    else if (lane < 7) lds_store_fp(sh.frame, o + ML1_HQ + lane - 3, ch[CH_HQ + lane - 3]);
+  }
+  if (lane == 0) sh.flag = 0;
+  __syncthreads();
+  coop_run(env, ml, sh.frame, sh.cbank, &sh.flag);
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (live[s] && lane < 12) reinterpret_cast<Fp*>(&b.f[i0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);
+}
+
 // Sets per wavefront for a batch: 1 for small batches (latency: one wave per set
 // spreads a small call over more SIMDs), 2 from BLS_PACK_MIN_SETS sets on
 // (throughput: the 2-set frame fits 20 KB of LDS, so two wavefronts share each SIMD;
@@ -221,6 +260,16 @@ static uint32_t pack_for(uint32_t n_sets) {
   }();
   if (forced >= 1 && forced <= 3) return (uint32_t)forced;
   return n_sets >= min_sets ? 2u : 1u;
+}
+
+hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  if (env.ml1_4.n > 0 && b.pack != 1) {
+    k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count);
+  } else {
+    k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env, first, count);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_k_pset(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {

@@ -18,6 +18,12 @@ hipError_t launch_k_status(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes, hipStream_t s);
 hipError_t launch_k_pre(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_exact(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_chain(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_gsum(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const bls::G2J* in,
+                         bls::G2J* out, hipStream_t s);
+hipError_t launch_k_vset(const bls::PipeBufs& b, const bls::G2J* sums, uint32_t n_groups, uint32_t vbase,
+                         hipStream_t s);
+#define GSUM_FAN 4u  // points per k_gsum segment (a 16-set chunk: two levels of 3 additions)
 hipError_t launch_k_hash_to_g2(const uint8_t* msgs, uint32_t n, uint8_t* out192, hipStream_t s);
 hipError_t launch_k_sig_aggregate(const uint8_t* in96, uint32_t n, const uint32_t* off, uint32_t n_lists,
                                   bls::G2A* pts, int32_t* sig_codes, uint8_t* out96, int32_t* codes, hipStream_t s);
@@ -39,3 +45,5 @@ hipError_t launch_k_coop_probe(const bls::CoopEnv& env, bls::CoopProg pg, uint32
 hipError_t launch_k_fprod(const bls::Fp12* in, uint32_t n, bls::Fp12* out, int32_t* verdict,
                           const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
+hipError_t launch_k_mln(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_t first, uint32_t count,
+                        hipStream_t s);

@@ -550,3 +550,37 @@ def run_pset2(pg, consts, frame, rs, simulate, inv):
     flag |= simulate(pg["pset2_affine2"], frame, consts)
     flag |= simulate(pg["pset2_ml2"], frame, consts)
     return flag, in_group
+
+
+# ----------------------------------------------------------------------------
+# single-pair Miller loops (k_mln after k_chain, signature pairing aggregated)
+# ----------------------------------------------------------------------------
+ML1_SLOTS = 19                 # per packed set: RP 0..2 (G1 Jacobian), HQ 3..6 (affine), F 7..18
+ML1_RP, ML1_HQ, ML1_F = 0, 3, 7
+
+
+def build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1, prefix="ml1"):
+    """f_s = ML(RP_s, HQ_s) for S sets packed in one wavefront (set s at slot offset
+    ML1_SLOTS * s): one pair per set, the signature side of the batch equation is
+    summed over the group (sum r_i sig_i) and paired once per group as a further
+    "set" with RP = -g1 (bls_gpu.hip, kernels/k_chain.hip)."""
+    c = Circuit(f"{prefix}_{S}", consts)
+    t = T(c)
+    for s in range(S):
+        o = ML1_SLOTS * s
+        c.zset = s
+        X, Y, Z = (Circuit.inp(o + ML1_RP + k) for k in range(3))
+        pz3 = c.mat(c.mul(c.mat(c.mul(Z, Z)), Z))
+        pxz = c.mat(c.mul(X, Z))
+        f = miller_loop_multi(t, [(t.f2(o + ML1_HQ), t.f2(o + ML1_HQ + 2), pxz, Y, pz3)], miller_dbl, miller_add,
+                              X_ABS)
+        for k in range(2):
+            for j in range(3):
+                for i in range(2):
+                    c.out(o + ML1_F + 6 * k + 2 * j + i, f[k][j][i])
+    c.zset = 0
+    live = set()
+    for s in range(S):
+        o = ML1_SLOTS * s
+        live |= set(range(o, o + ML1_F))
+    return schedule(c, FRAME, live)
