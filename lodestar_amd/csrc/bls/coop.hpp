@@ -79,8 +79,8 @@ struct CoopEnv {
       pset_affine2, pset_ml2;
   CoopPsetN packed[2];  // [0]: 2 sets per wavefront, [1]: 3 sets
   // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln):
-  // 1 set per wavefront (COOP_FRAME), 4 sets (COOP_FRAME2)
-  CoopProg ml1_1, ml1_4;
+  // 1 or 2 sets per wavefront (COOP_FRAME), 4 sets (COOP_FRAME2)
+  CoopProg ml1_1, ml1_2, ml1_4;
 };
 
 // fin frame registers

@@ -215,7 +215,7 @@ enum : int { ML1_SLOTS = 19, ML1_RP = 0, ML1_HQ = 3, ML1_F = 7 };
 template <int S, class Lds>
 __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count) {
   __shared__ Lds sh;
-  const CoopProg& ml = S == 1 ? env.ml1_1 : env.ml1_4;
+  const CoopProg& ml = S == 1 ? env.ml1_1 : (S == 2 ? env.ml1_2 : env.ml1_4);
   const int lane = threadIdx.x;
   const uint32_t i0 = first + (uint32_t)S * blockIdx.x, end = first + count;
   bool live[S];
@@ -262,10 +262,24 @@ static uint32_t pack_for(uint32_t n_sets) {
   return n_sets >= min_sets ? 2u : 1u;
 }
 
+// Sets per wavefront of k_mln: BLS_DEBUG_PACK(1 / 2) or $BLS_ML_PACK (1, 2, 4); default 4
+static uint32_t ml_pack(const PipeBufs& b) {
+  static const int env = [] {
+    const char* e = getenv("BLS_ML_PACK");
+    return e ? atoi(e) : 0;
+  }();
+  if (b.pack == 1 || b.pack == 2) return b.pack;
+  if (env == 1 || env == 2 || env == 4) return (uint32_t)env;
+  return 4u;
+}
+
 hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  if (env.ml1_4.n > 0 && b.pack != 1) {
+  const uint32_t S = ml_pack(b);
+  if (S == 4 && env.ml1_4.n > 0) {
     k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count);
+  } else if (S == 2 && env.ml1_2.n > 0) {
+    k_mln<2, CoopLds><<<(count + 1) / 2, COOP_LANES, 0, s>>>(b, env, first, count);
   } else {
     k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env, first, count);
   }

@@ -41,7 +41,7 @@ hipError_t launch_k_fold(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStr
 #define BLS_FOLD 16u  // sets per k_fold group
 hipError_t launch_k_coop_probe(const bls::CoopEnv& env, bls::CoopProg pg, uint32_t blocks, uint32_t reps,
                                uint32_t* sink, uint64_t* stamps, hipStream_t s);
-#define FPROD_FAN 64u
+#define FPROD_FAN 16u
 hipError_t launch_k_fprod(const bls::Fp12* in, uint32_t n, bls::Fp12* out, int32_t* verdict,
                           const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);

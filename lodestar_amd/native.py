@@ -273,8 +273,12 @@ class GpuContext:
         self._check(self.lib.bls_gpu_sk_to_pk(self._h, _ptr(s), n, _ptr(out)), "bls_gpu_sk_to_pk")
         return out[: 48 * n].reshape(n, 48)
 
+    # ORed into every set_debug_flags call (tests run a whole module once per path)
+    base_debug_flags = 0
+
     def set_debug_flags(self, flags: int) -> None:
-        self._check(self.lib.bls_gpu_set_debug_flags(self._h, flags), "bls_gpu_set_debug_flags")
+        self._check(self.lib.bls_gpu_set_debug_flags(self._h, flags | self.base_debug_flags),
+                    "bls_gpu_set_debug_flags")
 
     def mad_peak(self) -> tuple[float, float]:
         """Measured v_mad_u64_u32 rate (MAD/s) and the probe's duration (ms)."""

@@ -27,6 +27,20 @@ from lodestar_amd.native import pack_requests
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, scope="module", params=["pset", "sigagg"])
+def verify_path(request, gpu):
+    """Every test of this module runs on both per-set paths: the all-cooperative k_pset
+    and the aggregated-signature path (k_chain + k_gsum / k_vset + single-pair k_mln),
+    whatever the call size would pick."""
+    from lodestar_amd._abi import DEBUG_SIGAGG_OFF, DEBUG_SIGAGG_ON
+
+    gpu.base_debug_flags = DEBUG_SIGAGG_ON if request.param == "sigagg" else DEBUG_SIGAGG_OFF
+    gpu.set_debug_flags(0)
+    yield request.param
+    gpu.base_debug_flags = 0
+    gpu.set_debug_flags(0)
+
+
 def _h(b: bytes) -> bytes:
     return hashlib.sha256(b).digest()
 
@@ -152,6 +166,36 @@ def test_verify_edge_cases(gpu, oracle, table):
     ]
     v, _ = gpu.verify_packed(pack_requests(reqs))
     assert list(v) == [-CODE_EMPTY_SET, 0, -CODE_EMPTY_AGGREGATE, 0, 1]
+
+
+def test_large_groups_multi_level_sums(gpu, oracle, table):
+    """Requests of many sets: one batchable request of 300 sets (its chunk's r sig sum
+    runs several k_gsum levels), non-batchable requests of 70 and 2 sets (individual
+    groups summed in the individual pass), one of them with an invalid set; verdicts
+    with the merged check on and off."""
+    from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK
+
+    n = 300
+    sks = _keys(oracle, 100)
+    msgs = [_h(b"big-%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 100] for i in range(n)), b"".join(msgs))
+    sets = [([i % 100], msgs[i], sigs[i].tobytes()) for i in range(n)]
+    bad70 = list(sets[100:170])
+    bad70[37] = (bad70[37][0], _h(b"tampered"), bad70[37][2])
+    reqs = [(True, sets), (False, sets[:70]), (False, bad70), (False, sets[200:202]), (True, sets[250:300])]
+    for flags in (0, DEBUG_NO_MERGED_CHECK):
+        try:
+            gpu.set_debug_flags(flags)
+            v, st = gpu.verify_packed(pack_requests(reqs))
+        finally:
+            gpu.set_debug_flags(0)
+        assert list(v) == [1, 1, 0, 1, 1], flags
+        assert st.n_individual == 3
+    # the same with the big request invalid: its chunk fails, it is retried on its own
+    bad = list(sets)
+    bad[299] = (bad[299][0], bad[299][1], sets[0][2])
+    v, st = gpu.verify_packed(pack_requests([(True, bad), (True, sets[250:300])]))
+    assert list(v) == [0, 1] and st.batch_retries == 1 and st.n_individual == 2
 
 
 def test_verify_aggregate_sets(gpu, oracle, table):

@@ -485,9 +485,10 @@ def build_all():
                                  S=2, prefix="pset2")
     progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME3, psi, iso, G1X, G1Y,
                                  S=3, prefix="pset3")
-    # single-pair Miller loops of the aggregated-signature path (k_mln): 1 set per
-    # wavefront in the 256-slot frame, 4 sets in the 380-slot frame (2 waves / SIMD)
+    # single-pair Miller loops of the aggregated-signature path (k_mln): 1 or 2 sets
+    # per wavefront in the 256-slot frame, 4 sets in the 380-slot frame (2 waves / SIMD)
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1))
+    progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=2))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, S=4))
     return progs, consts
 
