@@ -60,7 +60,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
     os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-STAGE_NAMES = ["h2d", "k_pk", "k_pre", "k_pset", "k_exact", "-", "k_status+k_chunk", "k_indiv"]
+STAGE_NAMES = ["h2d", "k_pk", "k_pre", "per_set", "k_exact", "-", "k_status+k_chunk", "k_indiv"]
 X_ABS = 0xD201000000010000
 MADS_PER_FPM = 288   # 12x12 limb products + 12x12 reduction products per Montgomery product
 METRIC = "BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch"
@@ -98,10 +98,44 @@ def pset_products_per_set(S: int) -> float:
     return n / S
 
 
+SIGAGG_MIN_SETS = 512   # bls_gpu.hip use_sigagg: the aggregated-signature path from this call size on
+
+
+def sigagg_of(n_sets: int) -> bool:
+    e = os.environ.get("BLS_SIGAGG")
+    return (e != "0") if e not in (None, "") else n_sets >= SIGAGG_MIN_SETS
+
+
+def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
+    """Fp products the GPU executes per set for a cfg2 call of n_sets single-set
+    batchable requests, every kernel of the call (k_pre, the per-set path, the chunks'
+    signature sums and Miller loops, the merged check's product tree and final
+    exponentiation): stage counts from lodestar_amd/_native/work_model.json
+    (tools/work_model.cpp, host-compiled product math with the Fp-product counter) and
+    the cooperative programs' MUL ops (coop_programs.json)."""
+    pg = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
+    wm = json.loads((ROOT / "lodestar_amd" / "_native" / "work_model.json").read_text())
+    m = {k: v["mul_ops"] for k, v in pg.items()}
+    chunks = max(1, n_sets // reqs_per_chunk)
+    merged = (n_sets + chunks - 1) * m["fin_fmul"] + m["fin_fe1"] + m["fin_fe2"]
+    if sigagg_of(n_sets):
+        ml = m["ml1_4"] / 4
+        per = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"] + ml
+               + chunks / n_sets * (ml + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"] + merged / n_sets)
+        return per, ("k_pre %.0f + k_chain %.0f + k_mln %.0f + chunk sums/ML %.0f + merged check %.0f" %
+                     (wm["k_pre"], wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"], ml,
+                      chunks / n_sets * (ml + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"],
+                      merged / n_sets))
+    S = pack_of(n_sets)
+    ps = pset_products_per_set(S)
+    return wm["k_pre"] + ps + merged / n_sets, "k_pre %.0f + k_pset %.0f + merged check %.0f" % (
+        wm["k_pre"], ps, merged / n_sets)
+
+
 def pmc_summary(kernel_prefix: str):
     """The newest committed SQ-counter summary for the kernel (profiles/r*_pmc_*.json,
     rocprofv3 --pmc passes; tools/pmc_summary.py), or None."""
-    files = sorted((ROOT / "profiles").glob("r*_pmc_k_pset*.json"), key=lambda p: p.name)
+    files = sorted((ROOT / "profiles").glob("r*_pmc_k_*.json"), key=lambda p: p.name)
     for p in reversed(files):
         d = json.loads(p.read_text())
         for k, v in d.get("kernels", {}).items():
@@ -409,23 +443,28 @@ def main() -> None:
         # the timed region: sets/s per GPU x its MADs per set (launches overlap across the
         # in-flight streams, so wall time per launch = timed region / launches); the solo
         # launch time of one call is reported beside it.
-        fpm_set = pset_products_per_set(S)
+        fpm_set, fpm_note = work_per_set(args.sets)
         mad_set = fpm_set * MADS_PER_FPM
+        agg = sigagg_of(args.sets)
         solo = []
         for _ in range(5):
             _, st = gpu.verify_packed(batch)
-            solo.append(st.stage_ms[STAGE_NAMES.index("k_pset")])
+            solo.append(st.stage_ms[STAGE_NAMES.index("per_set")])
         solo_ms = statistics.median(solo)
         peak_rate, _ = gpu.mad_peak()
         peak = peak_rate / 1e12
         per_gpu = value / world
         achieved = per_gpu * mad_set / 1e12
         if rank == 0:
-            pmc = pmc_summary(f"k_psetn<{S}" if S > 1 else "k_pset")
-            roof = {"bound": "valu", "kernel": f"k_psetn<{S}>" if S > 1 else "k_pset", "achieved": round(achieved, 4),
+            kern = "k_mln<4>" if agg else (f"k_psetn<{S}" if S > 1 else "k_pset")
+            pmc = pmc_summary(kern.rstrip(">") if agg else kern)
+            roof = {"bound": "valu",
+                    "kernel": ("every kernel of the call; dominant: k_mln<4> (cooperative Miller loops) and k_chain "
+                               "(scalar chains, one lane per set)") if agg else kern,
+                    "achieved": round(achieved, 4),
                     "peak": round(peak, 3), "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5),
                     "traffic": None,
-                    "work": f"{fpm_set:.0f} Fp products/set x {MADS_PER_FPM} MAD ({S} sets per wavefront) x "
+                    "work": f"{fpm_set:.0f} Fp products/set ({fpm_note}) x {MADS_PER_FPM} MAD x "
                             f"{per_gpu:.0f} sets/s per GPU (timed region; launch wall time = region / launches)",
                     "solo_launch_ms": round(solo_ms, 3),
                     "solo_achieved": round(args.sets * mad_set / (solo_ms * 1e-3) / 1e12, 4),

@@ -67,10 +67,27 @@ def build_coop_tables(verbose: bool = True) -> Path:
     return out
 
 
+def build_work_model(verbose: bool = True) -> Path:
+    """Fp products per stage (tools/work_model.py), regenerated when the math changes:
+    the algorithmic work bench.py prices its roofline with."""
+    out = OUT_DIR / "work_model.json"
+    key = hashlib.sha256(_headers_digest().encode() + (ROOT / "tools" / "work_model.cpp").read_bytes()).hexdigest()
+    stamp = OUT_DIR / ".work_stamp"
+    if out.exists() and stamp.exists() and stamp.read_text() == key:
+        return out
+    sys.path.insert(0, str(ROOT / "tools"))
+    import work_model
+
+    work_model.build(out, verbose)
+    stamp.write_text(key)
+    return out
+
+
 def build(jobs: int | None = None, verbose: bool = True) -> Path:
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
     build_coop_tables(verbose)
+    build_work_model(verbose)
     hdr = _headers_digest()
     srcs = sources()
     jobs = jobs or min(len(srcs), os.cpu_count() or 4)

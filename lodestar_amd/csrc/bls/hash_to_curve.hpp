@@ -245,6 +245,33 @@ BLS_HD G2A iso_map_g2(const G2A& p) {
   return r;
 }
 
+// 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3) into Jacobian coordinates:
+// x = xn / xd, y = y' yn / yd  ->  Z = xd yd, X = xn xd yd^2, Y = y' yn xd^3 yd^2.
+// A zero denominator gives Z = 0, the point at infinity (iso_map_g2's convention).
+BLS_HD G2J iso_map_jac(const Fp2& x, const Fp2& y) {
+  Fp2 xn = c_iso_xnum_3();
+  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_2());
+  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_1());
+  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_0());
+  Fp2 xd = fp2_add(x, c_iso_xden_1());
+  xd = fp2_add(fp2_mul(xd, x), c_iso_xden_0());
+  Fp2 yn = c_iso_ynum_3();
+  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_2());
+  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_1());
+  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_0());
+  Fp2 yd = fp2_add(x, c_iso_yden_2());
+  yd = fp2_add(fp2_mul(yd, x), c_iso_yden_1());
+  yd = fp2_add(fp2_mul(yd, x), c_iso_yden_0());
+  const Fp2 yd2 = fp2_sqr(yd);
+  const Fp2 xd2 = fp2_sqr(xd);
+  G2J r;
+  r.z = fp2_mul(xd, yd);
+  r.x = fp2_mul(fp2_mul(xn, xd), yd2);
+  r.y = fp2_mul(fp2_mul(fp2_mul(y, yn), fp2_mul(xd2, xd)), yd2);
+  if (fp2_is_zero(r.z)) return jac_infinity<Fp2>();
+  return r;
+}
+
 // hash_to_G2 of a 32-byte message (8 big-endian words), Jacobian output
 BLS_HD G2J hash_to_g2_jac(const uint32_t msg[8]) {
   Fp2 u0, u1;

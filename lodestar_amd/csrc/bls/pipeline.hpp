@@ -35,7 +35,6 @@ namespace bls {
 // A group's virtual set (index n_sets + chunk, n_sets + n_chunks + individual
 // request) holds HQ = affine(sum of the group's RS) and RP = -g1.
 enum : int { CH_HQ = 0, CH_RP = 4, CH_RS = 7, CHAIN_WORDS = 13 };
-enum : uint32_t { CHAIN_ST_NOT_IN_G2 = 1u, CHAIN_ST_H_INF = 2u, CHAIN_ST_RP_INF = 4u };
 
 struct PipeBufs {
   uint32_t n_sets, n_reqs, n_chunks, n_indiv;
@@ -89,7 +88,7 @@ struct PipeBufs {
   uint32_t sigagg;
   Fp* chain;             // (n_sets + virtual) * CHAIN_WORDS (layout: CH_*)
   uint32_t* chain_live;  // n_sets + virtual: 1 = k_mln runs this set's Miller loop
-  uint32_t* chain_st;    // n_sets: CHAIN_ST_* bits from k_chain's roles
+  uint8_t* chain_st;     // 4 n_sets: per set, role 0 H = O, role 1 outside G2, role 3 [r] pk = O
   const uint32_t* gsets; // set indices of the groups being summed, group-major (k_gsum level 0)
   uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
   uint32_t* flag_count;  // 1 word: sets flagged by the cooperative kernel (GPU path)

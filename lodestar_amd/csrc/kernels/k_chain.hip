@@ -31,37 +31,22 @@ using namespace bls;
 
 namespace {
 
-// 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3) into Jacobian coordinates:
-// x = xn / xd, y = y' yn / yd  ->  Z = xd yd, X = xn xd yd^2, Y = y' yn xd^3 yd^2.
-// A zero denominator gives Z = 0, the point at infinity (iso_map_g2's convention).
-__device__ G2J iso_map_jac(const Fp2& x, const Fp2& y) {
-  Fp2 xn = c_iso_xnum_3();
-  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_2());
-  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_1());
-  xn = fp2_add(fp2_mul(xn, x), c_iso_xnum_0());
-  Fp2 xd = fp2_add(x, c_iso_xden_1());
-  xd = fp2_add(fp2_mul(xd, x), c_iso_xden_0());
-  Fp2 yn = c_iso_ynum_3();
-  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_2());
-  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_1());
-  yn = fp2_add(fp2_mul(yn, x), c_iso_ynum_0());
-  Fp2 yd = fp2_add(x, c_iso_yden_2());
-  yd = fp2_add(fp2_mul(yd, x), c_iso_yden_1());
-  yd = fp2_add(fp2_mul(yd, x), c_iso_yden_0());
-  const Fp2 yd2 = fp2_sqr(yd);
-  const Fp2 xd2 = fp2_sqr(xd);
+// out-of-line isogeny (bls/hash_to_curve.hpp iso_map_jac), called twice per set
+__device__ __noinline__ void iso_jac_nl(G2J* out, const Fp* q) { *out = iso_map_jac(Fp2{q[0], q[1]}, Fp2{q[2], q[3]}); }
+
+__device__ G2J iso_jac(const Fp* q) {
   G2J r;
-  r.z = fp2_mul(xd, yd);
-  r.x = fp2_mul(fp2_mul(xn, xd), yd2);
-  r.y = fp2_mul(fp2_mul(fp2_mul(y, yn), fp2_mul(xd2, xd)), yd2);
-  if (fp2_is_zero(r.z)) return jac_infinity<Fp2>();
+  iso_jac_nl(&r, q);
   return r;
 }
 
-// One out-of-line copy of each chain (called for A, U, C and RS on G2, RP on G1):
+// One out-of-line copy of each chain (A and U on a Jacobian G2 base, C and RS on the
+// affine signature, RP on G1):
 // the double-and-add body is large, so the kernel keeps a single instance of it.
 __device__ __noinline__ void g2_mul_u64(G2J* out, const G2J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
 __device__ __noinline__ void g1_mul_u64(G1J* out, const G1J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
+// affine base (the signature): mixed additions
+__device__ __noinline__ void g2_mul_aff(G2J* out, const G2A* in, uint64_t k) { *out = aff_mul_u64(*in, k); }
 // out-of-line general addition for the handful of additions outside the chains
 __device__ __noinline__ void g2_add(G2J* out, const G2J* a, const G2J* b) { *out = jac_add(*a, *b); }
 
@@ -101,10 +86,11 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
 // Four roles per set, one wavefront per (role, 64 sets), so a call of n sets runs
 // 4 n / 64 wavefronts and its latency is the longest chain, not their sum:
 //   role 0  H = clear_cofactor(iso(q0) + iso(q1)) -> HQ (affine)   ~2.9k Fp products
-//   role 1  psi(sig) == [x] sig                                     ~1.3k
+//   role 1  psi(sig) == [x] sig                                     ~1.2k
 //   role 2  RS = [r] sig                                            ~1.9k
 //   role 3  RP = [r] pk                                             ~1.0k
-// Results that decide the set's fate go to b.chain_st (k_chain_done reads them).
+// Results that decide the set's fate go to b.chain_st[4 i + role] (k_chain_done
+// reads them; every role that runs writes its byte, so no clearing is needed).
 __global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks_per_role) {
   const uint32_t role = blockIdx.x / blocks_per_role;
   const uint32_t i = (blockIdx.x % blocks_per_role) * BLS_BLOCK + threadIdx.x;
@@ -114,7 +100,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks
     // H = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P), P = iso(q0) + iso(q1)
     const Fp* q = b.q + 8ull * i;
     const G2J P =
-        g2_add_v(iso_map_jac(Fp2{q[0], q[1]}, Fp2{q[2], q[3]}), iso_map_jac(Fp2{q[4], q[5]}, Fp2{q[6], q[7]}));
+        g2_add_v(iso_jac(q), iso_jac(q + 4));
     const G2J t1 = g2_mul_x(P);
     const G2J t2 = g2_psi(P);
     G2J t3 = g2_psi(g2_psi(jac_dbl(P)));
@@ -122,10 +108,8 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks
     t3 = g2_add_v(t3, g2_mul_x(g2_add_v(t1, t2)));
     t3 = g2_add_v(t3, jac_neg(t1));
     const G2J Hj = g2_add_v(t3, jac_neg(P));
-    if (jac_is_inf(Hj)) {
-      atomicOr(&b.chain_st[i], CHAIN_ST_H_INF);
-      return;
-    }
+    b.chain_st[4 * i + 0] = jac_is_inf(Hj) ? 1 : 0;
+    if (jac_is_inf(Hj)) return;
     // HQ = affine H: one Fp inversion (binary GCD) of N(Z)
     const Fp ni = fp_inv_gcd(fp_add(fp_sqr(Hj.z.c0), fp_sqr(Hj.z.c1)));
     const Fp2 zi = Fp2{fp_mul(Hj.z.c0, ni), fp_neg(fp_mul(Hj.z.c1, ni))};
@@ -137,12 +121,14 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks
     o[CH_HQ + 2] = hy.c0;
     o[CH_HQ + 3] = hy.c1;
   } else if (role == 1) {
-    const G2J sj = jac_from_aff(b.sig[i]);
-    if (!jac_eq(g2_psi(sj), g2_mul_x(sj))) atomicOr(&b.chain_st[i], CHAIN_ST_NOT_IN_G2);
+    const G2A sig = b.sig[i];
+    G2J xs;
+    g2_mul_aff(&xs, &sig, (uint64_t)BLS_X_ABS);
+    b.chain_st[4 * i + 1] = jac_eq(g2_psi(jac_from_aff(sig)), jac_neg(xs)) ? 0 : 1;
   } else if (role == 2) {
-    const G2J sj = jac_from_aff(b.sig[i]);
+    const G2A sig = b.sig[i];
     G2J RS;
-    g2_mul_u64(&RS, &sj, set_scalar(b.seed, b.scalar_base + i));
+    g2_mul_aff(&RS, &sig, set_scalar(b.seed, b.scalar_base + i));
     o[CH_RS + 0] = RS.x.c0;
     o[CH_RS + 1] = RS.x.c1;
     o[CH_RS + 2] = RS.y.c0;
@@ -153,10 +139,8 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks
     G1J RP;
     const G1J pk = b.pk[i];
     g1_mul_u64(&RP, &pk, set_scalar(b.seed, b.scalar_base + i));
-    if (jac_is_inf(RP)) {
-      atomicOr(&b.chain_st[i], CHAIN_ST_RP_INF);
-      return;
-    }
+    b.chain_st[4 * i + 3] = jac_is_inf(RP) ? 1 : 0;
+    if (jac_is_inf(RP)) return;
     o[CH_RP + 0] = RP.x;
     o[CH_RP + 1] = RP.y;
     o[CH_RP + 2] = RP.z;
@@ -176,13 +160,13 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain_done(PipeBufs b) {
     flag_exact(b, i);
     return;
   }
-  const uint32_t st = b.chain_st[i];
-  if (st & CHAIN_ST_NOT_IN_G2) {  // psi(sig) != [x] sig: Signature.fromBytes(.., validate) throws
+  const uint8_t* st = b.chain_st + 4 * i;
+  if (st[1]) {  // psi(sig) != [x] sig: Signature.fromBytes(.., validate) throws
     b.sig_status[i] = BLS_POINT_NOT_IN_GROUP;
     store_one(&b.f[i]);
     return;
   }
-  if (st) {  // H = O or [r] pk = O: the exact path's complete formulas decide
+  if (st[0] || st[3]) {  // H = O or [r] pk = O: the exact path's complete formulas decide
     flag_exact(b, i);
     return;
   }
@@ -191,8 +175,6 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain_done(PipeBufs b) {
 
 hipError_t launch_k_chain(const PipeBufs& b, hipStream_t s) {
   const uint32_t nb = bls_grid_for(b.n_sets);
-  hipError_t e = hipMemsetAsync(b.chain_st, 0, sizeof(uint32_t) * b.n_sets, s);
-  if (e != hipSuccess) return e;
   k_chain<<<4 * nb, BLS_BLOCK, 0, s>>>(b, nb);
   k_chain_done<<<nb, BLS_BLOCK, 0, s>>>(b);
   return hipGetLastError();

@@ -178,6 +178,16 @@ int hs_g1_decompress(const uint8_t* pk48, uint8_t* out96) {
 }
 void hs_g2_compress(const uint8_t* g2, uint8_t* out96) { g2_compress96(rd_g2(g2), out96); }
 void hs_g1_compress(const uint8_t* g1, uint8_t* out48) { g1_compress48(rd_g1(g1), out48); }
+// the aggregated-signature path's Jacobian isogeny (k_chain role 0), as an affine point;
+// returns 0 for the point at infinity
+int hs_iso_map_jac(const uint8_t* xy192, uint8_t* out192) {
+  const G2J r = iso_map_jac(rd_fp2(xy192), rd_fp2(xy192 + 96));
+  if (jac_is_inf(r)) return 0;
+  const G2A a = jac_to_aff(r);
+  wr_fp2(a.x, out192);
+  wr_fp2(a.y, out192 + 96);
+  return 1;
+}
 void hs_g2_clear_cofactor(const uint8_t* g2, uint8_t* out192) {
   g2_serialize192(jac_to_aff(g2_clear_cofactor(jac_from_aff(rd_g2(g2)))), out192);
 }

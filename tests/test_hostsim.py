@@ -57,6 +57,26 @@ def test_sswu_fast_matches_oracle(hostsim, oracle):
     assert hostsim.hs_map_to_curve_sswu_fast(f2b((0, 0)), o) == 0
 
 
+def test_iso_map_jacobian_matches_oracle(hostsim, oracle):
+    """iso_map_jac (k_chain: the 3-isogeny into Jacobian coordinates, no inversion)
+    equals RFC 9380's rational map on SSWU outputs, and sends a zero denominator to
+    infinity like iso_map_g2."""
+    rng = random.Random(11)
+    o = _buf(192)
+    for _ in range(12):
+        u = (rng.randrange(P), rng.randrange(P))
+        q = oracle.map_to_curve_sswu(u)
+        assert hostsim.hs_iso_map_jac(f2b(q[0]) + f2b(q[1]), o) == 1
+        assert (bf2(o.raw[:96]), bf2(o.raw[96:])) == oracle.iso_map(q)
+    # a root of the x denominator (x^2 + a1 x + a0 = 0 over Fp2) maps to infinity
+    a1, a0 = oracle.ISO_XDEN[1], oracle.ISO_XDEN[0]
+    disc = oracle.f2_sub(oracle.f2_mul(a1, a1), oracle.f2_mul((4, 0), a0))
+    root = oracle.f2_sqrt(disc)
+    if root is not None:
+        x = oracle.f2_mul(oracle.f2_sub(root, a1), oracle.f2_inv((2, 0)))
+        assert hostsim.hs_iso_map_jac(f2b(x) + f2b((1, 0)), o) == 0
+
+
 def _gx1(oracle, u):
     Z = oracle.Z_SSWU
     zu2 = oracle.f2_mul(Z, oracle.f2_mul(u, u))

@@ -1,19 +1,24 @@
 #!/bin/bash
 # Round-2 measurement set on one MI355X: parity tests, the driver-shaped bench line
 # (with the CPU baseline), the N-API mode, a kernel trace with the calls overlapping,
-# and SQ / HBM counter passes over a full-occupancy launch of the per-set kernel.
-# Everything lands in gpurun_out/meas.
+# and SQ / HBM counter passes over one 8192-set call (k_chain: 512 wavefronts,
+# k_mln<4>: 2048 + 128 wavefronts, 2 per SIMD).  Everything lands in gpurun_out/meas.
+# $SKIP_TESTS=1 skips the parity tests, $SKIP_BENCH=1 the two bench lines.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/meas
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" $O/pytest_gpu.log | tail -30; exit 1; }
-tail -1 $O/pytest_gpu.log
-timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
-cat $O/bench.json
-timeout -k 10 400 python -u bench.py --mode napi --steps 8 --warmup 1 > $O/bench_napi.json 2> $O/bench_napi.err || { echo "napi bench failed"; tail -20 $O/bench_napi.err; }
-cat $O/bench_napi.json
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" $O/pytest_gpu.log | tail -30; exit 1; }
+  tail -1 $O/pytest_gpu.log
+fi
+if [ -z "$SKIP_BENCH" ]; then
+  timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
+  cat $O/bench.json
+  timeout -k 10 400 python -u bench.py --mode napi --steps 8 --warmup 1 > $O/bench_napi.json 2> $O/bench_napi.err || { echo "napi bench failed"; tail -20 $O/bench_napi.err; }
+  cat $O/bench_napi.json
+fi
 cd /tmp && export TMPDIR=/tmp
 B="python3 $R/bench.py --no-cpu-baseline --latency-runs 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace16 -o run --output-format csv -- $B --steps 4 --warmup 1 > $O/trace16.log 2>&1 || { tail -20 $O/trace16.log; exit 1; }
@@ -25,7 +30,9 @@ P5="WRITE_SIZE"
 k=0
 for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   k=$((k+1))
-  timeout -s KILL 150 rocprofv3 --pmc $P -d $O/pmc$k -o run --output-format csv -- $B --sets 4096 --inflight 1 --steps 1 --warmup 1 > $O/pmc$k.log 2>&1 || { tail -20 $O/pmc$k.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc $P -d $O/pmc$k -o run --output-format csv -- $B --sets 8192 --inflight 1 --steps 1 --warmup 1 > $O/pmc$k.log 2>&1 || { tail -20 $O/pmc$k.log; exit 1; }
 done
 cd $R
-python3 tools/pmc_summary.py $O/pmc_summary.json "one 4096-set cfg2 call (bench.py --sets 4096 --inflight 1): 2048 wavefronts of k_psetn<2> = 2 per SIMD" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5
+python3 tools/pmc_summary.py $O/pmc_summary.json "one 8192-set cfg2 call (bench.py --sets 8192 --inflight 1): k_chain 512 wavefronts (1 per SIMD, 512 registers), k_mln<4> 2176 wavefronts (2 per SIMD)" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5
+python3 tools/trace_timeline.py $(find $O/trace16 -name "*kernel_trace.csv" | head -1) k_mln > $O/timeline.txt
+cat $O/timeline.txt

@@ -1,0 +1,81 @@
+// Algorithmic work model of the aggregated-signature verify path: Fp (Montgomery)
+// products per stage, counted by running the product's own host-compiled math
+// (lodestar_amd/csrc/bls/*.hpp with BLS_COUNT_OPS) through the same curve-level calls
+// the kernels make, role by role (kernels/k_chain.hip, k_pre.hip, k_gsum.hip).  The
+// cooperative programs (Miller loops, final exponentiation) are counted from their
+// tables instead (coop_programs.json: MUL ops per program).
+//
+// Build + run: python tools/work_model.py (writes lodestar_amd/_native/work_model.json).
+#define BLS_COUNT_OPS 1
+#include <stdio.h>
+
+#include "bls/hash_to_curve.hpp"
+#include "bls/pairing.hpp"
+#include "bls/pipeline.hpp"
+
+unsigned long long bls_fpm_counter = 0;
+
+using namespace bls;
+
+static unsigned long long tick() {
+  unsigned long long c = bls_fpm_counter;
+  bls_fpm_counter = 0;
+  return c;
+}
+
+int main() {
+  const int N = 64;  // sets (messages, scalars) averaged over
+  double pre = 0, h = 0, c = 0, rs = 0, rp = 0, gadd = 0, vset = 0;
+  uint32_t seed[8] = {1, 2, 3, 4, 5, 6, 7, 8};
+  G2J prev = jac_infinity<Fp2>();
+  for (int k = 0; k < N; ++k) {
+    uint32_t w[8];
+    for (int j = 0; j < 8; ++j) w[j] = 0x9e3779b9u * (uint32_t)(k * 8 + j + 1);
+    // a signature-like G2 point and its compressed bytes, a G1 key
+    const G2A sig = hash_to_g2(w);
+    uint8_t sig96[96];
+    g2_compress96(sig, sig96);
+    const G1J pk = aff_mul_u64(g1_generator(), 1000003ull + (uint64_t)k);
+    const uint64_t r = set_scalar(seed, (uint32_t)k);
+    tick();
+    // k_pre: hash_to_field + two SSWU maps (one lane each), signature decode
+    Fp2 u0, u1, x0, y0, x1, y1;
+    hash_to_field_fp2_x2(w, u0, u1);
+    map_to_curve_sswu_fast(u0, x0, y0);
+    map_to_curve_sswu_fast(u1, x1, y1);
+    G2A dec;
+    g2_decompress96(sig96, dec);
+    pre += tick();
+    // k_chain role 0: H = clear_cofactor(iso(q0) + iso(q1)), affine
+    const G2J P = jac_add(iso_map_jac(x0, y0), iso_map_jac(x1, y1));
+    const G2J Hj = g2_clear_cofactor(P);
+    const Fp ni = fp_inv_gcd(fp_add(fp_sqr(Hj.z.c0), fp_sqr(Hj.z.c1)));
+    const Fp2 zi = Fp2{fp_mul(Hj.z.c0, ni), fp_neg(fp_mul(Hj.z.c1, ni))};
+    const Fp2 zi2 = fp2_sqr(zi);
+    (void)fp2_mul(Hj.x, zi2);
+    (void)fp2_mul(Hj.y, fp2_mul(zi2, zi));
+    h += tick();
+    // role 1: psi(sig) == [x] sig
+    (void)jac_eq(g2_psi(jac_from_aff(sig)), jac_neg(aff_mul_u64(sig, (uint64_t)BLS_X_ABS)));
+    c += tick();
+    // role 2: [r] sig (affine base, mixed additions: k_chain's g2_mul_aff)
+    const G2J RS = aff_mul_u64(sig, r);
+    rs += tick();
+    // role 3: [r] pk
+    (void)jac_mul_u64(pk, r);
+    rp += tick();
+    // k_gsum: one G2 addition per summed point; k_vset: one affine conversion per group
+    prev = jac_add(prev, RS);
+    gadd += tick();
+    const Fp vi = fp_inv_gcd(fp_add(fp_sqr(RS.z.c0), fp_sqr(RS.z.c1)));
+    const Fp2 vz = Fp2{fp_mul(RS.z.c0, vi), fp_neg(fp_mul(RS.z.c1, vi))};
+    const Fp2 vz2 = fp2_sqr(vz);
+    (void)fp2_mul(RS.x, vz2);
+    (void)fp2_mul(RS.y, fp2_mul(vz2, vz));
+    vset += tick();
+  }
+  printf("{\"sets_averaged\": %d, \"k_pre\": %.1f, \"chain_h\": %.1f, \"chain_subgroup\": %.1f, "
+         "\"chain_r_sig\": %.1f, \"chain_r_pk\": %.1f, \"gsum_add\": %.1f, \"vset\": %.1f}\n",
+         N, pre / N, h / N, c / N, rs / N, rp / N, gadd / N, vset / N);
+  return 0;
+}
