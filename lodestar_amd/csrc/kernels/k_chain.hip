@@ -85,7 +85,8 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
 
 // Four roles per set, one wavefront per (role, 64 sets), so a call of n sets runs
 // 4 n / 64 wavefronts and its latency is the longest chain, not their sum:
-//   role 0  H = clear_cofactor(iso(q0) + iso(q1)) -> HQ (affine)   ~2.9k Fp products
+//   role 0  H = clear_cofactor(iso(q0) + iso(q1)) -> HQ (affine)   ~2.9k Fp products,
+//           once per distinct signing root
 //   role 1  psi(sig) == [x] sig                                     ~1.2k
 //   role 2  RS = [r] sig                                            ~1.9k
 //   role 3  RP = [r] pk                                             ~1.0k
@@ -94,7 +95,11 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
 __global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks_per_role) {
   const uint32_t role = blockIdx.x / blocks_per_role;
   const uint32_t i = (blockIdx.x % blocks_per_role) * BLS_BLOCK + threadIdx.x;
-  if (i >= b.n_sets || chain_skip(b, i)) return;
+  if (i >= b.n_sets) return;
+  // H(m) once per distinct signing root: only the root's first set
+  // (plan_msg_dedup) runs role 0, whatever its own pubkey / signature status, unless
+  // its SSWU points went to the exact path; k_chain_done shares the result
+  if (role == 0 ? ((b.msg_rep && b.msg_rep[i] != i) || b.set_flag[i]) : chain_skip(b, i)) return;
   Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
   if (role == 0) {
     // H = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P), P = iso(q0) + iso(q1)
@@ -166,9 +171,16 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain_done(PipeBufs b) {
     store_one(&b.f[i]);
     return;
   }
-  if (st[0] || st[3]) {  // H = O or [r] pk = O: the exact path's complete formulas decide
+  const uint32_t rep = b.msg_rep ? b.msg_rep[i] : i;  // the set that computed this root's H
+  if (b.chain_st[4 * rep + 0] || st[3]) {  // H = O or [r] pk = O: the exact path's complete formulas decide
     flag_exact(b, i);
     return;
+  }
+  if (rep != i) {
+    const Fp* src = b.chain + (size_t)CHAIN_WORDS * rep + CH_HQ;
+    Fp* dst = b.chain + (size_t)CHAIN_WORDS * i + CH_HQ;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = src[k];
   }
   b.chain_live[i] = 1u;
 }

@@ -677,8 +677,8 @@ def test_cfg5_shape_two_roots_with_invalid(gpu, oracle, table):
             sig, code = sigs[n - 1 - i].tobytes(), 0
         if i in (257, 1000):         # another validator's key
             pk, code = [(i + 7) % 100], 0
-        if i == 513:                 # undecodable
-            sig, code = bytes(96), -CODE_BAD_ENCODING
+        if i in (0, 513):            # undecodable; set 0 is its root's first set, the one
+            sig, code = bytes(96), -CODE_BAD_ENCODING  # that computes the shared H(m)
         reqs.append((True, [(pk, msgs[i], sig)]))
         expect.append(code)
     pb = pack_requests(reqs)
