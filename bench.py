@@ -315,6 +315,8 @@ def main() -> None:
     ap.add_argument("--roots", type=int, default=0,
                     help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
     ap.add_argument("--no-dedup", action="store_true", help="hash every set's root (BLS_DEBUG_NO_MSG_DEDUP)")
+    ap.add_argument("--no-units", action="store_true",
+                    help="one Miller loop per set even for shared roots (BLS_DEBUG_NO_UNITS)")
     ap.add_argument("--no-merged-check", action="store_true",
                     help="one final exponentiation per chunk only (BLS_DEBUG_NO_MERGED_CHECK)")
     args = ap.parse_args()
@@ -338,11 +340,12 @@ def main() -> None:
             dist.barrier()
             torch.cuda.synchronize()
 
-    from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK, DEBUG_NO_MSG_DEDUP
+    from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK, DEBUG_NO_MSG_DEDUP, DEBUG_NO_UNITS
     from lodestar_amd.native import GpuContext
     from lodestar_amd.shard import global_throughput
 
-    flags = (DEBUG_NO_MSG_DEDUP if args.no_dedup else 0) | (DEBUG_NO_MERGED_CHECK if args.no_merged_check else 0)
+    flags = ((DEBUG_NO_MSG_DEDUP if args.no_dedup else 0) | (DEBUG_NO_MERGED_CHECK if args.no_merged_check else 0)
+             | (DEBUG_NO_UNITS if args.no_units else 0))
     inflight = args.inflight if args.mode == "cfg2" else 1
     ctxs = [GpuContext(local_rank) for _ in range(inflight)]
     gpu = ctxs[0]
@@ -370,6 +373,7 @@ def main() -> None:
                     f"cfg5 shape: {args.sets} single-pubkey sets per call over {args.roots} committee-shared signing "
                     "roots, batchable requests" + (", root dedup off" if args.no_dedup else ""))
         workload += ", merged check off" if args.no_merged_check else ""
+        workload += ", one Miller loop per set" if args.no_units else ""
         config = {"workload": workload, "sets_per_call": args.sets, "calls_in_flight_per_gpu": inflight,
                   "sets_per_step_per_gpu": args.sets * inflight, "parallelism": f"shard-by-request x{world}"}
         scaling = "weak"

@@ -66,9 +66,10 @@ typedef struct bls_stats {
   uint32_t n_individual;       /* requests verified on their own */
   uint32_t n_flagged;          /* sets finished by the exact single-lane path */
   double device_ms;            /* device time of the call (HIP events) */
-  double stage_ms[8];          /* per stage: h2d, pk, pre (SSWU + sig decode), pset, exact, -, status+chunk, individual */
+  double stage_ms[8];          /* per stage: h2d, pk, pre (SSWU + sig decode), per-set (k_pset, or k_chain .. k_mln), exact, -, status+chunk, individual */
   uint32_t n_unique_msgs;      /* distinct signing roots hashed to the curve (== n_sets without dedup) */
   uint32_t merged_check;       /* 0 not run, 1 passed (per-chunk checks skipped), 2 failed (chunks checked) */
+  uint32_t n_ml_units;         /* Miller-loop units (chunk x shared signing root pairings), 0 = one per set */
 } bls_stats;
 
 typedef struct bls_gpu_ctx bls_gpu_ctx;
@@ -204,6 +205,9 @@ int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint
  * the all-cooperative per-set path; default: by call size (>= 512 sets: aggregated). */
 #define BLS_DEBUG_SIGAGG_ON 8u
 #define BLS_DEBUG_SIGAGG_OFF 16u
+/* Test / bench hook: no Miller-loop units (one Miller loop per set even when sets of a
+ * chunk share a signing root). */
+#define BLS_DEBUG_NO_UNITS 32u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

@@ -62,6 +62,7 @@ DEBUG_NO_MSG_DEDUP = 2
 DEBUG_NO_MERGED_CHECK = 4
 DEBUG_SIGAGG_ON = 8
 DEBUG_SIGAGG_OFF = 16
+DEBUG_NO_UNITS = 32
 
 
 def DEBUG_PACK(n: int) -> int:
@@ -96,6 +97,7 @@ class BlsStats(ctypes.Structure):
         ("stage_ms", ctypes.c_double * 8),
         ("n_unique_msgs", ctypes.c_uint32),
         ("merged_check", ctypes.c_uint32),
+        ("n_ml_units", ctypes.c_uint32),
     ]
 
 

@@ -35,6 +35,7 @@ namespace bls {
 // A group's virtual set (index n_sets + chunk, n_sets + n_chunks + individual
 // request) holds HQ = affine(sum of the group's RS) and RP = -g1.
 enum : int { CH_HQ = 0, CH_RP = 4, CH_RS = 7, CHAIN_WORDS = 13 };
+#define UNIT_NONE 0xFFFFFFFFu
 
 struct PipeBufs {
   uint32_t n_sets, n_reqs, n_chunks, n_indiv;
@@ -90,6 +91,14 @@ struct PipeBufs {
   uint32_t* chain_live;  // n_sets + virtual: 1 = k_mln runs this set's Miller loop
   uint8_t* chain_st;     // 4 n_sets: per set, role 0 H = O, role 1 outside G2, role 3 [r] pk = O
   const uint32_t* gsets; // set indices of the groups being summed, group-major (k_gsum level 0)
+  // Miller-loop units (sum r_i pk_i per signing root): with committee-shared
+  // roots, the batchable sets of one chunk that sign the same root share ONE Miller loop
+  // ML(sum r_i pk_i, H(root)) at f[unit_base + u]; such a set's own f_i is 1.
+  // set_unit[i] = its unit or UNIT_NONE (own Miller loop); nullable (no units).
+  const uint32_t* set_unit;
+  const uint32_t* unit_off;  // n_chunks + 1: chunk c's units [unit_off[c], unit_off[c + 1])
+  uint32_t unit_base, n_units;
+  uint32_t indiv_vbase;      // f index of individually verified request t's signature sum
   uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
   uint32_t* flag_count;  // 1 word: sets flagged by the cooperative kernel (GPU path)
   // outputs

@@ -182,6 +182,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain_done(PipeBufs b) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) dst[k] = src[k];
   }
+  if (b.set_unit && b.set_unit[i] != UNIT_NONE) store_one(&b.f[i]);  // paired in its unit
   b.chain_live[i] = 1u;
 }
 

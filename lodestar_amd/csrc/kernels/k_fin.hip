@@ -54,9 +54,15 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv e
   bool first = true;
   for (uint32_t k = beg; k < end; ++k) {
     const uint32_t r = b.chunk_reqs[k];
-    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) fin_accumulate_set(b, env, sh, i, first);
+    for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; ++i) {
+      // a live set paired in its Miller-loop unit has f_i = 1: skip the product
+      if (b.set_unit && b.set_unit[i] != UNIT_NONE && b.chain_live[i]) continue;
+      fin_accumulate_set(b, env, sh, i, first);
+    }
   }
   if (b.sigagg) fin_accumulate_set(b, env, sh, b.n_sets + c, first);  // ML(-g1, sum of the chunk's r sig)
+  if (b.unit_off)
+    for (uint32_t u = b.unit_off[c]; u < b.unit_off[c + 1]; ++u) fin_accumulate_set(b, env, sh, b.unit_base + u, first);
   bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.chunk_ok[c] = ok ? 1 : 0;
 }
@@ -74,7 +80,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
   bool first = true;
   const uint32_t stride = b.fold > 1 ? b.fold : 1u;  // f's pre-multiplied in groups by k_fold
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set(b, env, sh, i, first);
-  if (b.sigagg) fin_accumulate_set(b, env, sh, b.n_sets + b.n_chunks + t, first);  // the request's own sum
+  if (b.sigagg) fin_accumulate_set(b, env, sh, b.indiv_vbase + t, first);  // the request's own signature sum
   bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.indiv_verdict[t] = ok ? 1 : 0;
 }

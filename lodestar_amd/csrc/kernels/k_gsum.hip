@@ -80,6 +80,72 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_vset(PipeBufs b, const G2J* sums,
   b.chain_live[v] = 1u;
 }
 
+// Miller-loop units: segmented sums of RP_i = [r_i] pk_i (G1 Jacobian) over each unit's
+// live sets, the same segment plan as k_gsum; k_uset then writes the unit's chain entry
+// (HQ of the root's first set, RP = the sum; no affine form needed on G1).
+__device__ __noinline__ void g1_add_p(G1J* acc, const G1J* p) { *acc = jac_add(*acc, *p); }
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_gsum1(PipeBufs b, const uint32_t* seg, uint32_t n_seg, const G1J* in,
+                                                     G1J* out) {
+  const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (k >= n_seg) return;
+  const uint32_t beg = seg[2 * k], end = seg[2 * k + 1];
+  G1J acc = jac_infinity<Fp>();
+  for (uint32_t j = beg; j < end; ++j) {
+    G1J p;
+    if (in) {
+      p = in[j];
+    } else {
+      const uint32_t i = b.gsets[j];
+      if (!b.chain_live[i]) continue;
+      const Fp* c = b.chain + (size_t)CHAIN_WORDS * i + CH_RP;
+      p.x = c[0];
+      p.y = c[1];
+      p.z = c[2];
+    }
+    g1_add_p(&acc, &p);
+  }
+  out[k] = acc;
+}
+
+// unit u of the call: rep = the set whose HQ the unit pairs (its root's first set)
+__global__ __launch_bounds__(BLS_BLOCK) void k_uset(PipeBufs b, const G1J* sums, const uint32_t* unit_rep) {
+  const uint32_t u = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (u >= b.n_units) return;
+  const uint32_t v = b.unit_base + u;
+  const G1J s = sums[u];
+  const uint32_t rep = unit_rep[u];
+  if (jac_is_inf(s)) {  // no live set (errors, exact path) or a cancelling sum: f = 1
+    b.chain_live[v] = 0u;
+    Fp* d = reinterpret_cast<Fp*>(&b.f[v]);
+    d[0] = c_one();
+#pragma unroll
+    for (int k = 1; k < 12; ++k) d[k] = fp_zero();
+    return;
+  }
+  Fp* o = b.chain + (size_t)CHAIN_WORDS * v;
+  const Fp* h = b.chain + (size_t)CHAIN_WORDS * rep + CH_HQ;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[CH_HQ + k] = h[k];
+  o[CH_RP + 0] = s.x;
+  o[CH_RP + 1] = s.y;
+  o[CH_RP + 2] = s.z;
+  b.chain_live[v] = 1u;
+}
+
+hipError_t launch_k_gsum1(const PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const G1J* in, G1J* out,
+                          hipStream_t s) {
+  if (n_seg == 0) return hipSuccess;
+  k_gsum1<<<bls_grid_for(n_seg), BLS_BLOCK, 0, s>>>(b, seg, n_seg, in, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_k_uset(const PipeBufs& b, const G1J* sums, const uint32_t* unit_rep, hipStream_t s) {
+  if (b.n_units == 0) return hipSuccess;
+  k_uset<<<bls_grid_for(b.n_units), BLS_BLOCK, 0, s>>>(b, sums, unit_rep);
+  return hipGetLastError();
+}
+
 hipError_t launch_k_gsum(const PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const G2J* in, G2J* out,
                          hipStream_t s) {
   if (n_seg == 0) return hipSuccess;

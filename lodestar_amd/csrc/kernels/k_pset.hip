@@ -213,7 +213,8 @@ __global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
 enum : int { ML1_SLOTS = 19, ML1_RP = 0, ML1_HQ = 3, ML1_F = 7 };
 
 template <int S, class Lds>
-__global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count) {
+__global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count,
+                                                    uint32_t units_paired) {
   __shared__ Lds sh;
   const CoopProg& ml = S == 1 ? env.ml1_1 : (S == 2 ? env.ml1_2 : env.ml1_4);
   const int lane = threadIdx.x;
@@ -223,7 +224,10 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint32_t i = i0 + s;
-    live[s] = i < end && b.chain_live[i];
+    // a set paired inside its Miller-loop unit has f_i = 1 here (units_paired: the
+    // first pass), but runs its own loop when its request is verified alone
+    live[s] = i < end && b.chain_live[i] &&
+              !(units_paired && b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE);
     if (live[s] && first_live < 0) first_live = s;
   }
   if (first_live < 0) return;
@@ -273,15 +277,18 @@ static uint32_t ml_pack(const PipeBufs& b) {
   return 4u;
 }
 
-hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s) {
+// own_only: sets run their own Miller loop even when they belong to a unit (requests
+// verified alone after their chunk failed)
+hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s,
+                        bool own_only) {
   if (count == 0) return hipSuccess;
-  const uint32_t S = ml_pack(b);
+  const uint32_t S = ml_pack(b), up = own_only ? 0u : 1u;
   if (S == 4 && env.ml1_4.n > 0) {
-    k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count);
+    k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count, up);
   } else if (S == 2 && env.ml1_2.n > 0) {
-    k_mln<2, CoopLds><<<(count + 1) / 2, COOP_LANES, 0, s>>>(b, env, first, count);
+    k_mln<2, CoopLds><<<(count + 1) / 2, COOP_LANES, 0, s>>>(b, env, first, count, up);
   } else {
-    k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env, first, count);
+    k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env, first, count, up);
   }
   return hipGetLastError();
 }

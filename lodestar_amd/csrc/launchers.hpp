@@ -23,6 +23,9 @@ hipError_t launch_k_gsum(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n
                          bls::G2J* out, hipStream_t s);
 hipError_t launch_k_vset(const bls::PipeBufs& b, const bls::G2J* sums, uint32_t n_groups, uint32_t vbase,
                          hipStream_t s);
+hipError_t launch_k_gsum1(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const bls::G1J* in,
+                          bls::G1J* out, hipStream_t s);
+hipError_t launch_k_uset(const bls::PipeBufs& b, const bls::G1J* sums, const uint32_t* unit_rep, hipStream_t s);
 #define GSUM_FAN 4u  // points per k_gsum segment (a 16-set chunk: two levels of 3 additions)
 hipError_t launch_k_hash_to_g2(const uint8_t* msgs, uint32_t n, uint8_t* out192, hipStream_t s);
 hipError_t launch_k_sig_aggregate(const uint8_t* in96, uint32_t n, const uint32_t* off, uint32_t n_lists,
@@ -46,4 +49,4 @@ hipError_t launch_k_fprod(const bls::Fp12* in, uint32_t n, bls::Fp12* out, int32
                           const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_mln(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_t first, uint32_t count,
-                        hipStream_t s);
+                        hipStream_t s, bool own_only = false);

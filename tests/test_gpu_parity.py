@@ -658,12 +658,12 @@ def test_cfg2_1024_call_with_invalid_sets(gpu, oracle, golden, table):
         assert st.merged_check == (0 if name == "no_merged" else 1), name
 
 
-def test_cfg5_shape_two_roots_with_invalid(gpu, oracle, table):
+def test_cfg5_shape_two_roots_with_invalid(gpu, oracle, table, verify_path):
     """cfg5 shape: 1024 attestations of two committees sharing two signing
     roots, with invalid sets (a signature over the other root, a wrong key, an
     undecodable signature) in both committees; verdicts equal with root dedup on / off,
     every packing and the exact path."""
-    from lodestar_amd._abi import DEBUG_NO_MSG_DEDUP
+    from lodestar_amd._abi import DEBUG_NO_MSG_DEDUP, DEBUG_NO_UNITS
 
     n = 1024
     roots = [_h(b"epoch-root-a"), _h(b"epoch-root-b")]
@@ -683,16 +683,25 @@ def test_cfg5_shape_two_roots_with_invalid(gpu, oracle, table):
         expect.append(code)
     pb = pack_requests(reqs)
     res = _run_all_paths(gpu, pb)
-    try:
-        gpu.set_debug_flags(DEBUG_NO_MSG_DEDUP)
-        res["no_dedup"] = gpu.verify_packed(pb)
-    finally:
-        gpu.set_debug_flags(0)
+    for name, flags in (("no_dedup", DEBUG_NO_MSG_DEDUP), ("no_units", DEBUG_NO_UNITS)):
+        try:
+            gpu.set_debug_flags(flags)
+            res[name] = gpu.verify_packed(pb)
+        finally:
+            gpu.set_debug_flags(0)
     retries, ok = _expected_stats(expect)
     for name, (v, st) in res.items():
         assert list(v) == expect, name
         assert (st.batch_retries, st.batch_sigs_success) == (retries, ok), name
     assert res["auto"][1].n_unique_msgs == 2 and res["no_dedup"][1].n_unique_msgs == n
+    # aggregated-signature path: one Miller loop per (chunk, root) -- 64 chunks of 16
+    # requests, the roots change at a chunk boundary (set 512)
+    assert res["auto"][1].n_ml_units == (64 if verify_path == "sigagg" else 0)
+    assert res["no_units"][1].n_ml_units == 0
+    # all valid: the merged check passes over the units
+    good = pack_requests([(True, [([i % 100], msgs[i], sigs[i].tobytes())]) for i in range(n)])
+    v, st = gpu.verify_packed(good)
+    assert list(v) == [1] * n and st.merged_check == 1
 
 
 def test_kat3_mainnet_points_gpu_decode(gpu, golden, oracle, table):
