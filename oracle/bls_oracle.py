@@ -28,8 +28,8 @@ KAT-2 100 interop pubkeys (`state-transition/test-cache/interop-pubkeys.json`),
 KAT-3 real mainnet G2 points (`beacon-node/test/unit/sync/backfill/blocks.json`).
 
 Pure Python big-int arithmetic: slow (a pairing takes ~0.5 s) and meant for small
-cases only.  The fast CPU restatement used for the CPU baseline lives in
-`oracle/c/bls_ref.c`.
+cases only.  The multi-threaded C++ restatement of the reference's worker pool that
+bench.py times as the CPU baseline lives in `oracle/cpu/bls_cpu.cpp` ("not blst").
 """
 from __future__ import annotations
 
