@@ -75,6 +75,10 @@ struct PipeBufs {
   // message before any verification and throws on the first bad key
   // (worker.ts:43-46), so the whole call rejects with that key's code.
   uint32_t* first_bad_pk;
+  uint32_t* first_bad_pk_next;  // the next call's slot, reset by k_pk
+  uint32_t init_set_flag;       // k_pk's initial set_flag (1: BLS_DEBUG_FORCE_EXACT)
+  int32_t* req_status_host;     // host-mapped mirror of req_status (k_status), nullable
+  uint32_t* flag_count_host;    // host-mapped copy of *flag_count (k_status), nullable
   G2A* H;
   G1J* rpk;
   G2J* rsig;

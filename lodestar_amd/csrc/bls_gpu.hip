@@ -46,8 +46,14 @@ struct bls_gpu_ctx {
   // grow-only device workspace and pinned staging
   uint8_t* dev_ws;
   size_t dev_ws_cap;
-  uint8_t* host_stage;
+  uint8_t* host_stage;      // verify inputs, pinned + device-mapped: kernels read them in place
+  uint8_t* host_stage_dev;  // device view of host_stage
   size_t host_stage_cap;
+  uint8_t* host_res;        // verify results written by kernels (host-mapped, coherent)
+  uint8_t* host_res_dev;
+  size_t host_res_cap;
+  uint32_t* first_bad;      // two device slots for first_bad_pk (k_pk resets the next call's)
+  uint32_t first_bad_slot;
   // cooperative programs (coop_tables.bin, tools/gen_coop.py)
   CoopEnv coop;
   void* coop_dev;
@@ -78,10 +84,12 @@ namespace {
 struct Carver {
   uint8_t* base;
   size_t off;
+  uint8_t* host = nullptr;  // offsets below `split` map into this (device view of pinned memory)
+  size_t split = 0;
   template <class T>
   T* take(size_t count) {
     off = (off + 255) & ~(size_t)255;
-    T* p = (T*)(base ? base + off : nullptr);
+    T* p = (T*)(base ? (off < split && host ? host : base) + off : nullptr);
     off += sizeof(T) * (count ? count : 1);
     return p;
   }
@@ -97,22 +105,36 @@ int ensure_dev(bls_gpu_ctx* ctx, size_t bytes) {
   return 0;
 }
 
-int ensure_host(bls_gpu_ctx* ctx, size_t bytes) {
-  if (bytes <= ctx->host_stage_cap) return 0;
-  if (ctx->host_stage) HIPC(ctx, hipHostFree(ctx->host_stage));
-  ctx->host_stage = nullptr;
-  size_t cap = bytes + bytes / 4;
-  HIPC(ctx, hipHostMalloc(&ctx->host_stage, cap, hipHostMallocDefault));
-  ctx->host_stage_cap = cap;
+// Pinned, device-mapped, coherent host memory: the kernels of a verify call read its
+// inputs from here and write its results here, so a call moves no data with copy or
+// fill blits (those queue behind other contexts' and wait for CU slots under load).
+int ensure_mapped(bls_gpu_ctx* ctx, size_t bytes, uint8_t** host, uint8_t** dev, size_t* cap_io) {
+  if (bytes <= *cap_io) return 0;
+  if (*host) HIPC(ctx, hipHostFree(*host));
+  *host = *dev = nullptr;
+  size_t cap = bytes + bytes / 4 + 4096;
+  HIPC(ctx, hipHostMalloc((void**)host, cap, hipHostMallocMapped | hipHostMallocCoherent));
+  HIPC(ctx, hipHostGetDevicePointer((void**)dev, *host, 0));
+  *cap_io = cap;
   return 0;
 }
 
-// Copy a host array into the staging area at the same offset its device twin has.
+int ensure_host(bls_gpu_ctx* ctx, size_t bytes) {
+  return ensure_mapped(ctx, bytes, &ctx->host_stage, &ctx->host_stage_dev, &ctx->host_stage_cap);
+}
+
+// Write a host array into the staging area behind its device-side pointer.
 template <class T>
 void stage_copy(bls_gpu_ctx* ctx, const T* dev_ptr, const void* src, size_t bytes) {
   if (!src || !bytes) return;
-  size_t off = (const uint8_t*)dev_ptr - ctx->dev_ws;
+  size_t off = (const uint8_t*)dev_ptr - ctx->host_stage_dev;
   memcpy(ctx->host_stage + off, src, bytes);
+}
+
+// host view of a pointer into the result area
+template <class T>
+T* res_host(bls_gpu_ctx* ctx, T* dev_ptr) {
+  return (T*)(ctx->host_res + ((uint8_t*)dev_ptr - ctx->host_res_dev));
 }
 
 }  // namespace
@@ -298,6 +320,11 @@ int bls_gpu_init(int device, bls_gpu_ctx** out) {
     bls_gpu_close(ctx);
     return -1;
   }
+  if (hipMalloc(&ctx->first_bad, 2 * sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(ctx->first_bad, 0xFF, 2 * sizeof(uint32_t)) != hipSuccess) {
+    bls_gpu_close(ctx);
+    return -1;
+  }
   *out = ctx;
   return 0;
 }
@@ -311,6 +338,8 @@ void bls_gpu_close(bls_gpu_ctx* ctx) {
   if (ctx->table) (void)hipFree(ctx->table);
   if (ctx->dev_ws) (void)hipFree(ctx->dev_ws);
   if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
+  if (ctx->host_res) (void)hipHostFree(ctx->host_res);
+  if (ctx->first_bad) (void)hipFree(ctx->first_bad);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
   for (int i = 0; i < 9; ++i) (void)hipEventDestroy(ctx->ev[i]);
@@ -662,7 +691,6 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.sig_status = c.take<int32_t>(n);
     b.pk = c.take<G1J>(n);
     b.pk_status = c.take<int32_t>(n);
-    b.first_bad_pk = b.pubkeys ? c.take<uint32_t>(1) : nullptr;
     b.pk_inf = partial ? c.take<uint8_t>(n) : nullptr;
     b.q = c.take<Fp>(8ull * n);
     b.chain = sigagg ? c.take<Fp>((size_t)CHAIN_WORDS * n_total) : nullptr;
@@ -676,24 +704,38 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.flag_count = c.take<uint32_t>(1);
     b.f = c.take<Fp12>(n_total);
     b.req_status = c.take<int32_t>(R);
-    b.chunk_ok = c.take<int32_t>(n_chunks);
-    b.indiv_verdict = c.take<int32_t>(R);
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
       ptree[1] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
     }
+  };
+  // results: written by the kernels straight into host-mapped memory
+  auto carve_res = [&](Carver& c, PipeBufs& b) {
+    b.chunk_ok = c.take<int32_t>(n_chunks);
+    b.indiv_verdict = c.take<int32_t>(R);
+    b.req_status_host = c.take<int32_t>(R);
+    b.flag_count_host = c.take<uint32_t>(1);
     merged_ok = merged ? c.take<int32_t>(1) : nullptr;
   };
   PipeBufs b;
   memset(&b, 0, sizeof(b));
   size_t input_end = 0;
   {
-    Carver c{nullptr, 0};
+    Carver c{nullptr, 0}, cr{nullptr, 0};
     carve(c, b, input_end);
-    if (ensure_dev(ctx, c.off) || ensure_host(ctx, input_end)) return -1;
+    carve_res(cr, b);
+    if (ensure_dev(ctx, c.off) || ensure_host(ctx, input_end) ||
+        ensure_mapped(ctx, cr.off, &ctx->host_res, &ctx->host_res_dev, &ctx->host_res_cap))
+      return -1;
   }
-  Carver c{ctx->dev_ws, 0};
+  // inputs [0, input_end) live in the mapped staging area, the rest in device memory
+  Carver c{ctx->dev_ws, 0, ctx->host_stage_dev, input_end};
   carve(c, b, input_end);
+  Carver cr{ctx->host_res_dev, 0};
+  carve_res(cr, b);
+  b.first_bad_pk = b.pubkeys ? ctx->first_bad + ctx->first_bad_slot : nullptr;
+  b.first_bad_pk_next = ctx->first_bad + (ctx->first_bad_slot ^ 1u);
+  b.init_set_flag = (ctx->debug_flags & BLS_DEBUG_FORCE_EXACT) ? 1u : 0u;
   b.n_sets = n;
   b.n_reqs = R;
   b.n_chunks = n_chunks;
@@ -737,7 +779,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     // bytes past a short signature's length are never read (the set fails INVALID_SIZE)
     for (uint32_t i = 0; i < n; ++i) {
       uint32_t len = in->signature_lens[i] < 96 ? in->signature_lens[i] : 96;
-      uint8_t* dst = ctx->host_stage + ((const uint8_t*)b.sigs - ctx->dev_ws) + 96ull * i;
+      uint8_t* dst = ctx->host_stage + ((const uint8_t*)b.sigs - ctx->host_stage_dev) + 96ull * i;
       memset(dst, 0, 96);
       memcpy(dst, in->signatures + 96ull * i, len);
     }
@@ -748,13 +790,10 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
 
   hipStream_t s = ctx->stream;
   HIPC(ctx, hipEventRecord(ctx->ev0, s));
-  HIPC(ctx, hipMemcpyAsync(ctx->dev_ws, ctx->host_stage, input_end, hipMemcpyHostToDevice, s));
-  HIPC(ctx, hipEventRecord(ctx->ev[0], s));
-  if (b.first_bad_pk) HIPC(ctx, hipMemsetAsync(b.first_bad_pk, 0xFF, sizeof(uint32_t), s));
+  HIPC(ctx, hipEventRecord(ctx->ev[0], s));  // no H2D stage: the kernels read the mapped inputs
   if (n > 0) {
-    HIPC(ctx, hipMemsetAsync(b.set_flag, (ctx->debug_flags & BLS_DEBUG_FORCE_EXACT) ? 1 : 0, sizeof(uint32_t) * n, s));
-    HIPC(ctx, hipMemsetAsync(b.flag_count, 0, sizeof(uint32_t), s));
-    HIPC(ctx, launch_k_pk(b, s));
+    HIPC(ctx, launch_k_pk(b, s));  // also resets set_flag, flag_count, the next first_bad_pk slot
+    ctx->first_bad_slot ^= 1u;
     HIPC(ctx, hipEventRecord(ctx->ev[1], s));
     HIPC(ctx, launch_k_pre(b, s));
     HIPC(ctx, hipEventRecord(ctx->ev[2], s));
@@ -809,22 +848,23 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   std::vector<int32_t> merged_status(merged ? R : 0, 0);
   int32_t merged_verdict = 0;
   uint32_t flagged = 0;
-  auto read_merged = [&]() -> int {
-    HIPC(ctx, hipMemcpyAsync(&merged_verdict, merged_ok, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIPC(ctx, hipMemcpyAsync(merged_status.data(), b.req_status, sizeof(int32_t) * R, hipMemcpyDeviceToHost, s));
-    return 0;
+  // after a stream sync: the merged verdict and the statuses, from the mapped result area
+  auto read_merged = [&]() {
+    merged_verdict = *res_host(ctx, merged_ok);
+    memcpy(merged_status.data(), res_host(ctx, b.req_status_host), sizeof(int32_t) * R);
   };
-  if (merged && read_merged()) return -1;
-  if (n > 0) HIPC(ctx, hipMemcpyAsync(&flagged, b.flag_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIPC(ctx, hipStreamSynchronize(s));
+  if (merged) read_merged();
+  if (n > 0) flagged = *res_host(ctx, b.flag_count_host);
   if (flagged) {
     // rare: sets the cooperative kernel could not finish (exceptional additions,
     // infinity signatures, special SSWU inputs) -> exact path, then the status (the
     // exact path may find a signature outside G2) and the merged check again
     HIPC(ctx, launch_k_exact(b, s));
     HIPC(ctx, launch_k_status(b, s));
-    if (merged && (launch_merged() || read_merged())) return -1;
+    if (merged && launch_merged()) return -1;
     HIPC(ctx, hipStreamSynchronize(s));
+    if (merged) read_merged();
   }
   bool merged_pass = merged && merged_verdict == 1;
   for (uint32_t r = 0; merged_pass && r < R; ++r) merged_pass = merged_status[r] == BLS_OK;
@@ -833,8 +873,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   } else if (n_chunks > 0 && !partial) {
     // some set is invalid or erroneous (or no merged check): the per-chunk verdicts decide
     HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s));
-    HIPC(ctx, hipMemcpyAsync(chunk_ok.data(), b.chunk_ok, sizeof(int32_t) * n_chunks, hipMemcpyDeviceToHost, s));
     HIPC(ctx, hipStreamSynchronize(s));
+    memcpy(chunk_ok.data(), res_host(ctx, b.chunk_ok), sizeof(int32_t) * n_chunks);
   }
   if (stats) stats->merged_check = merged ? (merged_pass ? 1 : 2) : 0;
   if (stats) {
@@ -850,9 +890,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     // sets), then an infinity pubkey (verifyMultipleSignatures).  The shard reports its
     // first error of the lowest class with its set index, so the ranks can reduce
     // (class, call index) in that order (lodestar_amd/shard.py).
-    std::vector<int32_t> st(R, 0);
-    HIPC(ctx, hipMemcpyAsync(st.data(), b.req_status, sizeof(int32_t) * R, hipMemcpyDeviceToHost, s));
-    HIPC(ctx, hipStreamSynchronize(s));
+    std::vector<int32_t> st(res_host(ctx, b.req_status_host), res_host(ctx, b.req_status_host) + R);
     *partial_status = 0;
     for (uint32_t r = 0; r < R && !*partial_status; ++r)
       if (st[r] != 0) *partial_status = -st[r];
@@ -907,8 +945,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   GsumPlan indiv_gsum;           // likewise
   if (!indiv.empty()) {
     b.n_indiv = (uint32_t)indiv.size();
-    HIPC(ctx, hipMemcpyAsync((void*)b.indiv_reqs, indiv.data(), sizeof(uint32_t) * indiv.size(),
-                             hipMemcpyHostToDevice, s));
+    stage_copy(ctx, b.indiv_reqs, indiv.data(), sizeof(uint32_t) * indiv.size());  // the stream is idle
     HIPC(ctx, hipEventRecord(ctx->ev[7], s));
     if (sigagg) {
       // each individually verified request pairs the sum of its own r sig:
@@ -926,10 +963,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
         snprintf(ctx->err, sizeof(ctx->err), "group-sum plan exceeds its workspace");
         return -3;
       }
-      HIPC(ctx, hipMemcpyAsync(gsets_dev, indiv_gsum.gsets.data(), sizeof(uint32_t) * indiv_gsum.gsets.size(),
-                               hipMemcpyHostToDevice, s));
-      HIPC(ctx, hipMemcpyAsync(gseg_dev, indiv_gsum.seg.data(), sizeof(uint32_t) * indiv_gsum.seg.size(),
-                               hipMemcpyHostToDevice, s));
+      stage_copy(ctx, gsets_dev, indiv_gsum.gsets.data(), sizeof(uint32_t) * indiv_gsum.gsets.size());
+      stage_copy(ctx, gseg_dev, indiv_gsum.seg.data(), sizeof(uint32_t) * indiv_gsum.seg.size());
       if (launch_gsum(ctx, b, indiv_gsum, gseg_dev, gsets_dev, gtmp, indiv_vbase, s)) return -1;
       HIPC(ctx, launch_k_mln(b, ctx->coop, indiv_vbase, (uint32_t)indiv.size(), s));
     }
@@ -949,17 +984,15 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     if (any_fold) {
       b.fold = BLS_FOLD;
       b.n_fold = (uint32_t)(groups.size() / 2);
-      HIPC(ctx, hipMemcpyAsync((void*)b.fold_groups, groups.data(), sizeof(uint32_t) * groups.size(),
-                               hipMemcpyHostToDevice, s));
+      stage_copy(ctx, b.fold_groups, groups.data(), sizeof(uint32_t) * groups.size());
       HIPC(ctx, launch_k_fold(b, ctx->coop, s));
     }
     HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, s));
     HIPC(ctx, hipEventRecord(ctx->ev[8], s));
-    HIPC(ctx, hipMemcpyAsync(indiv_verdict.data(), b.indiv_verdict, sizeof(int32_t) * indiv.size(),
-                             hipMemcpyDeviceToHost, s));
   }
   HIPC(ctx, hipEventRecord(ctx->ev1, s));
   HIPC(ctx, hipStreamSynchronize(s));
+  if (!indiv.empty()) memcpy(indiv_verdict.data(), res_host(ctx, b.indiv_verdict), sizeof(int32_t) * indiv.size());
   assemble_verdicts(in, plan, chunk_ok.data(), indiv, indiv_verdict.data(), verdicts, stats);
   if (stats) {
     float ms = 0.f;

@@ -4,7 +4,20 @@
 
 using namespace bls;
 
-__global__ __launch_bounds__(BLS_BLOCK) void k_pk(PipeBufs b) { stage_pk(b, blockIdx.x * BLS_BLOCK + threadIdx.x); }
+// First kernel of a verify call: also resets the call's device-side words, so the
+// call needs no memset blits (which queue behind every context's copies and wait for
+// CU slots under load): set_flag (the exact-path marks), flag_count, and the other
+// slot of the two-slot first_bad_pk (the next call's; this call's slot was reset by
+// the previous call, or at context creation).
+__global__ __launch_bounds__(BLS_BLOCK) void k_pk(PipeBufs b) {
+  const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (i < b.n_sets) b.set_flag[i] = b.init_set_flag;
+  if (i == 0) {
+    *b.flag_count = 0u;
+    if (b.first_bad_pk_next) *b.first_bad_pk_next = 0xFFFFFFFFu;
+  }
+  stage_pk(b, i);
+}
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_aggregate(PipeBufs b, uint8_t* out96) {
   uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
@@ -45,8 +58,14 @@ hipError_t launch_k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk
   return hipGetLastError();
 }
 
+// Per-request status; also mirrors the statuses and the exact-path count into the
+// context's host-mapped result area (read by the host after the stream syncs, no D2H
+// copy blits).
 __global__ __launch_bounds__(BLS_BLOCK) void k_status(PipeBufs b) {
-  stage_req_status(b, blockIdx.x * BLS_BLOCK + threadIdx.x);
+  const uint32_t r = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  stage_req_status(b, r);
+  if (b.req_status_host && r < b.n_reqs) b.req_status_host[r] = b.req_status[r];
+  if (r == 0 && b.flag_count_host) *b.flag_count_host = b.n_sets ? *b.flag_count : 0u;
 }
 
 hipError_t launch_k_pk(const PipeBufs& b, hipStream_t s) {
