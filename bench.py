@@ -310,7 +310,7 @@ def main() -> None:
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--inflight", type=int, default=16, help="calls in flight per GPU (contexts / HIP streams)")
+    ap.add_argument("--inflight", type=int, default=20, help="calls in flight per GPU (contexts / HIP streams)")
     ap.add_argument("--mode", choices=("cfg2", "sharded", "napi"), default="cfg2")
     ap.add_argument("--roots", type=int, default=0,
                     help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
