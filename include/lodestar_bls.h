@@ -165,6 +165,35 @@ int bls_gpu_g2_decompress(bls_gpu_ctx* ctx, const uint8_t* in96, uint32_t n, int
  * ZCash order x.c1 || x.c0 || y.c1 || y.c0). */
 int bls_gpu_hash_to_g2(bls_gpu_ctx* ctx, const uint8_t* msgs, uint32_t n, uint8_t* out192);
 
+/* SSZ object kinds of bls_gpu_ssz_roots: the fixed-size containers whose signing roots
+ * the signature-set producers compute (state-transition/src/signatureSets/), given
+ * in their SSZ serialization (fields concatenated, integers little-endian).  The value
+ * is the serialized size in bytes in the low 8 bits. */
+enum {
+  BLS_SSZ_ROOT = 0x000 | 32,                /* Root / Bytes32: sync committee messages (block root), or an
+                                               object root computed elsewhere (e.g. AggregateAndProof) */
+  BLS_SSZ_UINT64 = 0x100 | 8,               /* Epoch / Slot: randao reveal, aggregate selection proof */
+  BLS_SSZ_CHECKPOINT = 0x200 | 40,          /* Checkpoint{epoch, root} */
+  BLS_SSZ_ATTESTATION_DATA = 0x300 | 128,   /* AttestationData: attestations, indexed attestations, slashings */
+  BLS_SSZ_TWO_UINT64 = 0x400 | 16,          /* VoluntaryExit{epoch, validator_index},
+                                               SyncAggregatorSelectionData{slot, subcommittee_index} */
+  BLS_SSZ_BEACON_BLOCK_HEADER = 0x500 | 112, /* BeaconBlockHeader (== the block's root given its body root):
+                                               proposer signatures, proposer slashings */
+  BLS_SSZ_DEPOSIT_MESSAGE = 0x600 | 88,     /* DepositMessage{pubkey 48, withdrawal_credentials, amount} */
+  BLS_SSZ_FORK_DATA = 0x700 | 36,           /* ForkData{current_version 4, genesis_validators_root}:
+                                               computeForkDataRoot (util/domain.ts:40-45) */
+  BLS_SSZ_SIGNING_DATA = 0x800 | 64         /* SigningData{object_root, domain} */
+};
+#define BLS_SSZ_SIZE(kind) ((uint32_t)(kind) & 0xFFu)
+
+/* computeSigningRoot(type, obj, domain) (state-transition/src/util/signingRoot.ts:7-13)
+ * for n serialized objects of one kind: out32[i] = hash_tree_root(SigningData{
+ * hash_tree_root(obj_i), domain_i}); with domains == NULL, out32[i] = hash_tree_root(obj_i)
+ * instead.  objs: n * BLS_SSZ_SIZE(kind) bytes; domain_stride 0 = one 32-byte domain for
+ * every object, 32 = one per object.  Returns -2 for an unknown kind or stride. */
+int bls_gpu_ssz_roots(bls_gpu_ctx* ctx, uint32_t kind, const uint8_t* objs, uint32_t n, const uint8_t* domains,
+                      uint32_t domain_stride, uint8_t* out32);
+
 /* Fixture helpers (signing is out of the verify path; used to synthesise inputs).
  * sks: n * 32 bytes big-endian scalars. */
 int bls_gpu_sk_to_pk(bls_gpu_ctx* ctx, const uint8_t* sks, uint32_t n, uint8_t* out48);

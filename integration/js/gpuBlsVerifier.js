@@ -99,6 +99,20 @@ function packRequests(jobs) {
   };
 }
 
+/** SSZ kinds of bls_gpu_ssz_roots (include/lodestar_bls.h; low 8 bits = serialized size) */
+const SSZ_KINDS = {
+  root: 0x000 | 32,
+  uint64: 0x100 | 8,
+  checkpoint: 0x200 | 40,
+  attestationData: 0x300 | 128,
+  voluntaryExit: 0x400 | 16,
+  syncAggregatorSelectionData: 0x400 | 16,
+  beaconBlockHeader: 0x500 | 112,
+  depositMessage: 0x600 | 88,
+  forkData: 0x700 | 36,
+  signingData: 0x800 | 64,
+};
+
 /** getAggregatedPubkeysCount (chain/bls/utils.ts:18-26): keys of aggregate-type sets */
 function getAggregatedPubkeysCount(sets) {
   let n = 0;
@@ -190,6 +204,18 @@ class GpuBlsVerifier {
   verifySignatureSetsEachSync(sets) {
     const v = this.addon.verifySync(this.ctxs[0].handle, packRequests(sets.map((s) => ({batchable: false, sets: [s]}))));
     return sets.map((_, i) => this._settle(v, i));
+  }
+
+  /**
+   * computeSigningRoot (state-transition/src/util/signingRoot.ts:7-13) for a batch of
+   * serialized SSZ objects of one kind on the GPU (SSZ_KINDS: attestationData,
+   * beaconBlockHeader, uint64, ...): Uint8Array(32 n) of signing roots; `domains` is one
+   * 32-byte domain, one per object, or null for the objects' hash_tree_roots.
+   */
+  computeSigningRoots(kind, objs, domains) {
+    const k = typeof kind === "string" ? SSZ_KINDS[kind] : kind;
+    if (k === undefined) throw Error(`unknown SSZ kind ${kind}`);
+    return this.addon.sszRoots(this.ctxs[0].handle, k, objs, domains === undefined ? null : domains);
   }
 
   /** IBlsVerifier.close (index.ts:176-197): abort queued jobs, wait for calls in flight */
@@ -342,4 +368,11 @@ class GpuBlsVerifier {
   }
 }
 
-module.exports = {GpuBlsVerifier, chunkifyMaximizeChunkSize, packRequests, getAggregatedPubkeysCount, ERROR_MESSAGES};
+module.exports = {
+  GpuBlsVerifier,
+  chunkifyMaximizeChunkSize,
+  packRequests,
+  getAggregatedPubkeysCount,
+  ERROR_MESSAGES,
+  SSZ_KINDS,
+};

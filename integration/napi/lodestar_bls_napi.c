@@ -289,6 +289,46 @@ static napi_value js_verify_sync(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* sszRoots(handle, kind, objs, domains | null) -> Uint8Array(32 n): computeSigningRoot
+ * (signingRoot.ts:7-13) for n serialized objects of one BLS_SSZ_* kind on the GPU;
+ * domains: 32 bytes for all, 32 per object, or null for the hash_tree_roots.  Synchronous
+ * (a few SHA-256 compressions per object). */
+static napi_value js_ssz_roots(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_handle* h = argc >= 3 ? get_handle(env, argv[0]) : NULL;
+  uint32_t kind = 0;
+  void *objs = NULL, *doms = NULL;
+  size_t ob = 0, db = 0;
+  if (!h || napi_get_value_uint32(env, argv[1], &kind) != napi_ok || view_of(env, argv[2], &objs, &ob) ||
+      (argc > 3 && view_of(env, argv[3], &doms, &db))) {
+    napi_throw_type_error(env, NULL, "sszRoots(handle, kind, Uint8Array, domains)");
+    return NULL;
+  }
+  const uint32_t size = BLS_SSZ_SIZE(kind);
+  if (size == 0 || ob % size) {
+    napi_throw_range_error(env, NULL, "sszRoots: objects are not a whole number of the kind's size");
+    return NULL;
+  }
+  const uint32_t n = (uint32_t)(ob / size);
+  uint32_t stride = 0;
+  if (doms && db == 32ull * n && n != 1) stride = 32;
+  else if (doms && db != 32) {
+    napi_throw_range_error(env, NULL, "sszRoots: domains must be 32 bytes or 32 bytes per object");
+    return NULL;
+  }
+  napi_value ab, out;
+  void* roots;
+  CHECK(env, napi_create_arraybuffer(env, 32 * (size_t)(n ? n : 1), &roots, &ab));
+  CHECK(env, napi_create_typedarray(env, napi_uint8_array, 32 * (size_t)n, ab, 0, &out));
+  if (bls_gpu_ssz_roots(h->ctx, kind, (const uint8_t*)objs, n, (const uint8_t*)doms, stride, (uint8_t*)roots) < 0) {
+    napi_throw_error(env, NULL, bls_gpu_last_error(h->ctx));
+    return NULL;
+  }
+  return out;
+}
+
 static napi_value module_init(napi_env env, napi_value exports) {
   napi_property_descriptor d[] = {
       {"init", NULL, js_init, NULL, NULL, NULL, napi_default, NULL},
@@ -296,6 +336,7 @@ static napi_value module_init(napi_env env, napi_value exports) {
       {"loadPubkeys", NULL, js_load_pubkeys, NULL, NULL, NULL, napi_default, NULL},
       {"verify", NULL, js_verify, NULL, NULL, NULL, napi_default, NULL},
       {"verifySync", NULL, js_verify_sync, NULL, NULL, NULL, napi_default, NULL},
+      {"sszRoots", NULL, js_ssz_roots, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
   return exports;

@@ -47,6 +47,7 @@ SYMBOLS = (
     "bls_gpu_partial",
     "bls_gpu_final_check",
     "bls_gpu_hash_to_g2",
+    "bls_gpu_ssz_roots",
     "bls_gpu_g2_decompress",
     "bls_gpu_aggregate_signatures",
     "bls_gpu_sk_to_pk",
@@ -57,6 +58,16 @@ SYMBOLS = (
     "bls_gpu_coop_probe",
     "bls_gpu_set_debug_flags",
 )
+# SSZ kinds of bls_gpu_ssz_roots (low 8 bits: serialized size)
+SSZ_ROOT = 0x000 | 32
+SSZ_UINT64 = 0x100 | 8
+SSZ_CHECKPOINT = 0x200 | 40
+SSZ_ATTESTATION_DATA = 0x300 | 128
+SSZ_TWO_UINT64 = 0x400 | 16
+SSZ_BEACON_BLOCK_HEADER = 0x500 | 112
+SSZ_DEPOSIT_MESSAGE = 0x600 | 88
+SSZ_FORK_DATA = 0x700 | 36
+SSZ_SIGNING_DATA = 0x800 | 64
 DEBUG_FORCE_EXACT = 1
 DEBUG_NO_MSG_DEDUP = 2
 DEBUG_NO_MERGED_CHECK = 4
@@ -130,6 +141,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_aggregate_signatures.restype = i32
         lib.bls_gpu_hash_to_g2.argtypes = [vp, vp, u32, vp]
         lib.bls_gpu_hash_to_g2.restype = i32
+        lib.bls_gpu_ssz_roots.argtypes = [vp, u32, vp, u32, vp, u32, vp]
+        lib.bls_gpu_ssz_roots.restype = i32
         lib.bls_gpu_sk_to_pk.argtypes = [vp, vp, u32, vp]
         lib.bls_gpu_sk_to_pk.restype = i32
         lib.bls_gpu_sign.argtypes = [vp, vp, vp, u32, vp]

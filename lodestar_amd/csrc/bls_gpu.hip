@@ -1194,6 +1194,36 @@ int bls_gpu_g2_decompress(bls_gpu_ctx* ctx, const uint8_t* in96, uint32_t n, int
   return 0;
 }
 
+int bls_gpu_ssz_roots(bls_gpu_ctx* ctx, uint32_t kind, const uint8_t* objs, uint32_t n, const uint8_t* domains,
+                      uint32_t domain_stride, uint8_t* out32) {
+  CTX_LOCK(ctx);
+  if (!ssz_kind_known(kind) || (domains && domain_stride != 0 && domain_stride != 32)) {
+    snprintf(ctx->err, sizeof(ctx->err), "bls_gpu_ssz_roots: unknown kind 0x%x or domain stride %u", kind,
+             domain_stride);
+    return -2;
+  }
+  HIPC(ctx, hipSetDevice(ctx->device));
+  if (n == 0) return 0;
+  if (!objs || !out32) return -2;
+  const size_t obj_bytes = (size_t)BLS_SSZ_SIZE(kind) * n, dom_bytes = domains ? (domain_stride ? 32ull * n : 32) : 0;
+  Carver cv{nullptr, 0};
+  cv.take<uint8_t>(obj_bytes);
+  cv.take<uint8_t>(dom_bytes);
+  cv.take<uint8_t>(32ull * n);
+  if (ensure_dev(ctx, cv.off)) return -1;
+  Carver c{ctx->dev_ws, 0};
+  uint8_t* d_obj = c.take<uint8_t>(obj_bytes);
+  uint8_t* d_dom = c.take<uint8_t>(dom_bytes);
+  uint8_t* d_out = c.take<uint8_t>(32ull * n);
+  hipStream_t s = ctx->stream;
+  HIPC(ctx, hipMemcpyAsync(d_obj, objs, obj_bytes, hipMemcpyHostToDevice, s));
+  if (domains) HIPC(ctx, hipMemcpyAsync(d_dom, domains, dom_bytes, hipMemcpyHostToDevice, s));
+  HIPC(ctx, launch_k_ssz_roots(kind, d_obj, n, domains ? d_dom : nullptr, domain_stride, d_out, s));
+  HIPC(ctx, hipMemcpyAsync(out32, d_out, 32ull * n, hipMemcpyDeviceToHost, s));
+  HIPC(ctx, hipStreamSynchronize(s));
+  return 0;
+}
+
 int bls_gpu_hash_to_g2(bls_gpu_ctx* ctx, const uint8_t* msgs, uint32_t n, uint8_t* out192) {
   CTX_LOCK(ctx);
   return run_simple(ctx, n, 32, msgs, 0, nullptr, 192, out192, 0);

@@ -32,6 +32,9 @@ hipError_t launch_k_sig_aggregate(const uint8_t* in96, uint32_t n, const uint32_
                                   bls::G2A* pts, int32_t* sig_codes, uint8_t* out96, int32_t* codes, hipStream_t s);
 hipError_t launch_k_g2_decompress(const uint8_t* in96, uint32_t n, int validate, uint8_t* out192, int32_t* codes,
                                   hipStream_t s);
+hipError_t launch_k_ssz_roots(uint32_t kind, const uint8_t* objs, uint32_t n, const uint8_t* domains,
+                              uint32_t domain_stride, uint8_t* out32, hipStream_t s);
+bool ssz_kind_known(uint32_t kind);
 hipError_t launch_k_sk_to_pk(const uint8_t* sks, uint32_t n, uint8_t* out48, hipStream_t s);
 hipError_t launch_k_sign(const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t s);
 hipError_t launch_k_mad_peak(uint64_t* out, uint32_t blocks, uint32_t iters, hipStream_t s);

@@ -234,6 +234,29 @@ class GpuContext:
         self._check(self.lib.bls_gpu_hash_to_g2(self._h, _ptr(m), n, _ptr(out)), "bls_gpu_hash_to_g2")
         return out[: 192 * n].reshape(n, 192)
 
+    def ssz_roots(self, kind: int, objs: bytes | np.ndarray, domains: bytes | np.ndarray | None = None) -> np.ndarray:
+        """computeSigningRoot over n serialized objects of one SSZ kind (bls_gpu_ssz_roots;
+        signingRoot.ts:7-13): n x 32 signing roots, or the objects' hash_tree_roots when
+        domains is None.  domains: one 32-byte domain for all, or 32 bytes per object."""
+        o = _u8(objs)
+        size = kind & 0xFF
+        if o.size % size:
+            raise ValueError(f"objects are {size} bytes each, got {o.size} bytes")
+        n = o.size // size
+        d, stride = None, 0
+        if domains is not None:
+            d = _u8(domains)
+            if d.size == 32:
+                stride = 0
+            elif d.size == 32 * n:
+                stride = 32
+            else:
+                raise ValueError("domains: 32 bytes, or 32 bytes per object")
+        out = np.zeros(32 * max(n, 1), dtype=np.uint8)
+        rc = self.lib.bls_gpu_ssz_roots(self._h, kind, _ptr(o) if n else None, n, _ptr(d), stride, _ptr(out))
+        self._check(rc, "bls_gpu_ssz_roots")
+        return out[: 32 * n].reshape(n, 32)
+
     def g2_decompress(self, sigs96: bytes | np.ndarray, validate: bool = True) -> tuple[np.ndarray, np.ndarray]:
         """Signature.fromBytes(b, affine, validate) for n 96-byte signatures:
         (n x 192 uncompressed bytes, n codes) (bls_gpu_g2_decompress)."""

@@ -20,9 +20,10 @@ pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node
 
 def test_addon_exports():
     code = ("const a = require(process.argv[1]);"
-            "console.log(JSON.stringify(['init','close','loadPubkeys','verify','verifySync'].map(k => typeof a[k])))")
+            "console.log(JSON.stringify(['init','close','loadPubkeys','verify','verifySync','sszRoots']"
+            ".map(k => typeof a[k])))")
     out = subprocess.run([NODE, "-e", code, str(ADDON)], capture_output=True, text=True, timeout=60, check=True)
-    assert json.loads(out.stdout) == ["function"] * 5
+    assert json.loads(out.stdout) == ["function"] * 6
 
 
 @pytest.mark.gpu
@@ -62,3 +63,25 @@ def test_js_adapter_host_side():
     assert r["verdicts_ok"] and r["max_call_sets"] == 1024 and 4 <= r["calls"] <= 6
     assert r["rejected"] == "BLST_ERROR: BLST_INVALID_SIZE" and r["others_true"]
     assert r["closed"] == "QUEUE_ABORTED" and r["inflight_at_close"] == 0
+
+
+@pytest.mark.gpu
+def test_js_signing_roots_kat1(gpu):
+    """GpuBlsVerifier.computeSigningRoots through the addon: KAT-1's deposit signing root
+    (genesisState.test.ts:65-69) and the computeDomain it needs (fork data on the GPU)."""
+    g = json.loads((ROOT / "tests" / "golden" / "ssz_golden.json").read_text())["kat1_deposit"]
+    code = f"""
+const {{GpuBlsVerifier}} = require({json.dumps(str(ROOT / "integration" / "js" / "gpuBlsVerifier.js"))});
+const v = new GpuBlsVerifier({{contexts: 1}});
+const fd = v.computeSigningRoots("forkData", Buffer.from("{g['fork_version']}" + "00".repeat(32), "hex"), null);
+const domain = Buffer.concat([Buffer.from("03000000", "hex"), Buffer.from(fd).subarray(0, 28)]);
+const amount = Buffer.alloc(8); amount.writeUInt32LE({g['amount']} % 2 ** 32, 0); amount.writeUInt32LE(Math.floor({g['amount']} / 2 ** 32), 4);
+const msg = Buffer.concat([Buffer.from("{g['pubkey']}", "hex"), Buffer.from("{g['withdrawal_credentials']}", "hex"), amount]);
+const r = v.computeSigningRoots("depositMessage", msg, domain);
+console.log(JSON.stringify({{domain: domain.toString("hex"), root: Buffer.from(r).toString("hex")}}));
+v.close();
+"""
+    out = subprocess.run([NODE, "-e", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r == {"domain": g["domain"], "root": g["signing_root"]}
