@@ -9,7 +9,11 @@ from __future__ import annotations
 import ctypes
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "_native" / "liblodestar_bls.so"
+import os
+
+# $LODESTAR_BLS_LIB: another build of the same library (A/B measurements, e.g. the
+# 32-bit-digit product variant from `python -m lodestar_amd.build --variant mul32`)
+LIB_PATH = Path(os.environ.get("LODESTAR_BLS_LIB") or Path(__file__).resolve().parent / "_native" / "liblodestar_bls.so")
 
 # verdict / error codes (include/lodestar_bls.h)
 CODE_OK = 0

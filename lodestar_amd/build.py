@@ -37,12 +37,17 @@ def sources() -> list[Path]:
     return [CSRC / "bls_gpu.hip"] + sorted((CSRC / "kernels").glob("*.hip"))
 
 
-def _compile(src: Path, hdr: str, verbose: bool) -> Path:
-    key = hashlib.sha256((hdr + " ".join(FLAGS)).encode() + src.read_bytes()).hexdigest()[:16]
+# A/B build variants: extra defines -> lodestar_amd/_native/liblodestar_bls_<name>.so
+VARIANTS = {"mul32": ["-DBLS_FP_MUL32"]}
+
+
+def _compile(src: Path, hdr: str, verbose: bool, extra: list[str] | None = None) -> Path:
+    flags = FLAGS + (extra or [])
+    key = hashlib.sha256((hdr + " ".join(flags)).encode() + src.read_bytes()).hexdigest()[:16]
     obj = OBJ_DIR / f"{src.stem}.{key}.o"
     if obj.exists():
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj) + ".tmp"]
+    cmd = [HIPCC, *flags, "-c", str(src), "-o", str(obj) + ".tmp"]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -83,27 +88,29 @@ def build_work_model(verbose: bool = True) -> Path:
     return out
 
 
-def build(jobs: int | None = None, verbose: bool = True) -> Path:
+def build(jobs: int | None = None, verbose: bool = True, variant: str | None = None) -> Path:
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
     build_coop_tables(verbose)
     build_work_model(verbose)
     hdr = _headers_digest()
     srcs = sources()
+    extra = VARIANTS[variant] if variant else None
+    lib = OUT_DIR / f"liblodestar_bls_{variant}.so" if variant else LIB
     jobs = jobs or min(len(srcs), os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hdr, verbose, extra), srcs))
     stamp = hashlib.sha256("".join(str(o) for o in objs).encode()).hexdigest()
-    stamp_file = OUT_DIR / ".lib_stamp"
-    if LIB.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
-        return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB) + ".tmp", *map(str, objs)]
+    stamp_file = OUT_DIR / (f".lib_stamp_{variant}" if variant else ".lib_stamp")
+    if lib.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
+        return lib
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib) + ".tmp", *map(str, objs)]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(str(LIB) + ".tmp", LIB)
+    os.replace(str(lib) + ".tmp", lib)
     stamp_file.write_text(stamp)
-    return LIB
+    return lib
 
 
 def build_hostsim(verbose: bool = True) -> Path:
@@ -158,6 +165,9 @@ def build_napi(verbose: bool = True) -> Path | None:
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":
+        build(variant=sys.argv[2])
+        sys.exit(0)
     build(jobs=int(sys.argv[1]) if len(sys.argv) > 1 else None)
     build_napi()
     build_hostsim()

@@ -255,6 +255,109 @@ BLS_HD Fp fp_half(const Fp& a) {
   return r;
 }
 
+// ---------------------------------------------------------------------------
+// Montgomery product over 28-bit digits (the device product; portable, so the host
+// harness checks it against the 64-bit product).  The 12 x 32-bit limbs are re-cut into
+// 14 digits of 28 bits: a 28 x 28-bit product is < 2^56, so a 64-bit column absorbs all
+// of its <= 28 products plus the carry from below without overflowing -- one
+// v_mad_u64_u32 per product and no carry instruction, where 32-bit digits need a
+// v_addc_co_u32 after every product.  196 (a*b) + 196 (m*p) products; the reduction takes
+// 13 digits of 28 bits and one of 20 (R = 2^384, the Montgomery form of the whole
+// library).  Inputs < 3p (< 2^383), output < 2p (9p^2/R + p < 2p); LAZY = false reduces
+// the output to [0, p).
+// ---------------------------------------------------------------------------
+#define BLS_D28_MASK 0xFFFFFFFu
+#define BLS_NP28 0xFFCFFFDu  // -p^-1 mod 2^28
+BLS_HD uint32_t p28_digit(int k) {
+  const uint32_t t[14] = {0xfffaaabu, 0xfefffffu, 0x3ffffb9u, 0xfffeb15u, 0x6241eabu, 0xa0f6b0fu, 0xf6730d2u,
+                          0xf38512bu, 0x4774b84u, 0x4bacd76u, 0xba7b643u, 0xe69a4b1u, 0x1ea397fu, 0x001a011u};
+  return t[k];
+}
+
+BLS_HD void fp_to_d28(const Fp& a, uint32_t d[14]) {
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const int o = 28 * k, w = o >> 5, s = o & 31;
+    const uint64_t pair = ((uint64_t)(w + 1 < 12 ? a.l[w + 1] : 0u) << 32) | a.l[w];
+    d[k] = (uint32_t)(pair >> s) & BLS_D28_MASK;
+  }
+}
+
+// t: the 27 columns of a 14 x 14-digit product; returns t / 2^384 mod p (< 2p)
+BLS_HD Fp fp_redc_d28(uint64_t t[27]) {
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const uint32_t m = ((uint32_t)t[i] * BLS_NP28) & BLS_D28_MASK;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)m * p28_digit(j);
+    t[i + 1] += t[i] >> 28;  // column i is now 0 mod 2^28
+  }
+  {
+    const uint32_t m = ((uint32_t)t[13] * BLS_NP28) & 0xFFFFFu;  // the last 20 bits
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[13 + j] += (uint64_t)m * p28_digit(j);
+  }
+  // result = t[13] / 2^20 + sum_{k >= 14} t[k] 2^(8 + 28 (k - 14)): normalise the
+  // digits from bit 8 on, then pack them into 32-bit limbs
+  const uint64_t u = t[13] >> 20;
+  t[14] += u >> 8;
+#pragma unroll
+  for (int k = 14; k < 26; ++k) {
+    t[k + 1] += t[k] >> 28;
+    t[k] &= BLS_D28_MASK;
+  }
+  Fp r;
+  uint64_t acc = u & 0xFFu;
+  int nb = 8, w = 0;
+#pragma unroll
+  for (int k = 14; k < 27; ++k) {
+    acc |= t[k] << nb;  // t[26] < 2^38 lands at bit 24 of the last two limbs
+    nb += 28;
+    while (nb >= 32 && w < 12) {
+      r.l[w++] = (uint32_t)acc;
+      acc >>= 32;
+      nb -= 32;
+    }
+  }
+  while (w < 12) {
+    r.l[w++] = (uint32_t)acc;
+    acc >>= 32;
+  }
+  return r;
+}
+
+BLS_HD Fp fp_mul_d28_lazy(const Fp& a, const Fp& b) {
+  uint32_t x[14], y[14];
+  fp_to_d28(a, x);
+  fp_to_d28(b, y);
+  uint64_t t[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)x[i] * y[j];
+  return fp_redc_d28(t);
+}
+
+// squaring: 14 squares + 91 cross products against doubled digits (< 2^29)
+BLS_HD Fp fp_sqr_d28_lazy(const Fp& a) {
+  uint32_t x[14], x2[14];
+  fp_to_d28(a, x);
+#pragma unroll
+  for (int k = 0; k < 14; ++k) x2[k] = x[k] << 1;
+  uint64_t t[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    t[2 * i] += (uint64_t)x[i] * x[i];
+#pragma unroll
+    for (int j = i + 1; j < 14; ++j) t[i + j] += (uint64_t)x2[i] * x[j];
+  }
+  return fp_redc_d28(t);
+}
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // gfx950: product-scanning (FIPS) Montgomery product.  Each 32x32 product is one
 // v_mad_u64_u32 into a 64-bit column accumulator whose carry-out (VOP3B sdst) feeds
@@ -412,9 +515,22 @@ __device__ __forceinline__ Fp fp_sqr_cols(const Fp& a) {
 #else
 #define BLS_FP_MUL_ATTR BLS_NOINLINE
 #endif
+// BLS_FP_D28 (a kernel TU that defines it before the includes): the 28-bit-digit
+// product (fp_mul_d28_lazy: ~580 VALU instructions instead of ~740 plus wait states,
+// ~20 % lower latency per product on gfx950).  Opted into by the TUs whose kernels stay
+// within 256 VGPRs (k_pre, the cooperative interpreter kernels); in the 400-512-VGPR
+// point-chain kernels (k_chain, k_gsum) it compiled to code that never finished on
+// gfx950 (ROCm 7.2, BLS_DEBUG_SYNC), so those keep the 32-bit-digit product.
+// BLS_FP_MUL32 (build variant mul32) forces the 32-bit-digit product everywhere.
+#if !defined(BLS_FP_D28) || defined(BLS_FP_MUL32)
 BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_sqr_cols(a); }
 __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul_cols<false>(a, b); }
 __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cols<true>(a, b); }
+#else
+BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_sqr_d28_lazy(a)); }
+__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_d28_lazy(a, b)); }
+__device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_d28_lazy(a, b); }
+#endif
 BLS_FP_MUL_ATTR Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
 #else
 // Host build: Montgomery product a*b/R mod p (R = 2^384) over 6 x 64-bit words,

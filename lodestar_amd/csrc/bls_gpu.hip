@@ -21,6 +21,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <sys/random.h>
+#include <time.h>
 
 #include <dlfcn.h>
 #include <stdlib.h>
@@ -439,6 +440,22 @@ static bool use_sigagg(const bls_gpu_ctx* ctx, uint32_t n) {
   return n >= SIGAGG_MIN_SETS;
 }
 
+// $BLS_DEBUG_SYNC: synchronise after every kernel of a verify call and log its name
+// and wall time to stderr (a kernel that never finishes is the last name printed)
+static void dbg_sync(hipStream_t s, const char* what) {
+  static const bool on = getenv("BLS_DEBUG_SYNC") != nullptr;
+  if (!on) return;
+  timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  fprintf(stderr, "[bls sync] %s ...", what);
+  fflush(stderr);
+  hipError_t e = hipStreamSynchronize(s);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  fprintf(stderr, " %.3f ms %s\n", (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6,
+          hipGetErrorString(e));
+  fflush(stderr);
+}
+
 // Segmented-sum plan for k_gsum over groups of requests: the groups' set indices
 // (group-major) and, per level, (beg, end) segments of at most GSUM_FAN items that
 // never straddle a group; level 0 indexes gsets, level L > 0 the outputs of level
@@ -555,11 +572,11 @@ static int launch_gsum(bls_gpu_ctx* ctx, PipeBufs& b, const GsumPlan& p, const u
   const G2J* in = nullptr;
   for (size_t L = 0; L < levels; ++L) {
     const uint32_t beg = p.level_off[L], n_seg = p.level_off[L + 1] - beg;
-    HIPC(ctx, launch_k_gsum(b, seg_dev + 2 * beg, n_seg, in, tmp[L & 1], s));
+    HIPC(ctx, launch_k_gsum(b, seg_dev + 2 * beg, n_seg, in, tmp[L & 1], s)); dbg_sync(s, "k_gsum");
     in = tmp[L & 1];
   }
   const uint32_t G = levels ? p.level_off[levels] - p.level_off[levels - 1] : 0;
-  HIPC(ctx, launch_k_vset(b, in, G, vbase, s));
+  HIPC(ctx, launch_k_vset(b, in, G, vbase, s)); dbg_sync(s, "k_vset");
   return 0;
 }
 
@@ -792,15 +809,15 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   HIPC(ctx, hipEventRecord(ctx->ev0, s));
   HIPC(ctx, hipEventRecord(ctx->ev[0], s));  // no H2D stage: the kernels read the mapped inputs
   if (n > 0) {
-    HIPC(ctx, launch_k_pk(b, s));  // also resets set_flag, flag_count, the next first_bad_pk slot
+    HIPC(ctx, launch_k_pk(b, s));  // also resets set_flag, flag_count, the next first_bad_pk slot dbg_sync(s, "k_pk");
     ctx->first_bad_slot ^= 1u;
     HIPC(ctx, hipEventRecord(ctx->ev[1], s));
-    HIPC(ctx, launch_k_pre(b, s));
+    HIPC(ctx, launch_k_pre(b, s)); dbg_sync(s, "k_pre");
     HIPC(ctx, hipEventRecord(ctx->ev[2], s));
     if (sigagg) {
       // per-set chains, the chunks' sums of r sig -> virtual sets n + c, then every
       // Miller loop (sets and virtual sets) in one launch
-      HIPC(ctx, launch_k_chain(b, s));
+      HIPC(ctx, launch_k_chain(b, s)); dbg_sync(s, "k_chain");
       if (launch_gsum(ctx, b, chunk_gsum, gseg_dev, gsets_dev, gtmp, n, s)) return -1;
       if (use_units) {
         // sum r_i pk_i per unit (levels over the members), then the units' chain entries
@@ -809,15 +826,15 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
         const size_t levels = unit_gsum.level_off.size() - 1;
         for (size_t L = 0; L < levels; ++L) {
           const uint32_t beg = unit_gsum.level_off[L], n_seg = unit_gsum.level_off[L + 1] - beg;
-          HIPC(ctx, launch_k_gsum1(b, useg_dev + 2 * beg, n_seg, uin, utmp[L & 1], s));
+          HIPC(ctx, launch_k_gsum1(b, useg_dev + 2 * beg, n_seg, uin, utmp[L & 1], s)); dbg_sync(s, "k_gsum1");
           uin = utmp[L & 1];
         }
-        HIPC(ctx, launch_k_uset(b, uin, unit_rep_dev, s));
+        HIPC(ctx, launch_k_uset(b, uin, unit_rep_dev, s)); dbg_sync(s, "k_uset");
         b.gsets = gsets_dev;
       }
-      HIPC(ctx, launch_k_mln(b, ctx->coop, 0, indiv_vbase, s));
+      HIPC(ctx, launch_k_mln(b, ctx->coop, 0, indiv_vbase, s)); dbg_sync(s, "k_mln");
     } else {
-      HIPC(ctx, launch_k_pset(b, ctx->coop, s));
+      HIPC(ctx, launch_k_pset(b, ctx->coop, s)); dbg_sync(s, "k_pset");
     }
     HIPC(ctx, hipEventRecord(ctx->ev[3], s));
     HIPC(ctx, hipEventRecord(ctx->ev[4], s));
@@ -825,7 +842,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   } else {
     for (int i = 1; i <= 5; ++i) HIPC(ctx, hipEventRecord(ctx->ev[i], s));
   }
-  HIPC(ctx, launch_k_status(b, s));
+  HIPC(ctx, launch_k_status(b, s)); dbg_sync(s, "k_status");
   // Merged check: FE(prod of every f_i) == 1 with one final exponentiation (k_fprod
   // tree 1024 -> 16 -> 1), before any per-chunk one.
   const uint32_t n_prod = sigagg ? indiv_vbase : n;  // the f's of every set, chunk group and unit
@@ -833,12 +850,12 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     const Fp12* cur = b.f;
     uint32_t m = n_prod, lvl = 0;
     while (m > FPROD_FAN) {
-      HIPC(ctx, launch_k_fprod(cur, m, ptree[lvl & 1], nullptr, ctx->coop, s));
+      HIPC(ctx, launch_k_fprod(cur, m, ptree[lvl & 1], nullptr, ctx->coop, s)); dbg_sync(s, "k_fprod");
       cur = ptree[lvl & 1];
       m = (m + FPROD_FAN - 1) / FPROD_FAN;
       ++lvl;
     }
-    HIPC(ctx, launch_k_fprod(cur, m, nullptr, merged_ok, ctx->coop, s));
+    HIPC(ctx, launch_k_fprod(cur, m, nullptr, merged_ok, ctx->coop, s)); dbg_sync(s, "k_fprod merged");
     return 0;
   };
   if (merged && launch_merged()) return -1;
@@ -860,8 +877,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     // rare: sets the cooperative kernel could not finish (exceptional additions,
     // infinity signatures, special SSWU inputs) -> exact path, then the status (the
     // exact path may find a signature outside G2) and the merged check again
-    HIPC(ctx, launch_k_exact(b, s));
-    HIPC(ctx, launch_k_status(b, s));
+    HIPC(ctx, launch_k_exact(b, s)); dbg_sync(s, "k_exact");
+    HIPC(ctx, launch_k_status(b, s)); dbg_sync(s, "k_status");
     if (merged && launch_merged()) return -1;
     HIPC(ctx, hipStreamSynchronize(s));
     if (merged) read_merged();
@@ -872,7 +889,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     for (uint32_t ch = 0; ch < n_chunks; ++ch) chunk_ok[ch] = 1;
   } else if (n_chunks > 0 && !partial) {
     // some set is invalid or erroneous (or no merged check): the per-chunk verdicts decide
-    HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s));
+    HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s)); dbg_sync(s, "k_chunk_coop");
     HIPC(ctx, hipStreamSynchronize(s));
     memcpy(chunk_ok.data(), res_host(ctx, b.chunk_ok), sizeof(int32_t) * n_chunks);
   }
@@ -919,7 +936,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     const Fp12* cur = b.f;
     uint32_t m = n_prod, lvl = 0;
     while (m > 1) {
-      HIPC(ctx, launch_k_fprod(cur, m, ptree[lvl & 1], nullptr, ctx->coop, s));
+      HIPC(ctx, launch_k_fprod(cur, m, ptree[lvl & 1], nullptr, ctx->coop, s)); dbg_sync(s, "k_fprod");
       cur = ptree[lvl & 1];
       m = (m + FPROD_FAN - 1) / FPROD_FAN;
       ++lvl;
@@ -954,7 +971,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       if (use_units)
         for (size_t t = plan.nonbatch_reqs.size(); t < indiv.size(); ++t) {
           const uint32_t r = indiv[t], beg = in->req_set_offsets[r];
-          HIPC(ctx, launch_k_mln(b, ctx->coop, beg, in->req_set_offsets[r + 1] - beg, s, true));
+          HIPC(ctx, launch_k_mln(b, ctx->coop, beg, in->req_set_offsets[r + 1] - beg, s, true)); dbg_sync(s, "k_mln own");
         }
       std::vector<uint32_t> goff(indiv.size() + 1);
       for (size_t t = 0; t <= indiv.size(); ++t) goff[t] = (uint32_t)t;
@@ -966,7 +983,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       stage_copy(ctx, gsets_dev, indiv_gsum.gsets.data(), sizeof(uint32_t) * indiv_gsum.gsets.size());
       stage_copy(ctx, gseg_dev, indiv_gsum.seg.data(), sizeof(uint32_t) * indiv_gsum.seg.size());
       if (launch_gsum(ctx, b, indiv_gsum, gseg_dev, gsets_dev, gtmp, indiv_vbase, s)) return -1;
-      HIPC(ctx, launch_k_mln(b, ctx->coop, indiv_vbase, (uint32_t)indiv.size(), s));
+      HIPC(ctx, launch_k_mln(b, ctx->coop, indiv_vbase, (uint32_t)indiv.size(), s)); dbg_sync(s, "k_mln indiv");
     }
     // groups of BLS_FOLD consecutive sets per request, multiplied in parallel first
     bool any_fold = false;
@@ -985,9 +1002,9 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       b.fold = BLS_FOLD;
       b.n_fold = (uint32_t)(groups.size() / 2);
       stage_copy(ctx, b.fold_groups, groups.data(), sizeof(uint32_t) * groups.size());
-      HIPC(ctx, launch_k_fold(b, ctx->coop, s));
+      HIPC(ctx, launch_k_fold(b, ctx->coop, s)); dbg_sync(s, "k_fold");
     }
-    HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, s));
+    HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, s)); dbg_sync(s, "k_indiv_coop");
     HIPC(ctx, hipEventRecord(ctx->ev[8], s));
   }
   HIPC(ctx, hipEventRecord(ctx->ev1, s));

@@ -7,6 +7,7 @@
 // Task: F = prod f_i, verdict = (FE(F) == 1).  Each f_i holds both pairings of its
 // set (k_pset), or (aggregated-signature path, b.sigagg) only e(r pk, H) and the task
 // multiplies in its group's virtual set ML(-g1, sum r_i sig_i).
+#define BLS_FP_D28 1  // 28-bit-digit Montgomery product (bls/field.hpp)
 #include "../launchers.hpp"
 #include "../bls/coop.hpp"
 

@@ -3,6 +3,7 @@
 // exponentiations each) and the signature decompression.  Lanes [0, 2u) map,
 // lanes [2u, 2u + n) decode, so each wavefront runs one kind of work; k_qdup then
 // hands each set its root's points.
+#define BLS_FP_D28 1  // 28-bit-digit Montgomery product (bls/field.hpp)
 #include "../launchers.hpp"
 
 using namespace bls;

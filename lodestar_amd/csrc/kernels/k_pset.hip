@@ -17,6 +17,7 @@
 // (pipeline.hpp stage_exact_set; kept out of this kernel so its registers and
 // stack do not lower this kernel's occupancy).  Flagged sets are counted; the host
 // launches k_exact (and redoes status + chunks) only when the count is non-zero.
+#define BLS_FP_D28 1  // 28-bit-digit Montgomery product (bls/field.hpp)
 #include "../launchers.hpp"
 
 using namespace bls;

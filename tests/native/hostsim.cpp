@@ -74,6 +74,15 @@ unsigned long long hs_fpm_count(void) { return bls_fpm_counter; }
 void hs_fpm_reset(void) { bls_fpm_counter = 0; }
 
 void hs_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_mul(rd_fp(a), rd_fp(b)), out); }
+// the device's 28-bit-digit Montgomery product on raw little-endian limbs (no
+// Montgomery conversion): out = a * b / 2^384 mod p, lazy (< 2p) for inputs < 3p
+void hs_fp_mul_d28_raw(const uint8_t* a, const uint8_t* b, uint8_t* out, int sqr) {
+  Fp x, y;
+  memcpy(x.l, a, 48);
+  memcpy(y.l, b, 48);
+  Fp r = sqr ? fp_sqr_d28_lazy(x) : fp_mul_d28_lazy(x, y);
+  memcpy(out, r.l, 48);
+}
 void hs_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_add(rd_fp(a), rd_fp(b)), out); }
 void hs_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_sub(rd_fp(a), rd_fp(b)), out); }
 void hs_fp_half(const uint8_t* a, uint8_t* out) { wr_fp(fp_half(rd_fp(a)), out); }

@@ -1,6 +1,7 @@
 """The HIP kernels' math compiled for the CPU (tests/native/hostsim.cpp) against the
 oracle and the golden fixtures -- runs without a GPU.  The device build differs only
-in fp_mul (inline-asm product scanning), which tests/test_gpu_parity.py pins."""
+in fp_mul (the 28-bit-digit product, checked here on raw limbs by
+test_fp_mul_d28_lazy, and on the GPU by tests/test_gpu_parity.py)."""
 from __future__ import annotations
 
 import ctypes
@@ -27,6 +28,24 @@ def test_fp_ops(hostsim):
         assert fp(o.raw) == (a - b) % P
     hostsim.hs_fp_inv(b48(12345), o)
     assert fp(o.raw) * 12345 % P == 1
+
+
+def test_fp_mul_d28_lazy(hostsim):
+    """The device Montgomery product (28-bit digits, field.hpp fp_mul_d28_lazy /
+    fp_sqr_d28_lazy) on raw limbs: a * b / 2^384 mod p, output < 2p for inputs < 3p,
+    including the extremes of the lazy range."""
+    rng = random.Random(28)
+    o = _buf(48)
+    rinv = pow(2, -384, P)
+    vals = [0, 1, P - 1, P, 2 * P - 1, 3 * P - 1, 2 ** 382, 3 * P - 2 ** 200]
+    vals += [rng.randrange(3 * P) for _ in range(300)]
+    for k, a in enumerate(vals):
+        b = vals[(7 * k + 3) % len(vals)]
+        for sqr in (0, 1):
+            hostsim.hs_fp_mul_d28_raw(a.to_bytes(48, "little"), b.to_bytes(48, "little"), o, sqr)
+            r = int.from_bytes(o.raw, "little")
+            assert r < 2 * P
+            assert r % P == (a * (a if sqr else b) * rinv) % P
 
 
 def test_fp_inv_gcd(hostsim):
