@@ -236,8 +236,9 @@ def cpu_baseline(sets, raw96, threads: int = 16, seconds: float = 10.0, latency_
 # modes
 # ---------------------------------------------------------------------------
 def timed_calls(ctxs, batches, steps: int):
-    """Every context runs `steps` calls of its batch back to back, all starting at one
-    barrier; returns (elapsed s, mean stage_ms, all verdicts valid)."""
+    """Every context runs `steps` passes of its calls back to back, all starting at one
+    barrier (a pass: one call, or a list of calls submitted together through
+    bls_gpu_verify_many); returns (elapsed s, mean stage_ms, all verdicts valid)."""
     n = len(ctxs)
     start = threading.Barrier(n + 1)
     stage_sum = np.zeros(8)
@@ -249,8 +250,12 @@ def timed_calls(ctxs, batches, steps: int):
         acc = np.zeros(8)
         good = True
         for _ in range(steps):
-            v, st = ctxs[i].verify_packed(batches[i])
-            good = good and bool((v == 1).all())
+            if isinstance(batches[i], list):
+                vs, st = ctxs[i].verify_many(batches[i])
+                good = good and all(bool((v == 1).all()) for v in vs)
+            else:
+                v, st = ctxs[i].verify_packed(batches[i])
+                good = good and bool((v == 1).all())
             acc += np.array(st.stage_ms[:])
         with lock:
             stage_sum[:] += acc
@@ -310,7 +315,10 @@ def main() -> None:
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--inflight", type=int, default=20, help="calls in flight per GPU (contexts / HIP streams)")
+    ap.add_argument("--inflight", type=int, default=8, help="verifier contexts (HIP streams) per GPU")
+    ap.add_argument("--calls-per-pass", type=int, default=4,
+                    help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "
+                         "its own chunks and verdicts)")
     ap.add_argument("--mode", choices=("cfg2", "sharded", "napi"), default="cfg2")
     ap.add_argument("--roots", type=int, default=0,
                     help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
@@ -349,24 +357,34 @@ def main() -> None:
     inflight = args.inflight if args.mode == "cfg2" else 1
     ctxs = [GpuContext(local_rank) for _ in range(inflight)]
     gpu = ctxs[0]
-    works = [make_workload(c, args.sets, rank, args.roots) for c in ctxs]
+    K = max(1, args.calls_per_pass) if args.mode == "cfg2" else 1
+    works = [make_workload(c, args.sets * K, rank, args.roots) for c in ctxs]
+    if K > 1:
+        from lodestar_amd.native import pack_requests as _pack
+
+        # K calls of args.sets distinct sets per context (distinct signing roots, so no
+        # cross-call dedup), each its own message
+        works = [([_pack([(True, [s]) for s in w[2][k * args.sets:(k + 1) * args.sets]]) for k in range(K)],
+                  _pack([(False, w[2][:128])]), w[2][:args.sets], w[3][:args.sets]) for w in works]
     for c in ctxs:
         c.set_debug_flags(flags)
     batch, call128, sets, raw96 = works[0]
+    if isinstance(batch, list):
+        batch = batch[0]  # one call of the pass: the solo-launch roofline probe below
     S = pack_of(args.sets)
     extra = {}
 
     if args.mode == "cfg2":
         for c, w in zip(ctxs, works):
             for _ in range(args.warmup):
-                v, _ = c.verify_packed(w[0])
-                assert (v == 1).all(), "warm-up verification failed"
+                vs = c.verify_many(w[0])[0] if K > 1 else [c.verify_packed(w[0])[0]]
+                assert all((v == 1).all() for v in vs), "warm-up verification failed"
         barrier_sync()
         elapsed, stage_ms, ok = timed_calls(ctxs, [w[0] for w in works], args.steps)
         barrier_sync()
         if not ok:
             raise SystemExit("verification failed inside the timed region")
-        local_sets = args.sets * args.steps * inflight
+        local_sets = args.sets * K * args.steps * inflight
         value, elapsed = global_throughput(local_sets, elapsed, dist, device=device)
         workload = ("cfg2: 1024 single-pubkey gossip sets per call, batchable requests, random-scalar batch in "
                     "chunks of 16 requests" if args.roots == 0 else
@@ -374,8 +392,12 @@ def main() -> None:
                     "roots, batchable requests" + (", root dedup off" if args.no_dedup else ""))
         workload += ", merged check off" if args.no_merged_check else ""
         workload += ", one Miller loop per set" if args.no_units else ""
-        config = {"workload": workload, "sets_per_call": args.sets, "calls_in_flight_per_gpu": inflight,
-                  "sets_per_step_per_gpu": args.sets * inflight, "parallelism": f"shard-by-request x{world}"}
+        if K > 1:
+            workload += (f"; each of the {inflight} contexts submits {K} calls per pass (bls_gpu_verify_many, "
+                         "one device pass, chunks and verdicts per call)")
+        config = {"workload": workload, "sets_per_call": args.sets, "contexts_per_gpu": inflight,
+                  "calls_per_pass": K, "calls_in_flight_per_gpu": inflight * K,
+                  "sets_per_step_per_gpu": args.sets * K * inflight, "parallelism": f"shard-by-request x{world}"}
         scaling = "weak"
     elif args.mode == "sharded":
         # the call: every rank's sets (each rank made its own keys/messages; the call's

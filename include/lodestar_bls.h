@@ -112,6 +112,16 @@ int bls_gpu_validate_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, u
  * verdicts: n_reqs int32 (see top of file).  stats nullable. */
 int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* batch, int32_t* verdicts, bls_stats* stats);
 
+/* Several verifyManySignatureSets messages submitted together (the pool handing one
+ * GPU context every message that is ready): the same verdicts and worker semantics as
+ * n_batches bls_gpu_verify calls -- each message's batchable requests are chunked on
+ * their own -- computed in one pass over the concatenated sets when every message
+ * carries table-index pubkeys (messages with raw pubkeys run one after another).
+ * verdicts: the messages' n_reqs entries concatenated; stats (nullable, one struct):
+ * totals over the messages. */
+int bls_gpu_verify_many(bls_gpu_ctx* ctx, const bls_batch* batches, uint32_t n_batches, int32_t* verdicts,
+                        bls_stats* stats);
+
 /* Sharded call across GPUs (north_star "each GPU reduces its shard to
  * an Fp12 partial, the partials are combined over RCCL/xGMI, and one final
  * exponentiation follows").  The reference verifies one call as ONE random-scalar

@@ -46,6 +46,7 @@ SYMBOLS = (
     "bls_gpu_last_error",
     "bls_gpu_load_pubkeys",
     "bls_gpu_verify",
+    "bls_gpu_verify_many",
     "bls_gpu_aggregate_pubkeys",
     "bls_gpu_validate_pubkeys",
     "bls_gpu_partial",
@@ -131,6 +132,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_load_pubkeys.restype = ctypes.c_int64
         lib.bls_gpu_verify.argtypes = [vp, ctypes.POINTER(BlsBatch), vp, ctypes.POINTER(BlsStats)]
         lib.bls_gpu_verify.restype = i32
+        lib.bls_gpu_verify_many.argtypes = [vp, ctypes.POINTER(BlsBatch), u32, vp, ctypes.POINTER(BlsStats)]
+        lib.bls_gpu_verify_many.restype = i32
         lib.bls_gpu_validate_pubkeys.argtypes = [vp, vp, u32, u32, vp]
         lib.bls_gpu_validate_pubkeys.restype = i32
         lib.bls_gpu_partial.argtypes = [vp, ctypes.POINTER(BlsBatch), u32, vp, vp, vp, ctypes.POINTER(BlsStats)]

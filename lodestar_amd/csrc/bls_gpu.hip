@@ -580,9 +580,32 @@ static int launch_gsum(bls_gpu_ctx* ctx, PipeBufs& b, const GsumPlan& p, const u
   return 0;
 }
 
+// plan_batch over several worker messages submitted together (bls_gpu_verify_many):
+// each message's batchable requests are chunked on their own (worker.ts:56 runs per
+// message), so the chunks never straddle a message; req_bounds[k] = first request of
+// message k, req_bounds[n_msgs] = n_reqs.
+static void plan_batch_msgs(const bls_batch* in, const std::vector<uint32_t>& req_bounds, BatchPlan& p) {
+  p.chunk_off.assign(1, 0);
+  p.chunk_reqs.clear();
+  p.nonbatch_reqs.clear();
+  std::vector<uint32_t> batchable, bounds;
+  for (size_t m = 0; m + 1 < req_bounds.size(); ++m) {
+    batchable.clear();
+    for (uint32_t r = req_bounds[m]; r < req_bounds[m + 1]; ++r) {
+      if (in->req_batchable && in->req_batchable[r]) batchable.push_back(r);
+      else p.nonbatch_reqs.push_back(r);
+    }
+    if (batchable.empty()) continue;
+    chunkify_maximize_chunk_size((uint32_t)batchable.size(), 16, bounds);
+    const uint32_t base = (uint32_t)p.chunk_reqs.size();
+    p.chunk_reqs.insert(p.chunk_reqs.end(), batchable.begin(), batchable.end());
+    for (size_t k = 1; k < bounds.size(); ++k) p.chunk_off.push_back(base + bounds[k]);
+  }
+}
+
 static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats,
                        uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status,
-                       uint32_t* partial_err = nullptr) {
+                       uint32_t* partial_err = nullptr, const std::vector<uint32_t>* req_bounds = nullptr) {
   CTX_LOCK(ctx);
   const bool partial = partial_out != nullptr;
   HIPC(ctx, hipSetDevice(ctx->device));
@@ -621,7 +644,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     }
   }
   BatchPlan plan;
-  plan_batch(in, plan);
+  if (req_bounds) plan_batch_msgs(in, *req_bounds, plan);
+  else plan_batch(in, plan);
   std::vector<uint32_t> msg_uniq, msg_rep;
   const uint32_t n_uniq = (ctx->debug_flags & BLS_DEBUG_NO_MSG_DEDUP) ? n : plan_msg_dedup(in->messages, n, msg_uniq, msg_rep);
   const bool dedup = n_uniq < n;
@@ -1033,6 +1057,87 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
 
 int bls_gpu_verify(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats) {
   return verify_impl(ctx, in, verdicts, stats, 0u, nullptr, nullptr);
+}
+
+int bls_gpu_verify_many(bls_gpu_ctx* ctx, const bls_batch* batches, uint32_t n_batches, int32_t* verdicts,
+                        bls_stats* stats) {
+  if (!ctx || (n_batches && (!batches || !verdicts))) return -2;
+  if (stats) memset(stats, 0, sizeof(*stats));
+  if (n_batches == 0) return 0;
+  if (n_batches == 1) return verify_impl(ctx, batches, verdicts, stats, 0u, nullptr, nullptr);
+  // messages with raw pubkeys keep their own pass: deserializeSet rejects a whole
+  // message (worker.ts:43-46), which the merged pass does not track per message
+  bool merge = true;
+  for (uint32_t k = 0; k < n_batches; ++k) merge = merge && batches[k].set_pk_offsets != nullptr;
+  if (!merge) {
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < n_batches; ++k) {
+      bls_stats st;
+      const int rc = verify_impl(ctx, &batches[k], verdicts + off, stats ? &st : nullptr, 0u, nullptr, nullptr);
+      if (rc != 0) return rc;
+      off += batches[k].n_reqs;
+      if (stats) {
+        stats->batch_retries += st.batch_retries;
+        stats->batch_sigs_success += st.batch_sigs_success;
+        stats->n_chunks += st.n_chunks;
+        stats->n_individual += st.n_individual;
+        stats->n_flagged += st.n_flagged;
+        stats->n_unique_msgs += st.n_unique_msgs;
+        stats->n_ml_units += st.n_ml_units;
+        stats->device_ms += st.device_ms;
+      }
+    }
+    return 0;
+  }
+  // one pass over the concatenated messages (SoA arrays joined, offsets rebased)
+  uint32_t n = 0, R = 0, n_idx = 0;
+  bool lens = false;
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    const bls_batch& b = batches[k];
+    if (b.n_reqs && b.req_set_offsets[b.n_reqs] != b.n_sets) {
+      snprintf(ctx->err, sizeof(ctx->err), "batch %u: req_set_offsets[n_reqs] != n_sets", k);
+      return -2;
+    }
+    n += b.n_sets;
+    R += b.n_reqs;
+    n_idx += b.set_pk_offsets[b.n_sets];
+    lens = lens || b.signature_lens != nullptr;
+  }
+  std::vector<uint32_t> req_off(R + 1, 0), set_pk_off(n + 1, 0), pk_idx(n_idx ? n_idx : 1), sig_lens(lens ? n : 0);
+  std::vector<uint8_t> batchable(R ? R : 1), msgs(32ull * n), sigs(96ull * n);
+  std::vector<uint32_t> req_bounds(1, 0);
+  uint32_t so = 0, ro = 0, io = 0;
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    const bls_batch& b = batches[k];
+    for (uint32_t r = 0; r < b.n_reqs; ++r) {
+      req_off[ro + r + 1] = so + b.req_set_offsets[r + 1];
+      batchable[ro + r] = b.req_batchable ? b.req_batchable[r] : 0;
+    }
+    for (uint32_t i = 0; i < b.n_sets; ++i) set_pk_off[so + i + 1] = io + b.set_pk_offsets[i + 1];
+    if (b.set_pk_offsets[b.n_sets]) memcpy(&pk_idx[io], b.pk_indices, sizeof(uint32_t) * b.set_pk_offsets[b.n_sets]);
+    if (b.n_sets) {
+      memcpy(&msgs[32ull * so], b.messages, 32ull * b.n_sets);
+      memcpy(&sigs[96ull * so], b.signatures, 96ull * b.n_sets);
+    }
+    for (uint32_t i = 0; lens && i < b.n_sets; ++i) sig_lens[so + i] = b.signature_lens ? b.signature_lens[i] : 96u;
+    so += b.n_sets;
+    ro += b.n_reqs;
+    io += b.set_pk_offsets[b.n_sets];
+    req_bounds.push_back(ro);
+  }
+  bls_batch all;
+  memset(&all, 0, sizeof(all));
+  all.n_sets = n;
+  all.n_reqs = R;
+  all.req_set_offsets = req_off.data();
+  all.req_batchable = batchable.data();
+  all.set_pk_offsets = set_pk_off.data();
+  all.pk_indices = pk_idx.data();
+  all.messages = msgs.data();
+  all.signatures = sigs.data();
+  all.signature_lens = lens ? sig_lens.data() : nullptr;
+  all.seed = batches[0].seed;  // scalars: one random batch per pass (verdicts do not depend on them)
+  return verify_impl(ctx, &all, verdicts, stats, 0u, nullptr, nullptr, nullptr, &req_bounds);
 }
 
 int bls_gpu_partial(bls_gpu_ctx* ctx, const bls_batch* in, uint32_t set_index_base, uint8_t* out576,

@@ -184,6 +184,25 @@ class GpuContext:
         self._check(rc, "bls_gpu_verify")
         return verdicts[: pb.n_reqs], stats
 
+    def verify_many(self, pbs: list[PackedBatch]) -> tuple[list[np.ndarray], BlsStats]:
+        """Several worker messages in one submission (bls_gpu_verify_many): per-message
+        verdict arrays (each as verify_packed would return it) and the totals."""
+        structs, keep = (BlsBatch * max(len(pbs), 1))(), []
+        for k, pb in enumerate(pbs):
+            b, kp = self._batch_struct(pb)
+            structs[k] = b
+            keep.append(kp)
+        total = sum(pb.n_reqs for pb in pbs)
+        verdicts = np.zeros(max(total, 1), dtype=np.int32)
+        stats = BlsStats()
+        rc = self.lib.bls_gpu_verify_many(self._h, structs, len(pbs), _ptr(verdicts), ctypes.byref(stats))
+        self._check(rc, "bls_gpu_verify_many")
+        out, off = [], 0
+        for pb in pbs:
+            out.append(verdicts[off: off + pb.n_reqs])
+            off += pb.n_reqs
+        return out, stats
+
     def partial(self, pb: PackedBatch, set_index_base: int):
         """Miller-loop partial of this shard of a sharded call (bls_gpu_partial):
         (576 opaque bytes or None on an error, status 0 / -code, (class, shard-local set

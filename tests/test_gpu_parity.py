@@ -733,3 +733,41 @@ def test_kat3_mainnet_points_gpu_decode(gpu, golden, oracle, table):
     want = [0 if (i - 5) % 37 == 0 and (i - 5) // 37 < len(pts) else 1 for i in range(600)]
     for name, (v, _) in _run_all_paths(gpu, pb).items():
         assert list(v) == want, name
+
+
+def test_verify_many_matches_separate_calls(gpu, oracle, table):
+    """bls_gpu_verify_many: several worker messages in one device pass give each message
+    the verdicts and chunking of its own bls_gpu_verify call (worker.ts:56 chunks per
+    message): messages of 40 / 17 / 33 batchable requests (chunk counts not multiples of
+    16 across the joined list), one with a non-batchable request, invalid sets in two,
+    a 32-byte signature in one; totals of the stats equal the sums; a message with raw
+    pubkeys (deserializeSet per message) runs on its own."""
+    sks = _keys(oracle, 16)
+    sizes = [40, 17, 33]
+    msgs = [[_h(b"many%d-%d" % (k, i)) for i in range(n)] for k, n in enumerate(sizes)]
+    flat = [m for ms in msgs for m in ms]
+    sigs = gpu.sign(b"".join(sks[j % 16] for j in range(len(flat))), b"".join(flat))
+    pbs, j = [], 0
+    bad = {(0, 7), (2, 30)}
+    for k, n in enumerate(sizes):
+        reqs = []
+        for i in range(n):
+            m = msgs[k][i] if (k, i) not in bad else _h(b"tampered%d-%d" % (k, i))
+            s = sigs[j].tobytes() if (k, i) != (1, 3) else bytes(32)
+            reqs.append((not (k == 2 and i == 5), [([j % 16], m, s)]))
+            j += 1
+        pbs.append(pack_requests(reqs))
+    sep = [gpu.verify_packed(pb) for pb in pbs]
+    many, st = gpu.verify_many(pbs)
+    for (v, _), w in zip(sep, many):
+        assert list(v) == list(w)
+    assert many[0][7] == 0 and many[2][30] == 0 and many[1][3] == -CODE_INVALID_SIZE
+    assert st.n_chunks == sum(s.n_chunks for _, s in sep)
+    assert st.batch_retries == sum(s.batch_retries for _, s in sep)
+    assert st.batch_sigs_success == sum(s.batch_sigs_success for _, s in sep)
+    # a raw-pubkey message among them: verified on its own, same verdicts
+    raw, _ = gpu.aggregate_pubkeys([[0], [1]])
+    rawpb = pack_requests([(True, [(raw[0], msgs[0][0], sigs[0].tobytes())]),
+                           (True, [(raw[1], msgs[0][1], sigs[1].tobytes())])])
+    many2, _ = gpu.verify_many([pbs[0], rawpb])
+    assert list(many2[0]) == list(sep[0][0]) and list(many2[1]) == [1, 1]
