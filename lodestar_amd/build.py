@@ -38,7 +38,7 @@ def sources() -> list[Path]:
 
 
 # A/B build variants: extra defines -> lodestar_amd/_native/liblodestar_bls_<name>.so
-VARIANTS = {"mul32": ["-DBLS_FP_MUL32"]}
+VARIANTS = {"mul32": ["-DBLS_FP_MUL32"], "chain_d28": ["-DBLS_CHAIN_D28"]}
 
 
 def _compile(src: Path, hdr: str, verbose: bool, extra: list[str] | None = None) -> Path:

@@ -24,7 +24,12 @@
 // Output per live set (b.chain, CH_* layout); b.chain_live[i] = 1 (k_chain_done).  A
 // set whose request errors (decode status, infinity pubkey) or whose signature is
 // outside G2 gets f_i = 1 and is not live (not summed, no Miller loop).
+#ifdef BLS_CHAIN_D28
+// build variant chain_d28: the 28-bit-digit product, called (not inlined)
+#define BLS_FP_D28 1
+#else
 #define BLS_FP_INLINE 1
+#endif
 #include "../launchers.hpp"
 
 using namespace bls;
