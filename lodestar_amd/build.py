@@ -38,7 +38,8 @@ def sources() -> list[Path]:
 
 
 # A/B build variants: extra defines -> lodestar_amd/_native/liblodestar_bls_<name>.so
-VARIANTS = {"mul32": ["-DBLS_FP_MUL32"], "chain_d28": ["-DBLS_CHAIN_D28"]}
+VARIANTS = {"mul32": ["-DBLS_FP_MUL32", "-DBLS_CHAIN_INL32"], "chain_inl32": ["-DBLS_CHAIN_INL32"],
+            "chain_occ2": ["-DBLS_CHAIN_OCC2"]}
 
 
 def _compile(src: Path, hdr: str, verbose: bool, extra: list[str] | None = None) -> Path:

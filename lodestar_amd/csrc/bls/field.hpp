@@ -517,10 +517,10 @@ __device__ __forceinline__ Fp fp_sqr_cols(const Fp& a) {
 #endif
 // BLS_FP_D28 (a kernel TU that defines it before the includes): the 28-bit-digit
 // product (fp_mul_d28_lazy: ~580 VALU instructions instead of ~740 plus wait states,
-// ~20 % lower latency per product on gfx950).  Opted into by the TUs whose kernels stay
-// within 256 VGPRs (k_pre, the cooperative interpreter kernels); in the 400-512-VGPR
-// point-chain kernels (k_chain, k_gsum) it compiled to code that never finished on
-// gfx950 (ROCm 7.2, BLS_DEBUG_SYNC), so those keep the 32-bit-digit product.
+// ~20 % lower latency per product on gfx950).  Opted into by k_pre, the cooperative
+// interpreter kernels and k_chain (out of line there: inlined into its 512-VGPR chains
+// it compiled to a kernel that never finished on gfx950, ROCm 7.2, BLS_DEBUG_SYNC);
+// the other point-chain kernels keep the 32-bit-digit product.
 // BLS_FP_MUL32 (build variant mul32) forces the 32-bit-digit product everywhere.
 #if !defined(BLS_FP_D28) || defined(BLS_FP_MUL32)
 BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_sqr_cols(a); }

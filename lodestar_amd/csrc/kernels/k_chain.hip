@@ -24,11 +24,15 @@
 // Output per live set (b.chain, CH_* layout); b.chain_live[i] = 1 (k_chain_done).  A
 // set whose request errors (decode status, infinity pubkey) or whose signature is
 // outside G2 gets f_i = 1 and is not live (not summed, no Miller loop).
-#ifdef BLS_CHAIN_D28
-// build variant chain_d28: the 28-bit-digit product, called (not inlined)
-#define BLS_FP_D28 1
-#else
+// The 28-bit-digit product (bls/field.hpp), called out of line: inlined into these
+// chains (512 VGPRs) it compiled to a kernel that never finished on gfx950 (ROCm 7.2,
+// BLS_DEBUG_SYNC); out of line it finishes, 394 VGPRs, and cfg2 runs 1-2 % faster than
+// with the inlined 32-bit-digit product (profiles/r02b_ab_chain_d28.json).  Build
+// variant chain_inl32 restores that one.
+#ifdef BLS_CHAIN_INL32
 #define BLS_FP_INLINE 1
+#else
+#define BLS_FP_D28 1
 #endif
 #include "../launchers.hpp"
 
@@ -97,7 +101,12 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
 //   role 3  RP = [r] pk                                             ~1.0k
 // Results that decide the set's fate go to b.chain_st[4 i + role] (k_chain_done
 // reads them; every role that runs writes its byte, so no clearing is needed).
-__global__ __launch_bounds__(BLS_BLOCK) void k_chain(PipeBufs b, uint32_t blocks_per_role) {
+#ifdef BLS_CHAIN_OCC2  // build variant chain_occ2: at most 256 VGPRs, two wavefronts per SIMD
+#define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#else
+#define BLS_CHAIN_ATTR
+#endif
+__global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, uint32_t blocks_per_role) {
   const uint32_t role = blockIdx.x / blocks_per_role;
   const uint32_t i = (blockIdx.x % blocks_per_role) * BLS_BLOCK + threadIdx.x;
   if (i >= b.n_sets) return;

@@ -16,7 +16,7 @@ fi
 if [ -z "$SKIP_BENCH" ]; then
   timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
   cat $O/bench.json
-  timeout -k 10 400 python -u bench.py --mode napi --steps 8 --warmup 1 > $O/bench_napi.json 2> $O/bench_napi.err || { echo "napi bench failed"; tail -20 $O/bench_napi.err; }
+  timeout -k 10 400 python -u bench.py --mode napi --steps 30 --warmup 1 > $O/bench_napi.json 2> $O/bench_napi.err || { echo "napi bench failed"; tail -20 $O/bench_napi.err; }
   cat $O/bench_napi.json
 fi
 cd /tmp && export TMPDIR=/tmp
@@ -30,7 +30,7 @@ P5="WRITE_SIZE"
 k=0
 for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   k=$((k+1))
-  timeout -s KILL 150 rocprofv3 --pmc $P -d $O/pmc$k -o run --output-format csv -- $B --sets 8192 --inflight 1 --steps 1 --warmup 1 > $O/pmc$k.log 2>&1 || { tail -20 $O/pmc$k.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc $P -d $O/pmc$k -o run --output-format csv -- $B --sets 8192 --inflight 1 --calls-per-pass 1 --steps 1 --warmup 1 > $O/pmc$k.log 2>&1 || { tail -20 $O/pmc$k.log; exit 1; }
 done
 cd $R
 python3 tools/pmc_summary.py $O/pmc_summary.json "one 8192-set cfg2 call (bench.py --sets 8192 --inflight 1): k_chain 512 wavefronts (1 per SIMD, 512 registers), k_mln<4> 2176 wavefronts (2 per SIMD)" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5
