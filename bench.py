@@ -119,12 +119,16 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
     chunks = max(1, n_sets // reqs_per_chunk)
     merged = (n_sets + chunks - 1) * m["fin_fmul"] + m["fin_fe1"] + m["fin_fe2"]
     if sigagg_of(n_sets):
-        ml = m["ml1_4"] / 4
+        # a set's Miller-loop share: four sets of a chunk share one loop (ml1s_4, k_mln's
+        # shared mode, $BLS_ML_SHARED) -- blst's multi-pairing likewise shares f's
+        # squarings; a chunk's signature-sum pair runs a single-pair loop (ml1_4 / 4)
+        ml1 = m["ml1_4"] / 4
+        ml = m["ml1s_4"] / 4 if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
         per = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"] + ml
-               + chunks / n_sets * (ml + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"] + merged / n_sets)
+               + chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"] + merged / n_sets)
         return per, ("k_pre %.0f + k_chain %.0f + k_mln %.0f + chunk sums/ML %.0f + merged check %.0f" %
                      (wm["k_pre"], wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"], ml,
-                      chunks / n_sets * (ml + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"],
+                      chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"],
                       merged / n_sets))
     S = pack_of(n_sets)
     ps = pset_products_per_set(S)
@@ -473,7 +477,7 @@ def main() -> None:
         # the timed region: sets/s per GPU x its MADs per set (launches overlap across the
         # in-flight streams, so wall time per launch = timed region / launches); the solo
         # launch time of one call is reported beside it.
-        fpm_set, fpm_note = work_per_set(args.sets)
+        fpm_set, fpm_note = work_per_set(args.sets * K)  # one device pass: K calls
         mad_set = fpm_set * MADS_PER_FPM
         agg = sigagg_of(args.sets)
         solo = []

@@ -81,6 +81,7 @@ struct CoopEnv {
   // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln):
   // 1 or 2 sets per wavefront (COOP_FRAME), 4 sets (COOP_FRAME2)
   CoopProg ml1_1, ml1_2, ml1_4;
+  CoopProg ml1s_4;  // four pairs of one product domain sharing f (build_ml1_shared)
 };
 
 // fin frame registers

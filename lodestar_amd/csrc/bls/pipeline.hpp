@@ -103,6 +103,11 @@ struct PipeBufs {
   const uint32_t* unit_off;  // n_chunks + 1: chunk c's units [unit_off[c], unit_off[c + 1])
   uint32_t unit_base, n_units;
   uint32_t indiv_vbase;      // f index of individually verified request t's signature sum
+  // Shared Miller loops (k_mln, first pass): ml_dom[item] = the item's product domain
+  // (its chunk, or 0x80000000 | request for a non-batchable request's sets); four
+  // consecutive live items of one domain run ONE loop over their four pairs and keep
+  // the product in the first item's f (the other three f = 1).  Nullable.
+  const uint32_t* ml_dom;
   uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
   uint32_t* flag_count;  // 1 word: sets flagged by the cooperative kernel (GPU path)
   // outputs

@@ -222,7 +222,8 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
               {"pset_add_xr", &ctx->coop.pset_add_xr},   {"pset_phase2", &ctx->coop.pset_phase2},
               {"pset_norm2", &ctx->coop.pset_norm2},     {"pset_affine2", &ctx->coop.pset_affine2},
               {"pset_ml2", &ctx->coop.pset_ml2},         {"ml1_1", &ctx->coop.ml1_1},
-              {"ml1_2", &ctx->coop.ml1_2},               {"ml1_4", &ctx->coop.ml1_4}};
+              {"ml1_2", &ctx->coop.ml1_2},               {"ml1_4", &ctx->coop.ml1_4},
+              {"ml1s_4", &ctx->coop.ml1s_4}};
   ctx->coop_progs = new std::vector<std::pair<std::string, CoopProg>>();
   for (uint32_t k = 0; k < h.n_progs; ++k) {
     CoopProgEntry e;
@@ -456,6 +457,15 @@ static void dbg_sync(hipStream_t s, const char* what) {
   fflush(stderr);
 }
 
+// Shared Miller loops in k_mln (PipeBufs::ml_dom): on unless $BLS_ML_SHARED=0
+static bool ml_shared_on() {
+  static const bool on = [] {
+    const char* e = getenv("BLS_ML_SHARED");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // Segmented-sum plan for k_gsum over groups of requests: the groups' set indices
 // (group-major) and, per level, (beg, end) segments of at most GSUM_FAN items that
 // never straddle a group; level 0 indexes gsets, level L > 0 the outputs of level
@@ -683,6 +693,25 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     return -3;
   }
 
+  // product domain of every first-pass Miller-loop item (sets, chunk signature sums,
+  // units): k_mln shares one loop among four consecutive live items of one domain
+  const bool ml_shared = sigagg && ml_shared_on();
+  std::vector<uint32_t> ml_dom;
+  if (ml_shared) {
+    ml_dom.assign(indiv_vbase, 0xFFFFFFFFu);
+    for (uint32_t ch = 0; ch < n_chunks; ++ch) {
+      for (uint32_t k = plan.chunk_off[ch]; k < plan.chunk_off[ch + 1]; ++k) {
+        const uint32_t r = plan.chunk_reqs[k];
+        for (uint32_t i = in->req_set_offsets[r]; i < in->req_set_offsets[r + 1]; ++i) ml_dom[i] = ch;
+      }
+      ml_dom[n + ch] = ch;
+      if (use_units)
+        for (uint32_t u = units.unit_off[ch]; u < units.unit_off[ch + 1]; ++u) ml_dom[unit_base + u] = ch;
+    }
+    for (uint32_t r : plan.nonbatch_reqs)
+      for (uint32_t i = in->req_set_offsets[r]; i < in->req_set_offsets[r + 1]; ++i) ml_dom[i] = 0x80000000u | r;
+  }
+
   uint32_t seed_words[8];
   {
     uint8_t seed[32];
@@ -718,6 +747,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.sig_lens = in->signature_lens ? c.take<uint32_t>(n) : nullptr;
     b.indiv_reqs = c.take<uint32_t>(R);
     b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
+    b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
     gsets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
     gseg_dev = sigagg ? c.take<uint32_t>(gseg_cap) : nullptr;
     if (use_units) {
@@ -796,6 +826,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     stage_copy(ctx, ugsets_dev, units.members.data(), sizeof(uint32_t) * units.members.size());
     stage_copy(ctx, useg_dev, unit_gsum.seg.data(), sizeof(uint32_t) * unit_gsum.seg.size());
   }
+  if (ml_shared) stage_copy(ctx, b.ml_dom, ml_dom.data(), sizeof(uint32_t) * ml_dom.size());
   if (sigagg) {
     stage_copy(ctx, gsets_dev, chunk_gsum.gsets.data(), sizeof(uint32_t) * chunk_gsum.gsets.size());
     stage_copy(ctx, gseg_dev, chunk_gsum.seg.data(), sizeof(uint32_t) * chunk_gsum.seg.size());
@@ -991,12 +1022,25 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     if (sigagg) {
       // each individually verified request pairs the sum of its own r sig:
       // virtual sets indiv_vbase + t; a request whose sets were paired in their
-      // chunk's units (its chunk failed) now runs their own Miller loops
-      if (use_units)
-        for (size_t t = plan.nonbatch_reqs.size(); t < indiv.size(); ++t) {
-          const uint32_t r = indiv[t], beg = in->req_set_offsets[r];
-          HIPC(ctx, launch_k_mln(b, ctx->coop, beg, in->req_set_offsets[r + 1] - beg, s, true)); dbg_sync(s, "k_mln own");
+      // chunk's units or shared loops (its chunk failed) now runs their own Miller loops
+      if (use_units || ml_shared) {
+        // one launch per run of consecutive sets (a failed chunk's requests are adjacent)
+        uint32_t run_beg = 0, run_end = 0;
+        for (size_t t = plan.nonbatch_reqs.size(); t <= indiv.size(); ++t) {
+          const bool last = t == indiv.size();
+          const uint32_t beg = last ? 0 : in->req_set_offsets[indiv[t]], end = last ? 0 : in->req_set_offsets[indiv[t] + 1];
+          if (!last && run_end > run_beg && beg == run_end) {
+            run_end = end;
+            continue;
+          }
+          if (run_end > run_beg) {
+            HIPC(ctx, launch_k_mln(b, ctx->coop, run_beg, run_end - run_beg, s, true));
+            dbg_sync(s, "k_mln own");
+          }
+          run_beg = beg;
+          run_end = end;
         }
+      }
       std::vector<uint32_t> goff(indiv.size() + 1);
       for (size_t t = 0; t <= indiv.size(); ++t) goff[t] = (uint32_t)t;
       plan_gsum(in, goff, indiv, indiv_gsum);

@@ -101,10 +101,13 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
 //   role 3  RP = [r] pk                                             ~1.0k
 // Results that decide the set's fate go to b.chain_st[4 i + role] (k_chain_done
 // reads them; every role that runs writes its byte, so no clearing is needed).
-#ifdef BLS_CHAIN_OCC2  // build variant chain_occ2: at most 256 VGPRs, two wavefronts per SIMD
-#define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(2)))
-#else
+// At most 256 VGPRs (93 spilled), so two wavefronts share a SIMD: cfg2 +1.2 % over one
+// 394-VGPR wavefront per SIMD (profiles/r02b_ab_chain_occ2.json); build variant
+// chain_occ1 lifts the cap.
+#ifdef BLS_CHAIN_OCC1
 #define BLS_CHAIN_ATTR
+#else
+#define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
 __global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, uint32_t blocks_per_role) {
   const uint32_t role = blockIdx.x / blocks_per_role;

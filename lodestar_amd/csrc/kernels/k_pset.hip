@@ -232,6 +232,13 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
     if (live[s] && first_live < 0) first_live = s;
   }
   if (first_live < 0) return;
+  // shared mode: four live items of one product domain -> one loop, f in the first item
+  bool shared = false;
+  if (S == 4 && units_paired && b.ml_dom && env.ml1s_4.n > 0 && i0 + S <= b.indiv_vbase) {
+    shared = true;
+#pragma unroll
+    for (int s = 0; s < S; ++s) shared = shared && live[s] && b.ml_dom[i0 + s] == b.ml_dom[i0];
+  }
   coop_stage_consts(env, sh.cbank);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
@@ -242,7 +249,12 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
   }
   if (lane == 0) sh.flag = 0;
   __syncthreads();
-  coop_run(env, ml, sh.frame, sh.cbank, &sh.flag);
+  coop_run(env, shared ? env.ml1s_4 : ml, sh.frame, sh.cbank, &sh.flag);
+  if (shared) {
+    if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(sh.frame, ML1_F + lane);
+    else if (lane < 48) reinterpret_cast<Fp*>(&b.f[i0 + 1 + (lane - 12) / 12])[lane % 12] = lane % 12 ? fp_zero() : c_one();
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < S; ++s)
     if (live[s] && lane < 12) reinterpret_cast<Fp*>(&b.f[i0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);

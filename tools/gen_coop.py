@@ -490,6 +490,7 @@ def build_all():
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=2))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, S=4))
+    progs.append(gen_pset.build_ml1_shared(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, S=4))
     return progs, consts
 
 
