@@ -33,6 +33,6 @@ for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   timeout -s KILL 150 rocprofv3 --pmc $P -d $O/pmc$k -o run --output-format csv -- $B --sets 8192 --inflight 1 --calls-per-pass 1 --steps 1 --warmup 1 > $O/pmc$k.log 2>&1 || { tail -20 $O/pmc$k.log; exit 1; }
 done
 cd $R
-python3 tools/pmc_summary.py $O/pmc_summary.json "one 8192-set cfg2 call (bench.py --sets 8192 --inflight 1): k_chain 512 wavefronts (1 per SIMD, 512 registers), k_mln<4> 2176 wavefronts (2 per SIMD)" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5
+python3 tools/pmc_summary.py $O/pmc_summary.json "one 8192-set cfg2 call (bench.py --sets 8192 --inflight 1): k_chain 512 wavefronts (256 VGPRs, 2 per SIMD), k_mln<4> 2176 wavefronts (2 per SIMD), shared 4-pair loops" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5
 python3 tools/trace_timeline.py $(find $O/trace16 -name "*kernel_trace.csv" | head -1) k_mln > $O/timeline.txt
 cat $O/timeline.txt
