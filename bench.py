@@ -119,8 +119,8 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
     chunks = max(1, n_sets // reqs_per_chunk)
     merged = (n_sets + chunks - 1) * m["fin_fmul"] + m["fin_fe1"] + m["fin_fe2"]
     if sigagg_of(n_sets):
-        # a set's Miller-loop share: four sets of a chunk share one loop (ml1s_4, k_mln's
-        # shared mode, $BLS_ML_SHARED) -- blst's multi-pairing likewise shares f's
+        # a set's Miller-loop share: four sets of a chunk share one loop (ml1s_4, k_mln4s /
+        # k_mln's shared mode, $BLS_ML_SHARED) -- blst's multi-pairing likewise shares f's
         # squarings; a chunk's signature-sum pair runs a single-pair loop (ml1_4 / 4)
         ml1 = m["ml1_4"] / 4
         ml = m["ml1s_4"] / 4 if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1

@@ -61,6 +61,8 @@ struct CoopLdsN {
 #define COOP_FRAME2 380  // the 2-set packed programs (tools/gen_coop.py FRAME2): with the
                          // 40-constant bank 20.2 KB of LDS, 8 blocks = 2 wavefronts per SIMD
 #define COOP_FRAME3 640  // the 3-set packed programs (tools/gen_coop.py FRAME3)
+#define COOP_FRAME4S 288  // the shared 4-pair Miller loop ml1s_4 (tools/gen_coop.py FRAME4S):
+                          // 15.7 KB with the bank, 10 wavefronts per CU (k_mln4s)
 
 // Programs of S sets packed in one wavefront (tools/gen_pset.py build_pset(S)):
 // add[(xb << S) | rmask], bit s of rmask = r bit of packed set s; add[0] unused
@@ -355,8 +357,8 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
 // buffers alternate: step s computes from one while step s + 1's ops load into the
 // other.
 template <bool TIMED>
-__device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
-                                        uint32_t* flag, uint64_t* stamps) {
+__device__ __forceinline__ void coop_run_body(const CoopEnv& env, CoopProg pg, Fp* frame, uint32_t* flag,
+                                              uint64_t* stamps) {
   const int lane = threadIdx.x;
   const GlobU4* base = (const GlobU4*)(const void*)env.ops;
   if (pg.n == 0) return;
@@ -377,9 +379,23 @@ __device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* fra
   if (TIMED && lane == 0) stamps[2 * pg.n] = __builtin_amdgcn_s_memtime();
 }
 
+// Out of line: one copy of the interpreter per code object.  Its register count
+// (256 with the default budget) then caps every caller at 2 wavefronts per SIMD.
+template <bool TIMED>
+__device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
+                                        uint32_t* flag, uint64_t* stamps) {
+  coop_run_body<TIMED>(env, pg, frame, flag, stamps);
+}
+
 __device__ __forceinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
                                          uint32_t* flag) {
   coop_run_t<false>(env, pg, frame, cbank, flag, nullptr);
+}
+
+// Inlined into the kernel, so the kernel's own occupancy attribute
+// (amdgpu_waves_per_eu) bounds the interpreter's registers (kernels/k_pset.hip k_mln4s)
+__device__ __forceinline__ void coop_run_inline(const CoopEnv& env, CoopProg pg, Fp* frame, uint32_t* flag) {
+  coop_run_body<false>(env, pg, frame, flag, nullptr);
 }
 
 // copy the constant bank into LDS (once per block)

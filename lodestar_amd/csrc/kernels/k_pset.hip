@@ -213,13 +213,29 @@ __global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
 // A part of the wave with no live set borrows the first live set's inputs.
 enum : int { ML1_SLOTS = 19, ML1_RP = 0, ML1_HQ = 3, ML1_F = 7 };
 
-template <int S, class Lds>
-__global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count,
-                                                    uint32_t units_paired) {
-  __shared__ Lds sh;
+// Whether the four items at i0 (first pass: units paired) are live items of one
+// product domain, so they can share one Miller loop (ml1s_4)
+__device__ __forceinline__ bool mln_shared4(const PipeBufs& b, const CoopEnv& env, uint32_t i0, uint32_t end) {
+  if (!b.ml_dom || env.ml1s_4.n == 0 || i0 + 4u > end || i0 + 4u > b.indiv_vbase) return false;
+  bool shared = true;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint32_t i = i0 + s;
+    shared = shared && b.chain_live[i] && !(b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE) &&
+             b.ml_dom[i] == b.ml_dom[i0];
+  }
+  return shared;
+}
+
+// S items starting at i0 on an LDS frame: the single-pair loops (ml1_S, constants
+// staged at slot cb, the frame size that program was scheduled for) or, for four live
+// items of one product domain, one shared 4-pair loop (ml1s_4, constants at slot
+// COOP_FRAME4S).  The body of k_mln<S>.
+template <int S>
+__device__ __forceinline__ void mln_items(const PipeBufs& b, const CoopEnv& env, Fp* frame, uint32_t* flag,
+                                          int cb, uint32_t i0, uint32_t end, uint32_t units_paired) {
   const CoopProg& ml = S == 1 ? env.ml1_1 : (S == 2 ? env.ml1_2 : env.ml1_4);
   const int lane = threadIdx.x;
-  const uint32_t i0 = first + (uint32_t)S * blockIdx.x, end = first + count;
   bool live[S];
   int first_live = -1;
 #pragma unroll
@@ -233,31 +249,85 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
   }
   if (first_live < 0) return;
   // shared mode: four live items of one product domain -> one loop, f in the first item
-  bool shared = false;
-  if (S == 4 && units_paired && b.ml_dom && env.ml1s_4.n > 0 && i0 + S <= b.indiv_vbase) {
-    shared = true;
-#pragma unroll
-    for (int s = 0; s < S; ++s) shared = shared && live[s] && b.ml_dom[i0 + s] == b.ml_dom[i0];
-  }
-  coop_stage_consts(env, sh.cbank);
+  const bool shared = S == 4 && units_paired && mln_shared4(b, env, i0, end);
+  coop_stage_consts(env, frame + (shared ? COOP_FRAME4S : cb));
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint32_t i = i0 + (live[s] ? s : first_live), o = ML1_SLOTS * s;
     const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
-    if (lane < 3) lds_store_fp(sh.frame, o + ML1_RP + lane, ch[CH_RP + lane]);
-    else if (lane < 7) lds_store_fp(sh.frame, o + ML1_HQ + lane - 3, ch[CH_HQ + lane - 3]);
+    if (lane < 3) lds_store_fp(frame, o + ML1_RP + lane, ch[CH_RP + lane]);
+    else if (lane < 7) lds_store_fp(frame, o + ML1_HQ + lane - 3, ch[CH_HQ + lane - 3]);
   }
-  if (lane == 0) sh.flag = 0;
+  if (lane == 0) *flag = 0;
   __syncthreads();
-  coop_run(env, shared ? env.ml1s_4 : ml, sh.frame, sh.cbank, &sh.flag);
+  coop_run(env, shared ? env.ml1s_4 : ml, frame, frame + (shared ? COOP_FRAME4S : cb), flag);
   if (shared) {
-    if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(sh.frame, ML1_F + lane);
+    if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(frame, ML1_F + lane);
     else if (lane < 48) reinterpret_cast<Fp*>(&b.f[i0 + 1 + (lane - 12) / 12])[lane % 12] = lane % 12 ? fp_zero() : c_one();
     return;
   }
 #pragma unroll
   for (int s = 0; s < S; ++s)
-    if (live[s] && lane < 12) reinterpret_cast<Fp*>(&b.f[i0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);
+    if (live[s] && lane < 12) reinterpret_cast<Fp*>(&b.f[i0 + s])[lane] = coop_get(frame, ML1_SLOTS * s + ML1_F + lane);
+}
+
+template <int S, class Lds>
+__global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count,
+                                                    uint32_t units_paired) {
+  __shared__ Lds sh;
+  mln_items<S>(b, env, sh.frame, &sh.flag, (int)(sizeof(sh.frame) / sizeof(Fp)), first + (uint32_t)S * blockIdx.x,
+               first + count, units_paired);
+}
+
+// The real sets of the first pass, four per wavefront on the small frame
+// (COOP_FRAME4S: 15.7 KB of LDS, 10 wavefronts per CU instead of 8): four live sets
+// of one chunk run the shared 4-pair loop (ml1s_4); otherwise each pair of items runs
+// the single-pair ml1_2 program (256-slot frame, constants at slot COOP_FRAME).  The
+// interpreter is inlined once here so the occupancy attribute bounds its registers
+// (141 VGPRs, 3 wavefronts per SIMD; the out-of-line copy takes 256 and 2).
+#ifndef BLS_MLN4S_WAVES
+#define BLS_MLN4S_WAVES 3
+#endif
+__global__ __launch_bounds__(COOP_LANES) __attribute__((amdgpu_waves_per_eu(BLS_MLN4S_WAVES, BLS_MLN4S_WAVES)))
+void k_mln4s(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count) {
+  __shared__ CoopLdsN<COOP_FRAME4S> sh;
+  const int lane = threadIdx.x;
+  const uint32_t i0 = first + 4u * blockIdx.x, end = first + count;
+  const bool sh4 = mln_shared4(b, env, i0, end);
+  const int n = sh4 ? 4 : 2, cb = sh4 ? COOP_FRAME4S : COOP_FRAME;
+  for (uint32_t h = 0; h < (sh4 ? 1u : 2u); ++h) {
+    const uint32_t j0 = i0 + 2u * h;
+    bool live[4];
+    int first_live = -1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t i = j0 + s;
+      live[s] = s < n && i < end && b.chain_live[i] && !(b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE);
+      if (live[s] && first_live < 0) first_live = s;
+    }
+    if (first_live < 0) continue;
+    __syncthreads();
+    coop_stage_consts(env, sh.frame + cb);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s >= n) break;
+      const uint32_t i = j0 + (live[s] ? s : first_live), o = ML1_SLOTS * s;
+      const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
+      if (lane < 3) lds_store_fp(sh.frame, o + ML1_RP + lane, ch[CH_RP + lane]);
+      else if (lane < 7) lds_store_fp(sh.frame, o + ML1_HQ + lane - 3, ch[CH_HQ + lane - 3]);
+    }
+    if (lane == 0) sh.flag = 0;
+    __syncthreads();
+    coop_run_inline(env, sh4 ? env.ml1s_4 : env.ml1_2, sh.frame, &sh.flag);
+    if (sh4) {
+      if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(sh.frame, ML1_F + lane);
+      else if (lane < 48) reinterpret_cast<Fp*>(&b.f[i0 + 1 + (lane - 12) / 12])[lane % 12] = lane % 12 ? fp_zero() : c_one();
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        if (live[s] && lane < 12) reinterpret_cast<Fp*>(&b.f[j0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);
+    }
+  }
 }
 
 // Sets per wavefront for a batch: 1 for small batches (latency: one wave per set
@@ -296,7 +366,18 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
                         bool own_only) {
   if (count == 0) return hipSuccess;
   const uint32_t S = ml_pack(b), up = own_only ? 0u : 1u;
-  if (S == 4 && env.ml1_4.n > 0) {
+  static const bool small_frame = [] {
+    const char* e = getenv("BLS_ML_SMALL_FRAME");
+    return !(e && e[0] == '0');
+  }();
+  if (S == 4 && up && small_frame && b.ml_dom && env.ml1s_4.n > 0 && env.ml1_2.n > 0) {
+    // first pass: the real sets on the small frame, the virtual items (chunk signature
+    // sums, Miller-loop units) on the 380-slot frame (ml1_4 when they cannot share)
+    const uint32_t end = first + count, mid = b.n_sets <= first ? first : (b.n_sets < end ? b.n_sets : end);
+    if (mid > first) k_mln4s<<<(mid - first + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, mid - first);
+    if (end > mid)
+      k_mln<4, CoopLdsN<COOP_FRAME2>><<<(end - mid + 3) / 4, COOP_LANES, 0, s>>>(b, env, mid, end - mid, up);
+  } else if (S == 4 && env.ml1_4.n > 0) {
     k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count, up);
   } else if (S == 2 && env.ml1_2.n > 0) {
     k_mln<2, CoopLds><<<(count + 1) / 2, COOP_LANES, 0, s>>>(b, env, first, count, up);

@@ -112,6 +112,7 @@ def test_ml1_shared_equals_product_of_single_loops(progs, oracle):
     pg, consts = progs
     rng = random.Random(21)
     frame = [0] * GC.FRAME2
+    assert pg["ml1s_4"].n_slots == GC.FRAME4S
     for s in range(4):
         o = PS.ML1_SLOTS * s
         k1, k2 = rng.randrange(1, oracle.R), rng.randrange(1, oracle.R)
@@ -131,3 +132,4 @@ def test_ml1_shared_equals_product_of_single_loops(progs, oracle):
     for s in range(1, 4):
         prod = oracle.f12_mul(prod, f12(single, PS.ML1_SLOTS * s + PS.ML1_F))
     assert f12(shared, PS.ML1_F) == prod
+

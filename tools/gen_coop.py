@@ -31,6 +31,7 @@ X_ABS = 0xD201000000010000
 FRAME = 256
 FRAME2 = 380   # frame of the 2-set programs (kernels/k_pset.hip, CoopLdsN<COOP_FRAME2>; 2 waves/SIMD)
 FRAME3 = 640   # frame of the 3-set programs (CoopLdsN<COOP_FRAME3>)
+FRAME4S = 288  # frame of the shared 4-pair Miller loop (k_mln4s, CoopLdsN<COOP_FRAME4S>; 10 waves / CU)
 MONT_R = 1 << 384
 
 # "fin" frame registers
@@ -490,7 +491,9 @@ def build_all():
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=2))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, S=4))
-    progs.append(gen_pset.build_ml1_shared(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, S=4))
+    # the shared 4-pair loop in the smallest frame it fits without extra steps (747
+    # steps at 288 slots as at 380): its LDS sets the occupancy of the k_mln4s launch
+    progs.append(gen_pset.build_ml1_shared(consts, T, miller_dbl, miller_add, X_ABS, FRAME4S, S=4))
     return progs, consts
 
 
