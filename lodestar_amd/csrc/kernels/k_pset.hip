@@ -279,23 +279,28 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
                first + count, units_paired);
 }
 
-// The real sets of the first pass, four per wavefront on the small frame
-// (COOP_FRAME4S: 15.7 KB of LDS, 10 wavefronts per CU instead of 8): four live sets
-// of one chunk run the shared 4-pair loop (ml1s_4); otherwise each pair of items runs
-// the single-pair ml1_2 program (256-slot frame, constants at slot COOP_FRAME).  The
-// interpreter is inlined once here so the occupancy attribute bounds its registers
-// (141 VGPRs, 3 wavefronts per SIMD; the out-of-line copy takes 256 and 2).
+// First-pass Miller loops on the small frame (COOP_FRAME4S: 15.7 KB of LDS, 10
+// wavefronts per CU instead of 8), one launch: blocks [0, G) take the real sets
+// [first, mid) four at a time -- four live sets of one chunk run the shared 4-pair
+// loop (ml1s_4), otherwise each pair runs ml1_2 -- and blocks [G, G + V) take one
+// virtual item of [mid, mid + V) each (chunk signature sums, units: ml1_1, 408 steps,
+// so they finish with the shared loops' 747 instead of trailing them).  The
+// interpreter is inlined once, so the occupancy attribute bounds its registers.
 #ifndef BLS_MLN4S_WAVES
 #define BLS_MLN4S_WAVES 3
 #endif
 __global__ __launch_bounds__(COOP_LANES) __attribute__((amdgpu_waves_per_eu(BLS_MLN4S_WAVES, BLS_MLN4S_WAVES)))
-void k_mln4s(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count) {
+void k_mln4s(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_virt) {
   __shared__ CoopLdsN<COOP_FRAME4S> sh;
   const int lane = threadIdx.x;
-  const uint32_t i0 = first + 4u * blockIdx.x, end = first + count;
-  const bool sh4 = mln_shared4(b, env, i0, end);
-  const int n = sh4 ? 4 : 2, cb = sh4 ? COOP_FRAME4S : COOP_FRAME;
-  for (uint32_t h = 0; h < (sh4 ? 1u : 2u); ++h) {
+  const uint32_t G = (mid - first + 3u) / 4u;
+  const bool virt = blockIdx.x >= G;
+  const uint32_t i0 = virt ? mid + (blockIdx.x - G) : first + 4u * blockIdx.x;
+  const uint32_t end = virt ? mid + n_virt : mid;
+  const bool sh4 = !virt && mln_shared4(b, env, i0, end);
+  const int n = virt ? 1 : (sh4 ? 4 : 2), cb = sh4 ? COOP_FRAME4S : COOP_FRAME;
+  const CoopProg pg = virt ? env.ml1_1 : (sh4 ? env.ml1s_4 : env.ml1_2);
+  for (uint32_t h = 0; h < ((virt || sh4) ? 1u : 2u); ++h) {
     const uint32_t j0 = i0 + 2u * h;
     bool live[4];
     int first_live = -1;
@@ -318,14 +323,15 @@ void k_mln4s(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count) {
     }
     if (lane == 0) sh.flag = 0;
     __syncthreads();
-    coop_run_inline(env, sh4 ? env.ml1s_4 : env.ml1_2, sh.frame, &sh.flag);
+    coop_run_inline(env, pg, sh.frame, &sh.flag);
     if (sh4) {
       if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(sh.frame, ML1_F + lane);
       else if (lane < 48) reinterpret_cast<Fp*>(&b.f[i0 + 1 + (lane - 12) / 12])[lane % 12] = lane % 12 ? fp_zero() : c_one();
     } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        if (live[s] && lane < 12) reinterpret_cast<Fp*>(&b.f[j0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);
+        if (s < n && live[s] && lane < 12)
+          reinterpret_cast<Fp*>(&b.f[j0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);
     }
   }
 }
@@ -371,12 +377,10 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
     return !(e && e[0] == '0');
   }();
   if (S == 4 && up && small_frame && b.ml_dom && env.ml1s_4.n > 0 && env.ml1_2.n > 0) {
-    // first pass: the real sets on the small frame, the virtual items (chunk signature
-    // sums, Miller-loop units) on the 380-slot frame (ml1_4 when they cannot share)
+    // first pass: the real sets four per wavefront, the virtual items (chunk signature
+    // sums, Miller-loop units) one per wavefront, in one launch
     const uint32_t end = first + count, mid = b.n_sets <= first ? first : (b.n_sets < end ? b.n_sets : end);
-    if (mid > first) k_mln4s<<<(mid - first + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, mid - first);
-    if (end > mid)
-      k_mln<4, CoopLdsN<COOP_FRAME2>><<<(end - mid + 3) / 4, COOP_LANES, 0, s>>>(b, env, mid, end - mid, up);
+    k_mln4s<<<(mid - first + 3) / 4 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid);
   } else if (S == 4 && env.ml1_4.n > 0) {
     k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count, up);
   } else if (S == 2 && env.ml1_2.n > 0) {
