@@ -490,10 +490,11 @@ def main() -> None:
         per_gpu = value / world
         achieved = per_gpu * mad_set / 1e12
         if rank == 0:
-            kern = "k_mln<4>" if agg else (f"k_psetn<{S}" if S > 1 else "k_pset")
+            small = os.environ.get("BLS_ML_SMALL_FRAME", "1") != "0"
+            kern = ("k_mln4s" if small else "k_mln<4>") if agg else (f"k_psetn<{S}" if S > 1 else "k_pset")
             pmc = pmc_summary(kern.rstrip(">") if agg else kern)
             roof = {"bound": "valu",
-                    "kernel": ("every kernel of the call; dominant: k_mln<4> (cooperative Miller loops) and k_chain "
+                    "kernel": (f"every kernel of the call; dominant: {kern} (cooperative Miller loops) and k_chain "
                                "(scalar chains, one lane per set)") if agg else kern,
                     "achieved": round(achieved, 4),
                     "peak": round(peak, 3), "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5),
