@@ -322,7 +322,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--inflight", type=int, default=8, help="verifier contexts (HIP streams) per GPU")
-    ap.add_argument("--calls-per-pass", type=int, default=4,
+    # default 8 x 8: the knee of profiles/r02c_knee.json (8 x 4 1.46M at 22 ms per pass,
+    # 8 x 6 1.64M at 30 ms, 8 x 8 1.72M at 38 ms, 8 x 10 1.73M at 47 ms); a call's verdicts
+    # arrive when its pass ends, well inside the reference's 100 ms job buffering
+    # (multithread/index.ts:57 MAX_BUFFER_WAIT_MS)
+    ap.add_argument("--calls-per-pass", type=int, default=8,
                     help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "
                          "its own chunks and verdicts)")
     ap.add_argument("--mode", choices=("cfg2", "sharded", "napi"), default="cfg2")
@@ -404,7 +408,8 @@ def main() -> None:
                          "one device pass, chunks and verdicts per call)")
         config = {"workload": workload, "sets_per_call": args.sets, "contexts_per_gpu": inflight,
                   "calls_per_pass": K, "calls_in_flight_per_gpu": inflight * K,
-                  "sets_per_step_per_gpu": args.sets * K * inflight, "parallelism": f"shard-by-request x{world}"}
+                  "sets_per_step_per_gpu": args.sets * K * inflight, "parallelism": f"shard-by-request x{world}",
+                  "call_latency_ms": round(elapsed / max(1, args.steps) * 1e3, 3)}
         scaling = "weak"
     elif args.mode == "sharded":
         # the call: every rank's sets (each rank made its own keys/messages; the call's
