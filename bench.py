@@ -119,11 +119,14 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
     chunks = max(1, n_sets // reqs_per_chunk)
     merged = (n_sets + chunks - 1) * m["fin_fmul"] + m["fin_fe1"] + m["fin_fe2"]
     if sigagg_of(n_sets):
-        # a set's Miller-loop share: four sets of a chunk share one loop (ml1s_4, k_mln4s /
-        # k_mln's shared mode, $BLS_ML_SHARED) -- blst's multi-pairing likewise shares f's
-        # squarings; a chunk's signature-sum pair runs a single-pair loop (ml1_4 / 4)
+        # a set's Miller-loop share: eight sets of a chunk share one loop (ml1s_8, k_mlns<8>;
+        # four with $BLS_ML_SHARE=4 or without the small frame; none with
+        # $BLS_ML_SHARED=0) -- blst's multi-pairing likewise shares f's squarings; a
+        # chunk's signature-sum pair runs a single-pair loop (ml1_4 / 4)
         ml1 = m["ml1_4"] / 4
-        ml = m["ml1s_4"] / 4 if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
+        sh8 = (os.environ.get("BLS_ML_SHARE") != "4" and os.environ.get("BLS_ML_SMALL_FRAME", "1") != "0"
+               and "ml1s_8" in m)
+        ml = (m["ml1s_8"] / 8 if sh8 else m["ml1s_4"] / 4) if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
         per = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"] + ml
                + chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"] + merged / n_sets)
         return per, ("k_pre %.0f + k_chain %.0f + k_mln %.0f + chunk sums/ML %.0f + merged check %.0f" %
@@ -496,7 +499,8 @@ def main() -> None:
         achieved = per_gpu * mad_set / 1e12
         if rank == 0:
             small = os.environ.get("BLS_ML_SMALL_FRAME", "1") != "0"
-            kern = ("k_mln4s" if small else "k_mln<4>") if agg else (f"k_psetn<{S}" if S > 1 else "k_pset")
+            share = "4" if os.environ.get("BLS_ML_SHARE") == "4" else "8"
+            kern = (f"k_mlns<{share}>" if small else "k_mln<4>") if agg else (f"k_psetn<{S}" if S > 1 else "k_pset")
             pmc = pmc_summary(kern.rstrip(">") if agg else kern)
             roof = {"bound": "valu",
                     "kernel": (f"every kernel of the call; dominant: {kern} (cooperative Miller loops) and k_chain "

@@ -62,7 +62,8 @@ struct CoopLdsN {
                          // 40-constant bank 20.2 KB of LDS, 8 blocks = 2 wavefronts per SIMD
 #define COOP_FRAME3 640  // the 3-set packed programs (tools/gen_coop.py FRAME3)
 #define COOP_FRAME4S 288  // the shared 4-pair Miller loop ml1s_4 (tools/gen_coop.py FRAME4S):
-                          // 15.7 KB with the bank, 10 wavefronts per CU (k_mln4s)
+                          // 15.7 KB with the bank, 10 wavefronts per CU (k_mlns<4>)
+#define COOP_FRAME8S 512  // the shared 8-pair loop ml1s_8 (FRAME8S): 26.5 KB, 6 per CU
 
 // Programs of S sets packed in one wavefront (tools/gen_pset.py build_pset(S)):
 // add[(xb << S) | rmask], bit s of rmask = r bit of packed set s; add[0] unused
@@ -84,6 +85,7 @@ struct CoopEnv {
   // 1 or 2 sets per wavefront (COOP_FRAME), 4 sets (COOP_FRAME2)
   CoopProg ml1_1, ml1_2, ml1_4;
   CoopProg ml1s_4;  // four pairs of one product domain sharing f (build_ml1_shared)
+  CoopProg ml1s_8;  // eight pairs sharing f (kernels/k_pset.hip k_mlns<8>)
 };
 
 // fin frame registers
@@ -393,7 +395,7 @@ __device__ __forceinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* fr
 }
 
 // Inlined into the kernel, so the kernel's own occupancy attribute
-// (amdgpu_waves_per_eu) bounds the interpreter's registers (kernels/k_pset.hip k_mln4s)
+// (amdgpu_waves_per_eu) bounds the interpreter's registers (kernels/k_pset.hip k_mlns)
 __device__ __forceinline__ void coop_run_inline(const CoopEnv& env, CoopProg pg, Fp* frame, uint32_t* flag) {
   coop_run_body<false>(env, pg, frame, flag, nullptr);
 }

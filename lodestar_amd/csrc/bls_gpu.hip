@@ -223,7 +223,7 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
               {"pset_norm2", &ctx->coop.pset_norm2},     {"pset_affine2", &ctx->coop.pset_affine2},
               {"pset_ml2", &ctx->coop.pset_ml2},         {"ml1_1", &ctx->coop.ml1_1},
               {"ml1_2", &ctx->coop.ml1_2},               {"ml1_4", &ctx->coop.ml1_4},
-              {"ml1s_4", &ctx->coop.ml1s_4}};
+              {"ml1s_4", &ctx->coop.ml1s_4},             {"ml1s_8", &ctx->coop.ml1s_8}};
   ctx->coop_progs = new std::vector<std::pair<std::string, CoopProg>>();
   for (uint32_t k = 0; k < h.n_progs; ++k) {
     CoopProgEntry e;

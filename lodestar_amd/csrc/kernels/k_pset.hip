@@ -213,13 +213,15 @@ __global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
 // A part of the wave with no live set borrows the first live set's inputs.
 enum : int { ML1_SLOTS = 19, ML1_RP = 0, ML1_HQ = 3, ML1_F = 7 };
 
-// Whether the four items at i0 (first pass: units paired) are live items of one
-// product domain, so they can share one Miller loop (ml1s_4)
-__device__ __forceinline__ bool mln_shared4(const PipeBufs& b, const CoopEnv& env, uint32_t i0, uint32_t end) {
-  if (!b.ml_dom || env.ml1s_4.n == 0 || i0 + 4u > end || i0 + 4u > b.indiv_vbase) return false;
+// Whether the SH items at i0 (first pass: units paired) are live items of one
+// product domain, so they can share one Miller loop (ml1s_4 / ml1s_8)
+template <int SH>
+__device__ __forceinline__ bool mln_shared(const PipeBufs& b, const CoopEnv& env, uint32_t i0, uint32_t end) {
+  const CoopProg& pg = SH == 8 ? env.ml1s_8 : env.ml1s_4;
+  if (!b.ml_dom || pg.n == 0 || i0 + (uint32_t)SH > end || i0 + (uint32_t)SH > b.indiv_vbase) return false;
   bool shared = true;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < SH; ++s) {
     const uint32_t i = i0 + s;
     shared = shared && b.chain_live[i] && !(b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE) &&
              b.ml_dom[i] == b.ml_dom[i0];
@@ -249,7 +251,7 @@ __device__ __forceinline__ void mln_items(const PipeBufs& b, const CoopEnv& env,
   }
   if (first_live < 0) return;
   // shared mode: four live items of one product domain -> one loop, f in the first item
-  const bool shared = S == 4 && units_paired && mln_shared4(b, env, i0, end);
+  const bool shared = S == 4 && units_paired && mln_shared<4>(b, env, i0, end);
   coop_stage_consts(env, frame + (shared ? COOP_FRAME4S : cb));
 #pragma unroll
   for (int s = 0; s < S; ++s) {
@@ -279,33 +281,38 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
                first + count, units_paired);
 }
 
-// First-pass Miller loops on the small frame (COOP_FRAME4S: 15.7 KB of LDS, 10
-// wavefronts per CU instead of 8), one launch: blocks [0, G) take the real sets
-// [first, mid) four at a time -- four live sets of one chunk run the shared 4-pair
-// loop (ml1s_4), otherwise each pair runs ml1_2 -- and blocks [G, G + V) take one
-// virtual item of [mid, mid + V) each (chunk signature sums, units: ml1_1, 408 steps,
-// so they finish with the shared loops' 747 instead of trailing them).  The
-// interpreter is inlined once, so the occupancy attribute bounds its registers.
+// First-pass Miller loops, one launch: blocks [0, G) take the real sets [first, mid)
+// SH at a time -- SH live sets of one chunk run one shared SH-pair loop (ml1s_SH),
+// otherwise each pair runs ml1_2 -- and blocks [G, G + V) take one virtual item of
+// [mid, mid + V) each (chunk signature sums, units: ml1_1, 408 steps, so they finish
+// with the shared loops instead of trailing them).  SH = 4: the 288-slot frame
+// (COOP_FRAME4S, 15.7 KB of LDS, 10 wavefronts per CU instead of 8 at 380 slots);
+// SH = 8: 512 slots (26.5 KB, 6 per CU), 24 % fewer interpreter steps per set.  The
+// interpreter is inlined once, so the occupancy attribute bounds its registers (163
+// VGPRs, 3 wavefronts per SIMD; the out-of-line copy takes 256 and 2).
 #ifndef BLS_MLN4S_WAVES
 #define BLS_MLN4S_WAVES 3
 #endif
-__global__ __launch_bounds__(COOP_LANES) __attribute__((amdgpu_waves_per_eu(BLS_MLN4S_WAVES, BLS_MLN4S_WAVES)))
-void k_mln4s(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_virt) {
-  __shared__ CoopLdsN<COOP_FRAME4S> sh;
+// (SH = 8: the LDS caps it at 1.5 per SIMD, so the register budget is 2)
+template <int SH>
+__global__ __launch_bounds__(COOP_LANES)
+__attribute__((amdgpu_waves_per_eu(SH == 8 ? 2 : BLS_MLN4S_WAVES, SH == 8 ? 2 : BLS_MLN4S_WAVES)))
+void k_mlns(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_virt) {
+  __shared__ CoopLdsN<SH == 8 ? COOP_FRAME8S : COOP_FRAME4S> sh;
   const int lane = threadIdx.x;
-  const uint32_t G = (mid - first + 3u) / 4u;
+  const uint32_t G = (mid - first + (uint32_t)SH - 1u) / (uint32_t)SH;
   const bool virt = blockIdx.x >= G;
-  const uint32_t i0 = virt ? mid + (blockIdx.x - G) : first + 4u * blockIdx.x;
+  const uint32_t i0 = virt ? mid + (blockIdx.x - G) : first + (uint32_t)SH * blockIdx.x;
   const uint32_t end = virt ? mid + n_virt : mid;
-  const bool sh4 = !virt && mln_shared4(b, env, i0, end);
-  const int n = virt ? 1 : (sh4 ? 4 : 2), cb = sh4 ? COOP_FRAME4S : COOP_FRAME;
-  const CoopProg pg = virt ? env.ml1_1 : (sh4 ? env.ml1s_4 : env.ml1_2);
-  for (uint32_t h = 0; h < ((virt || sh4) ? 1u : 2u); ++h) {
+  const bool shd = !virt && mln_shared<SH>(b, env, i0, end);
+  const int n = virt ? 1 : (shd ? SH : 2), cb = shd ? (SH == 8 ? COOP_FRAME8S : COOP_FRAME4S) : COOP_FRAME;
+  const CoopProg pg = virt ? env.ml1_1 : (shd ? (SH == 8 ? env.ml1s_8 : env.ml1s_4) : env.ml1_2);
+  for (uint32_t h = 0; h < ((virt || shd) ? 1u : (uint32_t)SH / 2u); ++h) {
     const uint32_t j0 = i0 + 2u * h;
-    bool live[4];
+    bool live[SH];
     int first_live = -1;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < SH; ++s) {
       const uint32_t i = j0 + s;
       live[s] = s < n && i < end && b.chain_live[i] && !(b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE);
       if (live[s] && first_live < 0) first_live = s;
@@ -314,7 +321,7 @@ void k_mln4s(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_v
     __syncthreads();
     coop_stage_consts(env, sh.frame + cb);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < SH; ++s) {
       if (s >= n) break;
       const uint32_t i = j0 + (live[s] ? s : first_live), o = ML1_SLOTS * s;
       const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
@@ -324,9 +331,11 @@ void k_mln4s(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_v
     if (lane == 0) sh.flag = 0;
     __syncthreads();
     coop_run_inline(env, pg, sh.frame, &sh.flag);
-    if (sh4) {
+    if (shd) {
+      // f of item 0 = the product; items 1 .. SH-1 = 1
       if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(sh.frame, ML1_F + lane);
-      else if (lane < 48) reinterpret_cast<Fp*>(&b.f[i0 + 1 + (lane - 12) / 12])[lane % 12] = lane % 12 ? fp_zero() : c_one();
+      for (int w = lane - 12; w >= 0 && w < 12 * (SH - 1); w += 52)
+        reinterpret_cast<Fp*>(&b.f[i0 + 1 + w / 12])[w % 12] = w % 12 ? fp_zero() : c_one();
     } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -379,8 +388,17 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
   if (S == 4 && up && small_frame && b.ml_dom && env.ml1s_4.n > 0 && env.ml1_2.n > 0) {
     // first pass: the real sets four per wavefront, the virtual items (chunk signature
     // sums, Miller-loop units) one per wavefront, in one launch
+    // eight pairs per shared loop by default (fewer interpreter steps per set: +6 % at
+    // the bench's 8 x 8 calls in flight, profiles/r02c_ab_share8.json); $BLS_ML_SHARE=4
+    static const uint32_t share = [] {
+      const char* e = getenv("BLS_ML_SHARE");
+      return (e && atoi(e) == 4) ? 4u : 8u;
+    }();
     const uint32_t end = first + count, mid = b.n_sets <= first ? first : (b.n_sets < end ? b.n_sets : end);
-    k_mln4s<<<(mid - first + 3) / 4 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid);
+    if (share == 8 && env.ml1s_8.n > 0)
+      k_mlns<8><<<(mid - first + 7) / 8 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid);
+    else
+      k_mlns<4><<<(mid - first + 3) / 4 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid);
   } else if (S == 4 && env.ml1_4.n > 0) {
     k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count, up);
   } else if (S == 2 && env.ml1_2.n > 0) {
