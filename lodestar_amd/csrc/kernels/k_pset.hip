@@ -283,11 +283,14 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
 
 // First-pass Miller loops, one launch: blocks [0, G) take the real sets [first, mid)
 // SH at a time -- SH live sets of one chunk run one shared SH-pair loop (ml1s_SH),
-// otherwise each pair runs ml1_2 -- and blocks [G, G + V) take one virtual item of
-// [mid, mid + V) each (chunk signature sums, units: ml1_1, 408 steps, so they finish
-// with the shared loops instead of trailing them).  SH = 4: the 288-slot frame
-// (COOP_FRAME4S, 15.7 KB of LDS, 10 wavefronts per CU instead of 8 at 380 slots);
-// SH = 8: 512 slots (26.5 KB, 6 per CU), 24 % fewer interpreter steps per set.  The
+// otherwise each pair runs ml1_2 -- and the blocks after them the virtual items of
+// [mid, mid + V) (chunk signature sums, units), vp per wavefront.  SH = 8 (default):
+// 512 slots (26.5 KB, 6 wavefronts per CU), 24 % fewer interpreter steps per set than
+// 4-pair loops; with no Miller-loop units its virtual items (the chunk signature sums)
+// go four per wavefront (vp = 4: ml1_4 in the same frame, 916 steps, inside the 1,133
+// of the shared loops); with units (cfg5) the units carry most of the Miller loops
+// and go one per wavefront (vp = 1: ml1_1, 408 steps) to keep the launch short.  SH = 4: the 288-slot frame (COOP_FRAME4S, 15.7 KB, 10 per CU), one
+// virtual item per wavefront (ml1_1, 408 steps: ml1_4 does not fit the frame).  The
 // interpreter is inlined once, so the occupancy attribute bounds its registers (163
 // VGPRs, 3 wavefronts per SIMD; the out-of-line copy takes 256 and 2).
 #ifndef BLS_MLN4S_WAVES
@@ -297,16 +300,29 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
 template <int SH>
 __global__ __launch_bounds__(COOP_LANES)
 __attribute__((amdgpu_waves_per_eu(SH == 8 ? 2 : BLS_MLN4S_WAVES, SH == 8 ? 2 : BLS_MLN4S_WAVES)))
-void k_mlns(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_virt) {
+void k_mlns(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_virt, uint32_t vp) {
+  constexpr int VP = SH == 8 ? 4 : 1;  // the most virtual items per wavefront
   __shared__ CoopLdsN<SH == 8 ? COOP_FRAME8S : COOP_FRAME4S> sh;
   const int lane = threadIdx.x;
   const uint32_t G = (mid - first + (uint32_t)SH - 1u) / (uint32_t)SH;
   const bool virt = blockIdx.x >= G;
-  const uint32_t i0 = virt ? mid + (blockIdx.x - G) : first + (uint32_t)SH * blockIdx.x;
+  const uint32_t i0 = virt ? mid + vp * (blockIdx.x - G) : first + (uint32_t)SH * blockIdx.x;
   const uint32_t end = virt ? mid + n_virt : mid;
   const bool shd = !virt && mln_shared<SH>(b, env, i0, end);
-  const int n = virt ? 1 : (shd ? SH : 2), cb = shd ? (SH == 8 ? COOP_FRAME8S : COOP_FRAME4S) : COOP_FRAME;
-  const CoopProg pg = virt ? env.ml1_1 : (shd ? (SH == 8 ? env.ml1s_8 : env.ml1s_4) : env.ml1_2);
+  const bool vsh = virt && VP == 4 && vp == 4u && mln_shared<4>(b, env, i0, end);
+  const int n = virt ? (int)vp : (shd ? SH : 2);
+  int cb = COOP_FRAME;
+  CoopProg pg = env.ml1_2;
+  if (shd) {
+    cb = SH == 8 ? COOP_FRAME8S : COOP_FRAME4S;
+    pg = SH == 8 ? env.ml1s_8 : env.ml1s_4;
+  } else if (vsh) {
+    cb = COOP_FRAME4S;
+    pg = env.ml1s_4;
+  } else if (virt) {
+    cb = (VP == 4 && vp == 4u) ? COOP_FRAME2 : COOP_FRAME;
+    pg = (VP == 4 && vp == 4u) ? env.ml1_4 : env.ml1_1;
+  }
   for (uint32_t h = 0; h < ((virt || shd) ? 1u : (uint32_t)SH / 2u); ++h) {
     const uint32_t j0 = i0 + 2u * h;
     bool live[SH];
@@ -331,14 +347,14 @@ void k_mlns(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_vi
     if (lane == 0) sh.flag = 0;
     __syncthreads();
     coop_run_inline(env, pg, sh.frame, &sh.flag);
-    if (shd) {
-      // f of item 0 = the product; items 1 .. SH-1 = 1
+    if (shd || vsh) {
+      // f of item 0 = the product; items 1 .. n-1 = 1
       if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(sh.frame, ML1_F + lane);
-      for (int w = lane - 12; w >= 0 && w < 12 * (SH - 1); w += 52)
+      for (int w = lane - 12; w >= 0 && w < 12 * (n - 1); w += 52)
         reinterpret_cast<Fp*>(&b.f[i0 + 1 + w / 12])[w % 12] = w % 12 ? fp_zero() : c_one();
     } else {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < (VP > 2 ? VP : 2); ++s)
         if (s < n && live[s] && lane < 12)
           reinterpret_cast<Fp*>(&b.f[j0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);
     }
@@ -395,10 +411,13 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
       return (e && atoi(e) == 4) ? 4u : 8u;
     }();
     const uint32_t end = first + count, mid = b.n_sets <= first ? first : (b.n_sets < end ? b.n_sets : end);
-    if (share == 8 && env.ml1s_8.n > 0)
-      k_mlns<8><<<(mid - first + 7) / 8 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid);
-    else
-      k_mlns<4><<<(mid - first + 3) / 4 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid);
+    if (share == 8 && env.ml1s_8.n > 0 && env.ml1_4.n > 0) {
+      const uint32_t vp = b.n_units ? 1u : 4u;
+      k_mlns<8><<<(mid - first + 7) / 8 + (end - mid + vp - 1) / vp, COOP_LANES, 0, s>>>(b, env, first, mid,
+                                                                                        end - mid, vp);
+    } else {
+      k_mlns<4><<<(mid - first + 3) / 4 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid, 1u);
+    }
   } else if (S == 4 && env.ml1_4.n > 0) {
     k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count, up);
   } else if (S == 2 && env.ml1_2.n > 0) {
