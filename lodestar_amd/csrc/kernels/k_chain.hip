@@ -103,9 +103,12 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
 // reads them; every role that runs writes its byte, so no clearing is needed).
 // At most 256 VGPRs (93 spilled), so two wavefronts share a SIMD: cfg2 +1.2 % over one
 // 394-VGPR wavefront per SIMD (profiles/r02b_ab_chain_occ2.json); build variant
-// chain_occ1 lifts the cap.
+// chain_occ1 lifts the cap, chain_occ3 lowers it to 3 per SIMD: both slower at the
+// bench default (1.69M and 1.82-1.84M vs 1.82-1.87M, profiles/r02c_ab_chain_occ.json).
 #ifdef BLS_CHAIN_OCC1
 #define BLS_CHAIN_ATTR
+#elif defined(BLS_CHAIN_OCC3)
+#define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #else
 #define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
