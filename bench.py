@@ -127,12 +127,17 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
         sh8 = (os.environ.get("BLS_ML_SHARE") != "4" and os.environ.get("BLS_ML_SMALL_FRAME", "1") != "0"
                and "ml1s_8" in m)
         ml = (m["ml1s_8"] / 8 if sh8 else m["ml1s_4"] / 4) if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
+        # the signature sums: one group sum over the pass and ONE signature Miller loop
+        # (merged signature sum, $BLS_SIG_TOTAL), or one per chunk
+        if os.environ.get("BLS_SIG_TOTAL", "1") != "0" and chunks > 1:
+            sums = (m["ml1_1"] + wm["vset"]) / n_sets + (n_sets - 1) / n_sets * wm["gsum_add"]
+        else:
+            sums = chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"]
         per = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"] + ml
-               + chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"] + merged / n_sets)
-        return per, ("k_pre %.0f + k_chain %.0f + k_mln %.0f + chunk sums/ML %.0f + merged check %.0f" %
+               + sums + merged / n_sets)
+        return per, ("k_pre %.0f + k_chain %.0f + k_mln %.0f + signature sums/ML %.0f + merged check %.0f" %
                      (wm["k_pre"], wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"], ml,
-                      chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"],
-                      merged / n_sets))
+                      sums, merged / n_sets))
     S = pack_of(n_sets)
     ps = pset_products_per_set(S)
     return wm["k_pre"] + ps + merged / n_sets, "k_pre %.0f + k_pset %.0f + merged check %.0f" % (

@@ -466,6 +466,16 @@ static bool ml_shared_on() {
   return on;
 }
 
+// Merged signature sum (with the merged check): one signature Miller loop per device
+// pass instead of one per chunk; on unless $BLS_SIG_TOTAL=0
+static bool sig_total_on() {
+  static const bool on = [] {
+    const char* e = getenv("BLS_SIG_TOTAL");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // Segmented-sum plan for k_gsum over groups of requests: the groups' set indices
 // (group-major) and, per level, (beg, end) segments of at most GSUM_FAN items that
 // never straddle a group; level 0 indexes gsets, level L > 0 the outputs of level
@@ -686,6 +696,19 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     plan_gsum(in, goff, plan.chunk_reqs, chunk_gsum);
   }
   if (use_units) plan_gsum_sets(units.goff, units.members, unit_gsum);
+  // Merged signature sum: under the merged check the chunks' signature sums only ever
+  // meet in the product of every f, and prod_c e(-g1, S_c) = e(-g1, sum_c S_c) after the
+  // final exponentiation, so the first pass sums every chunk's r_i sig_i into ONE point
+  // (chunk group 0; the other chunk groups are empty, so k_vset gives them f = 1) and
+  // pairs it once.  A failing merged check re-sums per chunk and pairs each sum before
+  // the per-chunk final exponentiations (k_chunk_coop), so chunk verdicts are unchanged.
+  const bool use_total = sigagg && merged && n_chunks > 1 && sig_total_on();
+  GsumPlan total_gsum;
+  if (use_total) {
+    std::vector<uint32_t> goff(n_chunks + 1, (uint32_t)chunk_gsum.gsets.size());
+    goff[0] = 0;
+    plan_gsum_sets(goff, chunk_gsum.gsets, total_gsum);
+  }
   const size_t gseg_cap = 2ull * (n / 2 + 12ull * R + 8);  // uint32s: every level of any plan (fan-in >= 4)
   const size_t gtmp_cap = n / GSUM_FAN + R + 1;                  // level-0 segments of any plan
   if (sigagg && chunk_gsum.seg.size() > gseg_cap) {
@@ -729,6 +752,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   int32_t* merged_ok = nullptr;          // FE(prod f_i) == 1 of the merged check
   uint32_t* gsets_dev = nullptr;         // group-sum plans (aggregated-signature path)
   uint32_t* gseg_dev = nullptr;
+  uint32_t* tseg_dev = nullptr;          // the merged signature sum's plan
   G2J* gtmp[2] = {nullptr, nullptr};
   uint32_t *unit_rep_dev = nullptr, *ugsets_dev = nullptr, *useg_dev = nullptr;  // Miller-loop units
   G1J* utmp[2] = {nullptr, nullptr};
@@ -750,6 +774,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
     gsets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
     gseg_dev = sigagg ? c.take<uint32_t>(gseg_cap) : nullptr;
+    tseg_dev = use_total ? c.take<uint32_t>(total_gsum.seg.size()) : nullptr;
     if (use_units) {
       b.set_unit = c.take<uint32_t>(n);
       unit_rep_dev = c.take<uint32_t>(n_units);
@@ -830,6 +855,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   if (sigagg) {
     stage_copy(ctx, gsets_dev, chunk_gsum.gsets.data(), sizeof(uint32_t) * chunk_gsum.gsets.size());
     stage_copy(ctx, gseg_dev, chunk_gsum.seg.data(), sizeof(uint32_t) * chunk_gsum.seg.size());
+    if (use_total) stage_copy(ctx, tseg_dev, total_gsum.seg.data(), sizeof(uint32_t) * total_gsum.seg.size());
   }
 
   stage_copy(ctx, b.req_off, in->req_set_offsets, sizeof(uint32_t) * (R + 1));
@@ -873,7 +899,9 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       // per-set chains, the chunks' sums of r sig -> virtual sets n + c, then every
       // Miller loop (sets and virtual sets) in one launch
       HIPC(ctx, launch_k_chain(b, s)); dbg_sync(s, "k_chain");
-      if (launch_gsum(ctx, b, chunk_gsum, gseg_dev, gsets_dev, gtmp, n, s)) return -1;
+      if (launch_gsum(ctx, b, use_total ? total_gsum : chunk_gsum, use_total ? tseg_dev : gseg_dev, gsets_dev, gtmp,
+                      n, s))
+        return -1;
       if (use_units) {
         // sum r_i pk_i per unit (levels over the members), then the units' chain entries
         b.gsets = ugsets_dev;
@@ -944,6 +972,11 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     for (uint32_t ch = 0; ch < n_chunks; ++ch) chunk_ok[ch] = 1;
   } else if (n_chunks > 0 && !partial) {
     // some set is invalid or erroneous (or no merged check): the per-chunk verdicts decide
+    if (use_total) {
+      // the chunks' own signature sums and their Miller loops (virtual sets n + c)
+      if (launch_gsum(ctx, b, chunk_gsum, gseg_dev, gsets_dev, gtmp, n, s)) return -1;
+      HIPC(ctx, launch_k_mln(b, ctx->coop, n, n_chunks, s)); dbg_sync(s, "k_mln chunk sums");
+    }
     HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s)); dbg_sync(s, "k_chunk_coop");
     HIPC(ctx, hipStreamSynchronize(s));
     memcpy(chunk_ok.data(), res_host(ctx, b.chunk_ok), sizeof(int32_t) * n_chunks);
