@@ -2,11 +2,11 @@
 # Round-2 (third session) measurement set on one MI355X: parity tests, the driver-shaped bench line
 # (with the CPU baseline), the N-API mode, a kernel trace with the calls overlapping,
 # and SQ / HBM counter passes over one 8192-set call (k_chain: 512 wavefronts,
-# k_mlns<8>: 1024 + 128 wavefronts, 6 per CU by LDS).  Everything lands in gpurun_out/meas5.
+# k_mlns<8>: 1024 + 128 wavefronts, one signature-sum loop, 6 per CU by LDS).  Everything lands in gpurun_out/meas6.
 # $SKIP_TESTS=1 skips the parity tests, $SKIP_BENCH=1 the two bench lines.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/meas5
+O=$R/gpurun_out/meas6
 mkdir -p $O
 cd $R
 if [ -z "$SKIP_TESTS" ]; then
@@ -33,6 +33,6 @@ for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   timeout -s KILL 150 rocprofv3 --pmc $P -d $O/pmc$k -o run --output-format csv -- $B --sets 8192 --inflight 1 --calls-per-pass 1 --steps 1 --warmup 1 > $O/pmc$k.log 2>&1 || { tail -20 $O/pmc$k.log; exit 1; }
 done
 cd $R
-python3 tools/pmc_summary.py $O/pmc_summary.json "one 8192-set cfg2 call (bench.py --sets 8192 --inflight 1): k_chain 512 wavefronts (256 VGPRs, 2 per SIMD), k_mlns<8> 1152 wavefronts (1024 shared 8-pair loops + 128 of four chunk signature sums; 166 VGPRs, 6 per CU by LDS)" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5
+python3 tools/pmc_summary.py $O/pmc_summary.json "one 8192-set cfg2 call (bench.py --sets 8192 --inflight 1): k_chain 512 wavefronts (256 VGPRs, 2 per SIMD), k_mlns<8> 1152 wavefronts (1024 shared 8-pair loops + 128 for the signature sums, one of them live: merged signature sum; 166 VGPRs, 6 per CU by LDS)" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5
 python3 tools/trace_timeline.py $(find $O/trace16 -name "*kernel_trace.csv" | head -1) k_mln > $O/timeline.txt
 cat $O/timeline.txt
