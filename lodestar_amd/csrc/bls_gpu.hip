@@ -792,6 +792,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.chain = sigagg ? c.take<Fp>((size_t)CHAIN_WORDS * n_total) : nullptr;
     b.chain_live = sigagg ? c.take<uint32_t>(n_total) : nullptr;
     b.chain_st = sigagg ? c.take<uint8_t>(4ull * n) : nullptr;
+    b.rtab2 = sigagg ? c.take<G2J>(15ull * n) : nullptr;
+    b.rtab1 = sigagg ? c.take<G1J>(15ull * n) : nullptr;
     gtmp[0] = sigagg ? c.take<G2J>(gtmp_cap) : nullptr;
     gtmp[1] = sigagg ? c.take<G2J>(gtmp_cap) : nullptr;
     utmp[0] = use_units ? c.take<G1J>(unit_gsum.level_off[1] + 1) : nullptr;

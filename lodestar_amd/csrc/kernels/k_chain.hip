@@ -53,9 +53,45 @@ __device__ G2J iso_jac(const Fp* q) {
 // affine signature, RP on G1):
 // the double-and-add body is large, so the kernel keeps a single instance of it.
 __device__ __noinline__ void g2_mul_u64(G2J* out, const G2J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
-__device__ __noinline__ void g1_mul_u64(G1J* out, const G1J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
 // affine base (the signature): mixed additions
 __device__ __noinline__ void g2_mul_aff(G2J* out, const G2A* in, uint64_t k) { *out = aff_mul_u64(*in, k); }
+// [k]P for the per-set batch scalar r with a fixed 4-bit window: a per-set table of
+// [1..15]P in the call's workspace (PipeBufs::rtab2 / rtab1: a private-memory table
+// raised the scratch size past what the runtime grants 64 calls in flight), then 15
+// windows of four doublings and one addition.  With one lane per set the scalars differ
+// across the wavefront, so double-and-add executes an addition at every bit (some
+// lane has a 1 there): 63 doublings + 63 additions per chain; the window executes 63
+// doublings + 13 table additions + 15 window additions.  Same complete formulas, so
+// the same group element.
+template <class F>
+__device__ Jac<F> mul_u64_w4(const Jac<F>& p, const Aff<F>* pa, uint64_t k, Jac<F>* T) {
+  T[0] = p;  // T[j - 1] = [j] P
+  Jac<F> t = jac_dbl(p);
+  T[1] = t;
+  for (int j = 2; j < 15; ++j) {
+    t = pa ? jac_add_aff(t, *pa) : jac_add(t, p);
+    T[j] = t;
+  }
+  const uint32_t top = (uint32_t)(k >> 60);
+  Jac<F> acc = top ? T[top - 1] : jac_infinity<F>();
+  for (int w = 14; w >= 0; --w) {
+    acc = jac_dbl(jac_dbl(jac_dbl(jac_dbl(acc))));
+    const uint32_t d = (uint32_t)(k >> (4 * w)) & 15u;
+    if (d) acc = jac_add(acc, T[d - 1]);
+  }
+  return acc;
+}
+#ifndef BLS_CHAIN_BINARY_R
+__device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J* T) {
+  *out = in->inf ? jac_infinity<Fp2>() : mul_u64_w4<Fp2>(jac_from_aff(*in), in, k, T);
+}
+__device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J* T) {
+  *out = mul_u64_w4<Fp>(*in, nullptr, k, T);
+}
+#else  // build variant chain_binr: double-and-add
+__device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J*) { *out = aff_mul_u64(*in, k); }
+__device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J*) { *out = jac_mul_u64(*in, k); }
+#endif
 // out-of-line general addition for the handful of additions outside the chains
 __device__ __noinline__ void g2_add(G2J* out, const G2J* a, const G2J* b) { *out = jac_add(*a, *b); }
 
@@ -153,7 +189,7 @@ __global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, 
   } else if (role == 2) {
     const G2A sig = b.sig[i];
     G2J RS;
-    g2_mul_aff(&RS, &sig, set_scalar(b.seed, b.scalar_base + i));
+    g2_mul_r(&RS, &sig, set_scalar(b.seed, b.scalar_base + i), b.rtab2 + 15ull * i);
     o[CH_RS + 0] = RS.x.c0;
     o[CH_RS + 1] = RS.x.c1;
     o[CH_RS + 2] = RS.y.c0;
@@ -163,7 +199,7 @@ __global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, 
   } else {
     G1J RP;
     const G1J pk = b.pk[i];
-    g1_mul_u64(&RP, &pk, set_scalar(b.seed, b.scalar_base + i));
+    g1_mul_r(&RP, &pk, set_scalar(b.seed, b.scalar_base + i), b.rtab1 + 15ull * i);
     b.chain_st[4 * i + 3] = jac_is_inf(RP) ? 1 : 0;
     if (jac_is_inf(RP)) return;
     o[CH_RP + 0] = RP.x;
