@@ -329,10 +329,11 @@ def main() -> None:
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--inflight", type=int, default=8, help="verifier contexts (HIP streams) per GPU")
-    # default 8 x 8: the knee of profiles/r02c_knee.json (8 x 4 1.46M at 22 ms per pass,
-    # 8 x 6 1.64M at 30 ms, 8 x 8 1.72M at 38 ms, 8 x 10 1.73M at 47 ms); a call's verdicts
-    # arrive when its pass ends, well inside the reference's 100 ms job buffering
+    ap.add_argument("--inflight", type=int, default=10, help="verifier contexts (HIP streams) per GPU")
+    # default 10 contexts x 8 calls: the knee of profiles/r02c_knee_final.json with the
+    # final kernels (8 x 8 2.0M at 33 ms per pass, 10 x 8 2.09M at 39 ms, 12 x 8 2.09M at
+    # 47 ms); a call's verdicts arrive when its pass ends, well inside the reference's
+    # 100 ms job buffering
     # (multithread/index.ts:57 MAX_BUFFER_WAIT_MS)
     ap.add_argument("--calls-per-pass", type=int, default=8,
                     help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "

@@ -2,11 +2,11 @@
 # Round-2 (third session) measurement set on one MI355X: parity tests, the driver-shaped bench line
 # (with the CPU baseline), the N-API mode, a kernel trace with the calls overlapping,
 # and SQ / HBM counter passes over one 8192-set call (k_chain: 512 wavefronts,
-# k_mlns<8>: 1024 + 128 wavefronts, one signature-sum loop, 6 per CU by LDS).  Everything lands in gpurun_out/meas7.
+# k_mlns<8>: 1024 + 128 wavefronts, one signature-sum loop, 6 per CU by LDS).  Everything lands in gpurun_out/meas8.
 # $SKIP_TESTS=1 skips the parity tests, $SKIP_BENCH=1 the two bench lines.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/meas7
+O=$R/gpurun_out/meas8
 mkdir -p $O
 cd $R
 if [ -z "$SKIP_TESTS" ]; then
