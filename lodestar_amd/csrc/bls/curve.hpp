@@ -217,6 +217,31 @@ BLS_HD Jac<F> aff_mul_u64(const Aff<F>& p, uint64_t k) {
   return acc;
 }
 
+// [k]P with a fixed 4-bit window and a caller-provided table T[0..14] = [1..15]P (in
+// memory the caller chooses; kernels/k_chain.hip uses the call workspace): 63
+// doublings, 13 table additions (mixed when the affine base pa is given) and 15 window
+// additions, whatever k -- the form for per-lane scalars, where double-and-add
+// executes an addition at every bit for the wavefront.  Complete formulas, so the same
+// group element as jac_mul_u64 / aff_mul_u64.
+template <class F>
+BLS_HD Jac<F> jac_mul_u64_w4(const Jac<F>& p, const Aff<F>* pa, uint64_t k, Jac<F>* T) {
+  T[0] = p;  // T[j - 1] = [j] P
+  Jac<F> t = jac_dbl(p);
+  T[1] = t;
+  for (int j = 2; j < 15; ++j) {
+    t = pa ? jac_add_aff(t, *pa) : jac_add(t, p);
+    T[j] = t;
+  }
+  const uint32_t top = (uint32_t)(k >> 60);
+  Jac<F> acc = top ? T[top - 1] : jac_infinity<F>();
+  for (int w = 14; w >= 0; --w) {
+    acc = jac_dbl(jac_dbl(jac_dbl(jac_dbl(acc))));
+    const uint32_t d = (uint32_t)(k >> (4 * w)) & 15u;
+    if (d) acc = jac_add(acc, T[d - 1]);
+  }
+  return acc;
+}
+
 // [k]P for a scalar given as 8 little-endian 32-bit words (secret keys, up to 256 bits)
 template <class F>
 BLS_HD Jac<F> aff_mul_u256(const Aff<F>& p, const uint32_t k[8]) {

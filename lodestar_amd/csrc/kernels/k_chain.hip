@@ -55,38 +55,19 @@ __device__ G2J iso_jac(const Fp* q) {
 __device__ __noinline__ void g2_mul_u64(G2J* out, const G2J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
 // affine base (the signature): mixed additions
 __device__ __noinline__ void g2_mul_aff(G2J* out, const G2A* in, uint64_t k) { *out = aff_mul_u64(*in, k); }
-// [k]P for the per-set batch scalar r with a fixed 4-bit window: a per-set table of
-// [1..15]P in the call's workspace (PipeBufs::rtab2 / rtab1: a private-memory table
-// raised the scratch size past what the runtime grants 64 calls in flight), then 15
-// windows of four doublings and one addition.  With one lane per set the scalars differ
-// across the wavefront, so double-and-add executes an addition at every bit (some
-// lane has a 1 there): 63 doublings + 63 additions per chain; the window executes 63
-// doublings + 13 table additions + 15 window additions.  Same complete formulas, so
-// the same group element.
-template <class F>
-__device__ Jac<F> mul_u64_w4(const Jac<F>& p, const Aff<F>* pa, uint64_t k, Jac<F>* T) {
-  T[0] = p;  // T[j - 1] = [j] P
-  Jac<F> t = jac_dbl(p);
-  T[1] = t;
-  for (int j = 2; j < 15; ++j) {
-    t = pa ? jac_add_aff(t, *pa) : jac_add(t, p);
-    T[j] = t;
-  }
-  const uint32_t top = (uint32_t)(k >> 60);
-  Jac<F> acc = top ? T[top - 1] : jac_infinity<F>();
-  for (int w = 14; w >= 0; --w) {
-    acc = jac_dbl(jac_dbl(jac_dbl(jac_dbl(acc))));
-    const uint32_t d = (uint32_t)(k >> (4 * w)) & 15u;
-    if (d) acc = jac_add(acc, T[d - 1]);
-  }
-  return acc;
-}
+// [r] sig and [r] pk for the per-set batch scalar r: a fixed 4-bit window
+// (curve.hpp jac_mul_u64_w4) with the per-set table of [1..15]P in the call's
+// workspace (PipeBufs::rtab2 / rtab1: a private-memory table raised the scratch size
+// past what the runtime grants 64 calls in flight).  With one lane per set the scalars
+// differ across the wavefront, so double-and-add executes an addition at every bit
+// (some lane has a 1 there): 63 doublings + 63 additions per chain; the window
+// executes 63 doublings + 28 additions (profiles/r02c_ab_chain_window.json).
 #ifndef BLS_CHAIN_BINARY_R
 __device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J* T) {
-  *out = in->inf ? jac_infinity<Fp2>() : mul_u64_w4<Fp2>(jac_from_aff(*in), in, k, T);
+  *out = in->inf ? jac_infinity<Fp2>() : jac_mul_u64_w4<Fp2>(jac_from_aff(*in), in, k, T);
 }
 __device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J* T) {
-  *out = mul_u64_w4<Fp>(*in, nullptr, k, T);
+  *out = jac_mul_u64_w4<Fp>(*in, nullptr, k, T);
 }
 #else  // build variant chain_binr: double-and-add
 __device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J*) { *out = aff_mul_u64(*in, k); }

@@ -70,6 +70,39 @@ static G2A rd_g2(const uint8_t* b) {
 
 extern "C" {
 
+// kernels/k_chain.hip's windowed [k]P (curve.hpp jac_mul_u64_w4) against
+// double-and-add on multiples of the generators, for n scalars from a splitmix64
+// stream plus the edge scalars; returns the number of mismatches
+static uint64_t hs_splitmix(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+int hs_mul_window_check(unsigned long long seed, int n) {
+  uint64_t st = seed;
+  int bad = 0;
+  const uint64_t edge[] = {0ull, 1ull, 15ull, 16ull, 0x0FFFFFFFFFFFFFFFull, 1ull << 60, 0xFFFFFFFFFFFFFFFFull,
+                           0x8000000000000001ull};
+  for (int i = 0; i < n + 8; ++i) {
+    const uint64_t k = i < 8 ? edge[i] : hs_splitmix(st);
+    const uint64_t m = hs_splitmix(st) | 1ull;
+    G1J T1[15];
+    const G1J p1 = jac_mul_u64(jac_from_aff(g1_generator()), m);
+    if (!jac_eq(jac_mul_u64_w4<Fp>(p1, nullptr, k, T1), jac_mul_u64(p1, k))) ++bad;
+    G2J T2[15];
+    G2A a2 = g2_generator();
+    if (i & 1) {  // an affine base other than the generator: [m] g2, normalised
+      const G2J j2 = jac_mul_u64(jac_from_aff(a2), m);
+      const Fp2 zi = fp2_inv(j2.z), zi2 = fp2_sqr(zi);
+      a2.x = fp2_mul(j2.x, zi2);
+      a2.y = fp2_mul(j2.y, fp2_mul(zi2, zi));
+    }
+    if (!jac_eq(jac_mul_u64_w4<Fp2>(jac_from_aff(a2), &a2, k, T2), aff_mul_u64(a2, k))) ++bad;
+  }
+  return bad;
+}
+
 unsigned long long hs_fpm_count(void) { return bls_fpm_counter; }
 void hs_fpm_reset(void) { bls_fpm_counter = 0; }
 

@@ -278,3 +278,12 @@ def test_signing_root_dedup_pre_stage(hostsim):
     assert f(b"".join(roots), 5, uniq.ctypes.data, rep.ctypes.data, q.ctypes.data) == 5
     assert f(roots[2] * 7, 7, uniq.ctypes.data, rep.ctypes.data, q.ctypes.data) == 1
     assert list(rep[:7]) == [0] * 7
+
+
+def test_windowed_scalar_mul_matches_double_and_add(hostsim):
+    """k_chain's [r] sig / [r] pk (curve.hpp jac_mul_u64_w4: a 4-bit window over a
+    table of [1..15]P) give the same G1 / G2 elements as double-and-add, for random
+    64-bit scalars and the edge ones (0, 1, 15, 16, top nibble 0, 2^60, 2^64 - 1)."""
+    hostsim.hs_mul_window_check.restype = ctypes.c_int
+    hostsim.hs_mul_window_check.argtypes = [ctypes.c_ulonglong, ctypes.c_int]
+    assert hostsim.hs_mul_window_check(20261017, 24) == 0
