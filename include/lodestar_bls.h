@@ -82,6 +82,14 @@ int bls_gpu_device_count(void);
  * (multithread/index.ts:199-233). */
 int bls_gpu_init(int device, bls_gpu_ctx** out);
 
+/* The same with a stream priority: BLS_PRIORITY_HIGH puts the context's kernels ahead
+ * of normal-priority contexts' queued work on the device -- the latency lane of
+ * verifyOnMainThread calls (multithread/index.ts:138-151: the reference runs them on the
+ * main thread, outside the worker queue).  BLS_PRIORITY_NORMAL = bls_gpu_init. */
+#define BLS_PRIORITY_NORMAL 0
+#define BLS_PRIORITY_HIGH 1
+int bls_gpu_init_priority(int device, int priority, bls_gpu_ctx** out);
+
 /* Release device memory and streams (IBlsVerifier.close, index.ts:176-197). */
 void bls_gpu_close(bls_gpu_ctx* ctx);
 
@@ -225,6 +233,10 @@ int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iters, double* 
 int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t blocks, uint32_t reps, double* us_per_step,
                        double* ms_total,
                        uint64_t* step_stamps /* nullable, 2 n_steps + 1 s_memtime stamps (step start, compute done) */);
+
+/* Design probe: launch the probe kernel `name` (kernels/k_probe.hip: "ml_simt_w1",
+ * "ml_simt_w2", "fpm_d28") over `lanes` lanes `reps` times; *ms = wall time of the reps. */
+int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uint32_t reps, double* ms);
 
 /* Test hook: BLS_DEBUG_FORCE_EXACT routes every set through the exact single-lane
  * path (stage_exact_set) instead of the cooperative programs, so parity tests cover both. */

@@ -11,6 +11,15 @@
  * and feeds the reference's metric series (metrics.bls / metrics.blsThreadPool,
  * lodestar.ts:378-446) when a metrics object is passed.
  *
+ * verifyOnMainThread calls (and the synchronous state-transition helpers) run on a
+ * dedicated high-priority context (bls_gpu_init_priority): the reference runs them on
+ * the main thread outside the worker queue (index.ts:138-151), so they never wait
+ * behind a pool call here either.  Each context runs its calls on a libuv worker
+ * (napi_async_work): the process needs UV_THREADPOOL_SIZE >= contexts + 2 (pool
+ * contexts, the main-thread lane, one spare), set in the environment before Node
+ * starts; this module sets 18 when it is unset (enough for 16 contexts), which takes
+ * effect only if nothing used the libuv pool yet.
+ *
  * A signature set is {pubkeyIndices: number[]} (indices into the device pubkey
  * table loaded with loadPubkeys, i.e. index2pubkey) or {pubkey: Uint8Array(96)}
  * (uncompressed affine, the worker wire format of index.ts:126), plus
@@ -22,6 +31,9 @@ const path = require("path");
 
 const ADDON_PATH = path.join(__dirname, "..", "..", "lodestar_amd", "_native", "lodestar_bls.node");
 let defaultAddon = null;
+// libuv reads this when its pool first starts (see the header comment)
+if (!process.env.UV_THREADPOOL_SIZE) process.env.UV_THREADPOOL_SIZE = "18";
+let warnedPoolSize = false;
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:39
 const GPU_SETS_PER_CALL = 1024; // sets per bls_gpu_verify call (cfg2 shape)
@@ -134,21 +146,38 @@ class GpuBlsVerifier {
     this.addon = opts.addon || (defaultAddon = defaultAddon || require(ADDON_PATH));
     const addon = this.addon;
     this.ctxs = [];
-    // `inflight`: calls queued or running on the context (the main-thread path may
-    // share context 0 with a pool job; the library serialises calls per context)
-    for (let i = 0; i < contexts; i++) this.ctxs.push({handle: addon.init(device), inflight: 0, id: i});
+    // `inflight`: calls queued or running on the context (at most one pool call each)
+    for (let i = 0; i < contexts; i++) this.ctxs.push({handle: addon.init(device, false), inflight: 0, id: i});
+    // the main-thread lane: its own high-priority context, never used by the pool
+    this.mainCtx = {handle: addon.init(device, true), inflight: 0, id: "main"};
+    const uvSize = Number(process.env.UV_THREADPOOL_SIZE || 4);
+    if (!opts.addon && contexts + 2 > uvSize && !warnedPoolSize) {
+      warnedPoolSize = true;
+      console.warn(`GpuBlsVerifier: UV_THREADPOOL_SIZE=${uvSize} < contexts + 2 = ${contexts + 2}; ` +
+        "GPU calls will queue for libuv threads (set it in the environment before starting node)");
+    }
     this.jobs = []; // queue: jobs[jobsHead..] are pending
     this.jobsHead = 0;
     this.runScheduled = false;
     this.bufferedJobs = null;
     this.closed = false;
-    this.stats = {jobsStarted: 0, sigSetsStarted: 0, jobGroupsStarted: 0, batchRetries: 0};
+    this.stats = {jobsStarted: 0, sigSetsStarted: 0, jobGroupsStarted: 0, batchRetries: 0, batchSigsSuccess: 0};
+    const tp = this.metrics && this.metrics.blsThreadPool;
+    // queueLength: sampled on collect, as index.ts:130 does
+    if (tp && tp.queueLength && typeof tp.queueLength.addCollect === "function") {
+      tp.queueLength.addCollect(() => tp.queueLength.set(this.queueLength()));
+    }
+  }
+
+  /** Jobs waiting for a context (blsThreadPool.queueLength, index.ts:130) */
+  queueLength() {
+    return this.jobs.length - this.jobsHead;
   }
 
   /** Append validator pubkeys (48 B compressed each) to every context's device table.
    * All or nothing (bls_gpu_load_pubkeys appends no key of a batch holding a bad one). */
   loadPubkeys(pks48) {
-    this.ctxs.forEach((c, i) => {
+    [this.mainCtx].concat(this.ctxs).forEach((c, i) => {
       const codes = this.addon.loadPubkeys(c.handle, pks48, 48);
       const bad = codes.findIndex((x) => x !== 0);
       if (bad >= 0) throw Error(i === 0 ? `invalid pubkey at batch index ${bad}; no key appended` : "pubkey tables diverged");
@@ -161,7 +190,7 @@ class GpuBlsVerifier {
     if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
       // "don't buffer": one non-batchable request now (verifySignatureSetsMaybeBatch)
       const timer = this.metrics && this.metrics.blsThreadPool.mainThreadDurationInThreadPool.startTimer();
-      return this._call(this.ctxs[0], [{batchable: false, sets}]).then(
+      return this._call(this.mainCtx, [{batchable: false, sets}]).then(
         (v) => {
           if (timer) timer();
           return this._settle(v, 0);
@@ -195,15 +224,22 @@ class GpuBlsVerifier {
    * signature does not decode (Signature.fromBytes(sig, undefined, true)).
    */
   verifySignatureSetSync(set) {
-    return this._settle(this.addon.verifySync(this.ctxs[0].handle, packRequests([{batchable: false, sets: [set]}])), 0);
+    return this._settle(this.addon.verifySync(this.mainCtx.handle, packRequests([{batchable: false, sets: [set]}])), 0);
   }
 
   /** verifySignatureSet over many sets in one GPU call (e.g. every inline check of a
-   * block when batch verification is off): per-set booleans; a set that does not decode
-   * throws, as its own verifySignatureSet would. */
+   * block when batch verification is off): per set a boolean, or the Error its own
+   * verifySignatureSet would throw (a signature that does not decode) -- one bad set
+   * does not hide the other sets' verdicts (lodestar_amd/stf.py returns the same). */
   verifySignatureSetsEachSync(sets) {
-    const v = this.addon.verifySync(this.ctxs[0].handle, packRequests(sets.map((s) => ({batchable: false, sets: [s]}))));
-    return sets.map((_, i) => this._settle(v, i));
+    const v = this.addon.verifySync(this.mainCtx.handle, packRequests(sets.map((s) => ({batchable: false, sets: [s]}))));
+    return sets.map((_, i) => {
+      try {
+        return this._settle(v, i);
+      } catch (e) {
+        return e;
+      }
+    });
   }
 
   /**
@@ -215,7 +251,7 @@ class GpuBlsVerifier {
   computeSigningRoots(kind, objs, domains) {
     const k = typeof kind === "string" ? SSZ_KINDS[kind] : kind;
     if (k === undefined) throw Error(`unknown SSZ kind ${kind}`);
-    return this.addon.sszRoots(this.ctxs[0].handle, k, objs, domains === undefined ? null : domains);
+    return this.addon.sszRoots(this.mainCtx.handle, k, objs, domains === undefined ? null : domains);
   }
 
   /** IBlsVerifier.close (index.ts:176-197): abort queued jobs, wait for calls in flight */
@@ -227,9 +263,11 @@ class GpuBlsVerifier {
     this.jobsHead = 0;
     this.bufferedJobs = null;
     for (const j of pending) j.reject(Error("QUEUE_ABORTED"));
-    while (this.ctxs.some((c) => c.inflight > 0)) await new Promise((r) => setTimeout(r, 5));
-    for (const c of this.ctxs) this.addon.close(c.handle);
+    const all = this.mainCtx ? this.ctxs.concat([this.mainCtx]) : this.ctxs;
+    while (all.some((c) => c.inflight > 0)) await new Promise((r) => setTimeout(r, 5));
+    for (const c of all) this.addon.close(c.handle);
     this.ctxs = [];
+    this.mainCtx = null;
   }
 
   _settle(verdicts, i) {
@@ -298,7 +336,12 @@ class GpuBlsVerifier {
   }
 
   /** runJob / prepareWork (index.ts:290-400) with GPU contexts as the workers.  A call
-   * carries jobs of one pubkey form (table indices or raw bytes), as the C-ABI takes one. */
+   * carries jobs of one pubkey form (table indices or raw bytes), as the C-ABI takes one.
+   * A raw-key call is one worker message as prepareWork builds it (jobs until >= 128
+   * sets): a key that does not decode rejects every job of its message
+   * (deserializeSet, worker.ts:43-46), so it must not take more jobs with it than the
+   * reference's message would.  Table-index calls cannot fail that way and take up to
+   * maxSetsPerCall sets. */
   async _runJob() {
     if (this.closed) return;
     const ctx = this.ctxs.find((c) => c.inflight === 0);
@@ -308,7 +351,8 @@ class GpuBlsVerifier {
     const jobs = [];
     const skipped = [];
     let total = 0;
-    while (this.jobsHead < this.jobs.length && total < this.maxSetsPerCall) {
+    const cap = kind ? MAX_SIGNATURE_SETS_PER_JOB : this.maxSetsPerCall;
+    while (this.jobsHead < this.jobs.length && total < cap) {
       const j = this.jobs[this.jobsHead];
       this.jobs[this.jobsHead++] = undefined;
       if (isRaw(j) === kind) {
@@ -337,7 +381,7 @@ class GpuBlsVerifier {
     }
     if (this.jobsHead < this.jobs.length) this._scheduleRun(); // another idle context may take the rest
     let verdicts;
-    const t0 = process.hrtime.bigint();
+    const jobStartNs = Number(process.hrtime.bigint());
     try {
       verdicts = await this._call(ctx, jobs);
     } catch (e) {
@@ -346,7 +390,22 @@ class GpuBlsVerifier {
       this._scheduleRun();
       return;
     }
-    if (tp) tp.jobsWorkerTime.inc({workerId: ctx.id}, Number(process.hrtime.bigint() - t0) / 1e9);
+    const jobEndNs = Number(process.hrtime.bigint());
+    // the worker's BlsWorkResult bookkeeping (addon: properties of the verdict array)
+    const wStart = verdicts.workerStartNs !== undefined ? verdicts.workerStartNs : jobStartNs;
+    const wEnd = verdicts.workerEndNs !== undefined ? verdicts.workerEndNs : jobEndNs;
+    const retries = verdicts.batchRetries || 0;
+    const sigsOk = verdicts.batchSigsSuccess || 0;
+    this.stats.batchRetries += retries;
+    this.stats.batchSigsSuccess += sigsOk;
+    if (tp) {
+      // index.ts:357-366
+      tp.jobsWorkerTime.inc({workerId: ctx.id}, (wEnd - wStart) / 1e9);
+      tp.latencyToWorker.observe(Math.max(0, wStart - jobStartNs) / 1e9);
+      tp.latencyFromWorker.observe(Math.max(0, jobEndNs - wEnd) / 1e9);
+      tp.batchRetries.inc(retries);
+      tp.batchSigsSuccess.inc(sigsOk);
+    }
     let ok = 0;
     let err = 0;
     for (let i = 0; i < jobs.length; i++) {

@@ -3,13 +3,20 @@
  * `GpuBlsVerifier` (integration/js/gpuBlsVerifier.js) loads in place of the
  * @chainsafe/blst worker pool (beacon-node/src/chain/bls/multithread/index.ts).
  *
- *   init(device) -> handle
+ *   init(device, highPriority?) -> handle   (highPriority: bls_gpu_init_priority HIGH)
  *   loadPubkeys(handle, Uint8Array pks, pkLen) -> Int32Array codes
  *   verify(handle, {reqSetOffsets, reqBatchable, messages, signatures,
  *                   setPkOffsets?, pkIndices?, pubkeys?, signatureLens?, seed?})
  *          -> Promise<Int32Array verdicts>   (1 valid, 0 invalid, -code error)
  *   verifySync(handle, request) -> Int32Array   (the same on the calling thread)
  *   close(handle)
+ *
+ * The verdict array carries the worker's BlsWorkResult bookkeeping (types.ts:26-38) as
+ * properties: batchRetries, batchSigsSuccess, deviceMs, and workerStartNs / workerEndNs
+ * (CLOCK_MONOTONIC ns as Numbers, the clock of process.hrtime.bigint(), taken on the
+ * thread that ran the call) -- what the pool turns into its metrics
+ * (multithread/index.ts:330-366: latencyToWorker, latencyFromWorker, batchRetries,
+ * batchSigsSuccess, jobsWorkerTime).
  *
  * verify runs bls_gpu_verify on a libuv worker thread (napi_async_work): the JS
  * main thread never blocks on the GPU.  Input buffers are referenced until the
@@ -24,6 +31,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "lodestar_bls.h"
 
@@ -63,13 +71,19 @@ static void handle_finalize(napi_env env, void* data, void* hint) {
 }
 
 static napi_value js_init(napi_env env, napi_callback_info info) {
-  size_t argc = 1;
-  napi_value argv[1];
+  size_t argc = 2;
+  napi_value argv[2];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   int32_t dev = 0;
+  bool high = false;
   if (argc > 0) CHECK(env, napi_get_value_int32(env, argv[0], &dev));
+  if (argc > 1) {
+    napi_valuetype t;
+    CHECK(env, napi_typeof(env, argv[1], &t));
+    if (t == napi_boolean) CHECK(env, napi_get_value_bool(env, argv[1], &high));
+  }
   bls_gpu_ctx* ctx = NULL;
-  if (bls_gpu_init(dev, &ctx) != 0 || !ctx) {
+  if (bls_gpu_init_priority(dev, high ? BLS_PRIORITY_HIGH : BLS_PRIORITY_NORMAL, &ctx) != 0 || !ctx) {
     napi_throw_error(env, NULL, "bls_gpu_init failed (no HIP device?)");
     return NULL;
   }
@@ -153,15 +167,40 @@ typedef struct {
   napi_ref keep;          /* the request object: keeps the input buffers alive */
   napi_ref keep_handle;   /* the handle's external: no finalizer while the job is out */
   int32_t* verdicts;
+  bls_stats stats;
+  double t_start_ns, t_end_ns;
   int rc;
   napi_deferred deferred;
   napi_async_work work;
 } verify_job;
 
+static double mono_ns(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec * 1e9 + (double)t.tv_nsec;
+}
+
+/* the BlsWorkResult bookkeeping as properties of the verdict array */
+static void attach_stats(napi_env env, napi_value out, const bls_stats* st, double t0, double t1) {
+  napi_value v;
+  napi_create_uint32(env, st->batch_retries, &v);
+  napi_set_named_property(env, out, "batchRetries", v);
+  napi_create_uint32(env, st->batch_sigs_success, &v);
+  napi_set_named_property(env, out, "batchSigsSuccess", v);
+  napi_create_double(env, st->device_ms, &v);
+  napi_set_named_property(env, out, "deviceMs", v);
+  napi_create_double(env, t0, &v);
+  napi_set_named_property(env, out, "workerStartNs", v);
+  napi_create_double(env, t1, &v);
+  napi_set_named_property(env, out, "workerEndNs", v);
+}
+
 static void verify_execute(napi_env env, void* data) {
   (void)env;
   verify_job* j = (verify_job*)data;
-  j->rc = bls_gpu_verify(j->ctx, &j->batch, j->verdicts, NULL);
+  j->t_start_ns = mono_ns();
+  j->rc = bls_gpu_verify(j->ctx, &j->batch, j->verdicts, &j->stats);
+  j->t_end_ns = mono_ns();
 }
 
 static void verify_complete(napi_env env, napi_status status, void* data) {
@@ -181,6 +220,7 @@ static void verify_complete(napi_env env, napi_status status, void* data) {
     napi_create_arraybuffer(env, 4 * (size_t)(n ? n : 1), &dst, &ab);
     memcpy(dst, j->verdicts, 4 * (size_t)n);
     napi_create_typedarray(env, napi_int32_array, n, ab, 0, &out);
+    attach_stats(env, out, &j->stats, j->t_start_ns, j->t_end_ns);
     napi_resolve_deferred(env, j->deferred, out);
   }
   napi_delete_reference(env, j->keep);
@@ -282,10 +322,13 @@ static napi_value js_verify_sync(napi_env env, napi_callback_info info) {
   void* dst;
   CHECK(env, napi_create_arraybuffer(env, 4 * (size_t)(b.n_reqs ? b.n_reqs : 1), &dst, &ab));
   CHECK(env, napi_create_typedarray(env, napi_int32_array, b.n_reqs, ab, 0, &out));
-  if (bls_gpu_verify(h->ctx, &b, (int32_t*)dst, NULL) != 0) {
+  bls_stats st;
+  const double t0 = mono_ns();
+  if (bls_gpu_verify(h->ctx, &b, (int32_t*)dst, &st) != 0) {
     napi_throw_error(env, NULL, bls_gpu_last_error(h->ctx));
     return NULL;
   }
+  attach_stats(env, out, &st, t0, mono_ns());
   return out;
 }
 

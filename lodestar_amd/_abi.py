@@ -42,6 +42,7 @@ ERROR_MESSAGES = {
 SYMBOLS = (
     "bls_gpu_device_count",
     "bls_gpu_init",
+    "bls_gpu_init_priority",
     "bls_gpu_close",
     "bls_gpu_last_error",
     "bls_gpu_load_pubkeys",
@@ -61,6 +62,7 @@ SYMBOLS = (
     "bls_gpu_fp_mul_test",
     "bls_gpu_fpm_bench",
     "bls_gpu_coop_probe",
+    "bls_gpu_kernel_probe",
     "bls_gpu_set_debug_flags",
 )
 # SSZ kinds of bls_gpu_ssz_roots (low 8 bits: serialized size)
@@ -124,6 +126,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_device_count.restype = i32
         lib.bls_gpu_init.argtypes = [i32, ctypes.POINTER(vp)]
         lib.bls_gpu_init.restype = i32
+        lib.bls_gpu_init_priority.argtypes = [i32, i32, ctypes.POINTER(vp)]
+        lib.bls_gpu_init_priority.restype = i32
         lib.bls_gpu_close.argtypes = [vp]
         lib.bls_gpu_close.restype = None
         lib.bls_gpu_last_error.argtypes = [vp]
@@ -163,6 +167,8 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_fpm_bench.restype = i32
         lib.bls_gpu_coop_probe.argtypes = [vp, ctypes.c_char_p, u32, u32, dp, dp, vp]
         lib.bls_gpu_coop_probe.restype = i32
+        lib.bls_gpu_kernel_probe.argtypes = [vp, ctypes.c_char_p, u32, u32, dp]
+        lib.bls_gpu_kernel_probe.restype = i32
         lib.bls_gpu_set_debug_flags.argtypes = [vp, u32]
         lib.bls_gpu_set_debug_flags.restype = i32
     return lib

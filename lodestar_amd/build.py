@@ -62,16 +62,23 @@ def build_coop_tables(verbose: bool = True) -> Path:
     generator sources change."""
     tools = ROOT / "tools"
     out = OUT_DIR / "coop_tables.bin"
+    gz = OUT_DIR / "coop_tables.bin.gz"  # what the library loads and what travels to the GPU box
     key = hashlib.sha256(b"".join((tools / f).read_bytes()
                                   for f in ("gen_coop.py", "gen_pset.py", "circuits.py", "gen_constants.py"))).hexdigest()
     stamp = OUT_DIR / ".coop_stamp"
-    if out.exists() and out.with_name("coop_programs.json").exists() and stamp.exists() and stamp.read_text() == key:
-        return out
-    if verbose:
-        print("[build] tools/gen_coop.py ->", out, flush=True)
-    subprocess.run([sys.executable, str(tools / "gen_coop.py"), str(out)], check=True)
+    if gz.exists() and out.with_name("coop_programs.json").exists() and stamp.exists() and stamp.read_text() == key:
+        return gz
+    if not (out.exists() and stamp.exists() and stamp.read_text() == key):
+        if verbose:
+            print("[build] tools/gen_coop.py ->", out, flush=True)
+        subprocess.run([sys.executable, str(tools / "gen_coop.py"), str(out)], check=True)
+    import gzip
+
+    with open(out, "rb") as src, gzip.open(str(gz) + ".tmp", "wb", compresslevel=6) as dst:
+        dst.write(src.read())
+    os.replace(str(gz) + ".tmp", gz)
     stamp.write_text(key)
-    return out
+    return gz
 
 
 def build_work_model(verbose: bool = True) -> Path:
@@ -106,7 +113,7 @@ def build(jobs: int | None = None, verbose: bool = True, variant: str | None = N
     stamp_file = OUT_DIR / (f".lib_stamp_{variant}" if variant else ".lib_stamp")
     if lib.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
         return lib
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib) + ".tmp", *map(str, objs)]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib) + ".tmp", *map(str, objs), "-lz"]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

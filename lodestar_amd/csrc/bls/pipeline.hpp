@@ -46,6 +46,10 @@ struct PipeBufs {
   const uint32_t* pk_idx;
   const G1A* pk_table;
   uint32_t pk_table_n;
+  // aggregate sets of >= agg_min keys (0: none) are summed one wavefront per set by
+  // k_pk_agg (a lane per key stride, then a tree over the lanes); stage_pk skips them
+  const uint32_t* agg_sets;    // n_agg set indices
+  uint32_t n_agg, agg_min;
   const uint8_t* msgs;         // n_sets * 32
   const uint8_t* sigs;         // n_sets * 96
   const uint32_t* sig_lens;    // nullable
@@ -155,6 +159,7 @@ BLS_HD void stage_pk(const PipeBufs& b, uint32_t i) {
   G1J acc = jac_infinity<Fp>();
   if (b.set_pk_off) {
     uint32_t beg = b.set_pk_off[i], end = b.set_pk_off[i + 1];
+    if (b.agg_min && end - beg >= b.agg_min) return;  // k_pk_agg sums it
     if (beg == end) code = BLS_EMPTY_AGGREGATE;
     for (uint32_t k = beg; k < end; ++k) {
       uint32_t idx = b.pk_idx[k];

@@ -25,6 +25,7 @@
 
 #include <dlfcn.h>
 #include <stdlib.h>
+#include <zlib.h>
 
 #include <mutex>
 #include <string>
@@ -158,6 +159,8 @@ struct CoopProgEntry {
   uint32_t first, n_steps, frame, n_mul;
 };
 
+// the gzip'd table (coop_tables.bin.gz, what travels with the tree) next to the
+// library; $BLS_COOP_TABLES may name a plain or gzip'd file (gzread reads both)
 std::string coop_tables_path() {
   const char* env = getenv("BLS_COOP_TABLES");
   if (env && *env) return env;
@@ -165,26 +168,36 @@ std::string coop_tables_path() {
   if (dladdr((void*)&bls_gpu_device_count, &info) && info.dli_fname) {
     std::string p(info.dli_fname);
     size_t slash = p.rfind('/');
-    return (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) + "/coop_tables.bin";
+    return (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) + "/coop_tables.bin.gz";
   }
-  return "coop_tables.bin";
+  return "coop_tables.bin.gz";
 }
 
 }  // namespace
 
 static int load_coop_tables(bls_gpu_ctx* ctx) {
   std::string path = coop_tables_path();
-  FILE* f = fopen(path.c_str(), "rb");
+  gzFile f = gzopen(path.c_str(), "rb");
   if (!f) {
     snprintf(ctx->err, sizeof(ctx->err), "cannot open %s (run the build: tools/gen_coop.py)", path.c_str());
     return -1;
   }
-  fseek(f, 0, SEEK_END);
-  long sz = ftell(f);
-  fseek(f, 0, SEEK_SET);
-  std::vector<uint8_t> buf((size_t)sz);
-  size_t got = fread(buf.data(), 1, (size_t)sz, f);
-  fclose(f);
+  std::vector<uint8_t> buf;
+  for (;;) {
+    const size_t at = buf.size();
+    buf.resize(at + (4u << 20));
+    const int got = gzread(f, buf.data() + at, 4u << 20);
+    if (got < 0) {
+      gzclose(f);
+      snprintf(ctx->err, sizeof(ctx->err), "read error in %s", path.c_str());
+      return -1;
+    }
+    buf.resize(at + (size_t)got);
+    if (got == 0) break;
+  }
+  gzclose(f);
+  const long sz = (long)buf.size();
+  const size_t got = buf.size();
   CoopHeader h;
   if (got != (size_t)sz || sz < (long)sizeof(h)) {
     snprintf(ctx->err, sizeof(ctx->err), "short read of %s", path.c_str());
@@ -293,7 +306,9 @@ int bls_gpu_device_count(void) {
   return n;
 }
 
-int bls_gpu_init(int device, bls_gpu_ctx** out) {
+int bls_gpu_init(int device, bls_gpu_ctx** out) { return bls_gpu_init_priority(device, BLS_PRIORITY_NORMAL, out); }
+
+int bls_gpu_init_priority(int device, int priority, bls_gpu_ctx** out) {
   *out = nullptr;
   bls_gpu_ctx* ctx = new bls_gpu_ctx();
   memset(ctx, 0, sizeof(*ctx));
@@ -306,7 +321,10 @@ int bls_gpu_init(int device, bls_gpu_ctx** out) {
     delete ctx;
     return -1;
   }
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+  int prio_lo = 0, prio_hi = 0;  // HIP: numerically lower = higher priority
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking,
+                                  priority == BLS_PRIORITY_HIGH ? prio_hi : prio_lo) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
     delete ctx;
     return -1;
@@ -735,6 +753,12 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       for (uint32_t i = in->req_set_offsets[r]; i < in->req_set_offsets[r + 1]; ++i) ml_dom[i] = 0x80000000u | r;
   }
 
+  // aggregate sets big enough for a wavefront each (k_pk_agg)
+  std::vector<uint32_t> agg_list;
+  if (in->set_pk_offsets)
+    for (uint32_t i = 0; i < n; ++i)
+      if (in->set_pk_offsets[i + 1] - in->set_pk_offsets[i] >= BLS_AGG_WAVE_MIN) agg_list.push_back(i);
+
   uint32_t seed_words[8];
   {
     uint8_t seed[32];
@@ -764,6 +788,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.pubkeys = in->set_pk_offsets ? nullptr : c.take<uint8_t>(96ull * n);
     b.set_pk_off = in->set_pk_offsets ? c.take<uint32_t>(n + 1) : nullptr;
     b.pk_idx = in->set_pk_offsets ? c.take<uint32_t>(n_pk_idx) : nullptr;
+    b.agg_sets = agg_list.empty() ? nullptr : c.take<uint32_t>(agg_list.size());
     b.msgs = c.take<uint8_t>(32ull * n);
     b.msg_uniq = dedup ? c.take<uint32_t>(n_uniq) : nullptr;
     b.msg_rep = dedup ? c.take<uint32_t>(n) : nullptr;
@@ -869,6 +894,9 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     stage_copy(ctx, b.set_pk_off, in->set_pk_offsets, sizeof(uint32_t) * (n + 1));
     stage_copy(ctx, b.pk_idx, in->pk_indices, sizeof(uint32_t) * n_pk_idx);
   }
+  b.n_agg = (uint32_t)agg_list.size();
+  b.agg_min = agg_list.empty() ? 0u : BLS_AGG_WAVE_MIN;
+  if (!agg_list.empty()) stage_copy(ctx, b.agg_sets, agg_list.data(), sizeof(uint32_t) * agg_list.size());
   stage_copy(ctx, b.msgs, in->messages, 32ull * n);
   b.n_uniq = dedup ? n_uniq : 0;
   if (dedup) {
@@ -892,7 +920,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   HIPC(ctx, hipEventRecord(ctx->ev0, s));
   HIPC(ctx, hipEventRecord(ctx->ev[0], s));  // no H2D stage: the kernels read the mapped inputs
   if (n > 0) {
-    HIPC(ctx, launch_k_pk(b, s));  // also resets set_flag, flag_count, the next first_bad_pk slot dbg_sync(s, "k_pk");
+    HIPC(ctx, launch_k_pk(b, s));  // also resets set_flag, flag_count, the next first_bad_pk slot
+    HIPC(ctx, launch_k_pk_agg(b, s)); dbg_sync(s, "k_pk");
     ctx->first_bad_slot ^= 1u;
     HIPC(ctx, hipEventRecord(ctx->ev[1], s));
     HIPC(ctx, launch_k_pre(b, s)); dbg_sync(s, "k_pre");
@@ -1273,11 +1302,15 @@ int bls_gpu_aggregate_pubkeys(bls_gpu_ctx* ctx, const uint32_t* set_pk_offsets, 
   HIPC(ctx, hipSetDevice(ctx->device));
   if (n_sets == 0) return 0;
   uint32_t n_idx = set_pk_offsets[n_sets];
+  std::vector<uint32_t> agg_list;
+  for (uint32_t i = 0; i < n_sets; ++i)
+    if (set_pk_offsets[i + 1] - set_pk_offsets[i] >= BLS_AGG_WAVE_MIN) agg_list.push_back(i);
   PipeBufs b;
   memset(&b, 0, sizeof(b));
   auto carve = [&](Carver& c, uint8_t*& d_out) {
     b.set_pk_off = c.take<uint32_t>(n_sets + 1);
     b.pk_idx = c.take<uint32_t>(n_idx);
+    b.agg_sets = c.take<uint32_t>(agg_list.size());
     b.pk = c.take<G1J>(n_sets);
     b.pk_status = c.take<int32_t>(n_sets);
     d_out = c.take<uint8_t>(96ull * n_sets);
@@ -1297,6 +1330,13 @@ int bls_gpu_aggregate_pubkeys(bls_gpu_ctx* ctx, const uint32_t* set_pk_offsets, 
   HIPC(ctx, hipMemcpyAsync((void*)b.set_pk_off, set_pk_offsets, sizeof(uint32_t) * (n_sets + 1),
                            hipMemcpyHostToDevice, s));
   HIPC(ctx, hipMemcpyAsync((void*)b.pk_idx, pk_indices, sizeof(uint32_t) * n_idx, hipMemcpyHostToDevice, s));
+  b.n_agg = (uint32_t)agg_list.size();
+  b.agg_min = agg_list.empty() ? 0u : BLS_AGG_WAVE_MIN;
+  if (!agg_list.empty()) {
+    HIPC(ctx, hipMemcpyAsync((void*)b.agg_sets, agg_list.data(), sizeof(uint32_t) * agg_list.size(),
+                             hipMemcpyHostToDevice, s));
+    HIPC(ctx, launch_k_pk_agg(b, s));  // the big aggregates first; k_aggregate serializes every set
+  }
   HIPC(ctx, launch_k_aggregate(b, d_out, s));
   HIPC(ctx, hipMemcpyAsync(out96, d_out, 96ull * n_sets, hipMemcpyDeviceToHost, s));
   if (codes) HIPC(ctx, hipMemcpyAsync(codes, b.pk_status, sizeof(int32_t) * n_sets, hipMemcpyDeviceToHost, s));
@@ -1507,6 +1547,27 @@ extern "C" int bls_gpu_fpm_bench(bls_gpu_ctx* ctx, uint32_t lanes, uint32_t iter
   HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   *ns_per_fpm = ms * 1e6 / iters;
   *fpm_per_s = (double)lanes * iters / (ms * 1e-3);
+  return 0;
+}
+
+extern "C" int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uint32_t reps, double* ms) {
+  CTX_LOCK(ctx);
+  HIPC(ctx, hipSetDevice(ctx->device));
+  const size_t per = name ? kernel_probe_out_bytes(name) : 0;
+  if (!per || !ms || lanes == 0) {
+    snprintf(ctx->err, sizeof(ctx->err), "unknown probe %s", name ? name : "(null)");
+    return -2;
+  }
+  if (ensure_dev(ctx, per * lanes)) return -1;
+  hipStream_t s = ctx->stream;
+  HIPC(ctx, launch_kernel_probe(name, ctx->dev_ws, lanes, s));  // warm-up
+  HIPC(ctx, hipEventRecord(ctx->ev0, s));
+  for (uint32_t r = 0; r < reps; ++r) HIPC(ctx, launch_kernel_probe(name, ctx->dev_ws, lanes, s));
+  HIPC(ctx, hipEventRecord(ctx->ev1, s));
+  HIPC(ctx, hipStreamSynchronize(s));
+  float t = 0.f;
+  HIPC(ctx, hipEventElapsedTime(&t, ctx->ev0, ctx->ev1));
+  *ms = t;
   return 0;
 }
 

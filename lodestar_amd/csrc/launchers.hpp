@@ -11,6 +11,8 @@
 static inline unsigned bls_grid_for(uint32_t n) { return (n + BLS_BLOCK - 1) / BLS_BLOCK; }
 
 hipError_t launch_k_pk(const bls::PipeBufs& b, hipStream_t s);
+hipError_t launch_k_pk_agg(const bls::PipeBufs& b, hipStream_t s);
+#define BLS_AGG_WAVE_MIN 16u  // aggregate sets of at least this many keys: k_pk_agg
 hipError_t launch_k_aggregate(const bls::PipeBufs& b, uint8_t* out96, hipStream_t s);
 hipError_t launch_k_load_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, bls::G1A* out, int32_t* codes,
                                  hipStream_t s);
@@ -40,6 +42,8 @@ hipError_t launch_k_sign(const uint8_t* sks, const uint8_t* msgs, uint32_t n, ui
 hipError_t launch_k_mad_peak(uint64_t* out, uint32_t blocks, uint32_t iters, hipStream_t s);
 hipError_t launch_k_fp_mul_test(const uint8_t* a, const uint8_t* b, uint32_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_k_fpm_chain(bls::Fp* io, uint32_t lanes, uint32_t iters, hipStream_t s);
+size_t kernel_probe_out_bytes(const char* name);
+hipError_t launch_kernel_probe(const char* name, void* out, uint32_t lanes, hipStream_t s);
 #include "bls/coop.hpp"
 hipError_t launch_k_chunk_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_indiv_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
@@ -53,3 +57,4 @@ hipError_t launch_k_fprod(const bls::Fp12* in, uint32_t n, bls::Fp12* out, int32
 hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_mln(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_t first, uint32_t count,
                         hipStream_t s, bool own_only = false);
+hipError_t launch_k_mls(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, hipStream_t s);

@@ -109,14 +109,16 @@ def pack_requests(requests, seed: bytes | None = None) -> PackedBatch:
 
 
 class GpuContext:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, high_priority: bool = False):
+        """high_priority: the context's stream outranks normal contexts' queued kernels
+        (bls_gpu_init_priority; the verifyOnMainThread latency lane)."""
         self.lib = load_library()
         ndev = self.lib.bls_gpu_device_count()
         if ndev <= device:
             raise NativeError(f"no HIP device {device} (visible: {ndev}); the verifier has no CPU fallback")
         h = ctypes.c_void_p()
-        if self.lib.bls_gpu_init(device, ctypes.byref(h)) != 0:
-            raise NativeError(f"bls_gpu_init({device}) failed")
+        if self.lib.bls_gpu_init_priority(device, 1 if high_priority else 0, ctypes.byref(h)) != 0:
+            raise NativeError(f"bls_gpu_init_priority({device}) failed")
         self._h = h
         self.device = device
 
@@ -339,6 +341,14 @@ class GpuContext:
         self._check(self.lib.bls_gpu_fpm_bench(self._h, lanes, iters, ctypes.byref(ns), ctypes.byref(rate)),
                     "bls_gpu_fpm_bench")
         return ns.value, rate.value
+
+    def kernel_probe(self, name: str, lanes: int, reps: int) -> float:
+        """Wall ms of `reps` launches of the design probe `name` over `lanes` lanes
+        (kernels/k_probe.hip)."""
+        ms = ctypes.c_double()
+        self._check(self.lib.bls_gpu_kernel_probe(self._h, name.encode(), lanes, reps, ctypes.byref(ms)),
+                    "bls_gpu_kernel_probe")
+        return ms.value
 
     def coop_probe(self, name: str, blocks: int, reps: int, n_stamps: int = 0):
         """(us per step, ms total[, per-step s_memtime stamps of one run])"""

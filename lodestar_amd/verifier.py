@@ -6,7 +6,9 @@ with GPU contexts in place of worker threads:
 * `verify_signature_sets(sets, batchable, verify_on_main_thread)` (interface.ts:20-46,
   index.ts:134-174): the main-thread branch (`verify_on_main_thread` and not
   `verify_all_multi_thread`) runs the call at once as one non-batchable request
-  (verifySignatureSetsMaybeBatch semantics, maybeBatch.ts:16-39); otherwise the sets
+  (verifySignatureSetsMaybeBatch semantics, maybeBatch.ts:16-39) on a dedicated
+  high-priority context that no pool call uses (the reference runs it on the main
+  thread, outside the worker queue, index.ts:138-151); otherwise the sets
   are split by chunkifyMaximizeChunkSize(sets, 128) into jobs (index.ts:156) whose
   results are AND-ed.
 * job queue (index.ts:238-285): batchable jobs are buffered until more than 32
@@ -19,9 +21,13 @@ with GPU contexts in place of worker threads:
   BLST_INVALID_SIZE", "Empty signature set", ...).  The reference caps a worker
   message at 128 sets (MAX_SIGNATURE_SETS_PER_JOB, sized for one CPU core); a GPU call
   wants ~1024 (one call of 128 sets fills 43 of 1024 SIMDs), so the default
-  coalesces queued jobs up to GPU_SETS_PER_CALL.  Verdicts per job are unchanged:
-  the worker chunks a message by request (worker.ts:56) and re-verifies a failing
-  chunk's requests alone, so which jobs share a message changes only batchRetries.
+  coalesces queued jobs up to GPU_SETS_PER_CALL.  For table-index keys verdicts per
+  job are unchanged: the worker chunks a message by request (worker.ts:56) and
+  re-verifies a failing chunk's requests alone, so which jobs share a message changes
+  only batchRetries.  Raw-key jobs are different: deserializeSet rejects a whole worker
+  message when one key does not decode (worker.ts:43-46), so they go to the GPU as the
+  reference's messages (prepareWork: jobs until >= 128 sets, index.ts:385-400), each
+  its own message of one bls_gpu_verify_many submission.
 * metrics: `metrics.bls.aggregatedPubkeys` and the `metrics.blsThreadPool.*` series
   under the reference's names (lodestar_amd/metrics.py, lodestar.ts:378-446).
 * `close()` (index.ts:176-197) rejects pending jobs with QUEUE_ABORTED.
@@ -103,7 +109,7 @@ class GpuBlsVerifier:
         self.verify_all_multi_thread = verify_all_multi_thread
         self.max_sets_per_call = max_sets_per_call
         self._ctxs = [GpuContext(device) for _ in range(n_contexts)]
-        self._main = self._ctxs[0]
+        self._main = GpuContext(device, high_priority=True)  # the main-thread lane, no pool call
         self._main_lock = threading.Lock()
         if pubkeys48 is not None:
             self.load_pubkeys(pubkeys48)
@@ -130,7 +136,7 @@ class GpuBlsVerifier:
         if (codes != 0).any():
             bad = int((codes != 0).argmax())
             raise BlsError(f"invalid pubkey at batch index {bad} (code {int(codes[bad])}); no key appended")
-        for c in self._ctxs[1:]:
+        for c in self._ctxs[1:] + [self._main]:
             codes = c.load_pubkeys(pubkeys48, 48)
             if (codes != 0).any():  # same bytes as context 0: cannot happen short of a device fault
                 raise BlsError("pubkey tables diverged across contexts")
@@ -189,7 +195,7 @@ class GpuBlsVerifier:
                 j.future.set_exception(QueueAborted("QUEUE_ABORTED"))
         for t in self._threads:
             t.join(timeout=30)
-        for c in self._ctxs:
+        for c in self._ctxs + [self._main]:
             c.close()
 
     def __enter__(self):
@@ -210,7 +216,9 @@ class GpuBlsVerifier:
         return code == 1
 
     def _call(self, ctx: GpuContext, reqs, worker_id: int = 0):
-        """One bls_gpu_verify; raw and table pubkeys go in separate calls."""
+        """One GPU submission per pubkey form: table-index requests as one message
+        (bls_gpu_verify), raw-key requests as the reference's worker messages (jobs until
+        >= 128 sets each) through one bls_gpu_verify_many."""
         def is_raw(req):
             return any(isinstance(pk, (bytes, bytearray, memoryview)) for pk, _, _ in req[1])
         groups = {}
@@ -219,11 +227,27 @@ class GpuBlsVerifier:
         verdicts = [0] * len(reqs)
         stats = None
         tp = self.metrics.blsThreadPool
-        for idx in groups.values():
+        for raw, idx in groups.items():
             t0 = time.perf_counter()
-            pb = pack_requests([reqs[k] for k in idx])
-            t1 = time.perf_counter()
-            v, stats = ctx.verify_packed(pb)
+            if raw:
+                msgs, cur, n = [], [], 0
+                for k in idx:
+                    cur.append(k)
+                    n += len(reqs[k][1])
+                    if n >= MAX_SIGNATURE_SETS_PER_JOB:
+                        msgs.append(cur)
+                        cur, n = [], 0
+                if cur:
+                    msgs.append(cur)
+                pbs = [pack_requests([reqs[k] for k in m]) for m in msgs]
+                t1 = time.perf_counter()
+                vs, stats = ctx.verify_many(pbs)
+                v = [x for part in vs for x in part]
+                idx = [k for m in msgs for k in m]
+            else:
+                pb = pack_requests([reqs[k] for k in idx])
+                t1 = time.perf_counter()
+                v, stats = ctx.verify_packed(pb)
             t2 = time.perf_counter()
             for k, x in zip(idx, v):
                 verdicts[k] = int(x)

@@ -578,12 +578,29 @@ def _decode_case(golden, name):
     return bytes.fromhex(next(c["bytes"] for c in golden["sig_decode"] if c["name"] == name))
 
 
-def _expected_stats(expect, n_chunk=16):
-    """batch_retries / batch_sigs_success of the chunked worker for single-set requests
-    (a chunk with any non-1 verdict is retried)."""
-    chunks = [expect[i:i + n_chunk] for i in range(0, len(expect), n_chunk)]
-    retries = sum(1 for c in chunks if any(v != 1 for v in c))
-    ok = sum(len(c) for c in chunks if all(v == 1 for v in c))
+def _expected_stats(oracle, expect):
+    """batch_retries / batch_sigs_success of one worker message of single-set batchable
+    requests, from the oracle's worker semantics (oracle.verify_many_signature_sets,
+    worker.ts:32-108) over outcome tokens: each set is its known outcome (1 valid, 0
+    invalid, -code).  The token predicate restates oracle.verify_signature_sets_maybe_batch
+    (maybeBatch.ts:16-39): every signature is decoded first and a decode error throws;
+    one set alone verifies deterministically (an infinity signature throws
+    ZERO_SIGNATURE there, and only makes a batch false); otherwise the batch is valid iff
+    every set is.  The oracle's per-request verdicts must equal `expect`."""
+    zero = -oracle.E_ZERO_SIGNATURE
+
+    def maybe_batch(tokens):
+        if len(tokens) == 0:
+            raise oracle.BlsError(oracle.E_EMPTY_SET)
+        for t in tokens:
+            if t < 0 and t != zero:
+                raise oracle.BlsError(-t)
+        if len(tokens) == 1 and tokens[0] == zero:
+            raise oracle.BlsError(oracle.E_ZERO_SIGNATURE)
+        return all(t == 1 for t in tokens)
+
+    res, retries, ok = oracle.verify_many_signature_sets([(True, [c]) for c in expect], maybe_batch)
+    assert [(1 if r[1] else 0) if r[0] == "success" else -r[1].code for r in res] == list(expect)
     return retries, ok
 
 
@@ -642,7 +659,7 @@ def test_cfg2_1024_call_with_invalid_sets(gpu, oracle, golden, table):
         reqs.append((True, [(pk, m, sig)]))
         expect.append(code)
     pb = pack_requests(reqs)
-    retries, ok = _expected_stats(expect)
+    retries, ok = _expected_stats(oracle, expect)
     res = _run_all_paths(gpu, pb)
     for name, (v, st) in res.items():
         assert list(v) == expect, name
@@ -689,7 +706,7 @@ def test_cfg5_shape_two_roots_with_invalid(gpu, oracle, table, verify_path):
             res[name] = gpu.verify_packed(pb)
         finally:
             gpu.set_debug_flags(0)
-    retries, ok = _expected_stats(expect)
+    retries, ok = _expected_stats(oracle, expect)
     for name, (v, st) in res.items():
         assert list(v) == expect, name
         assert (st.batch_retries, st.batch_sigs_success) == (retries, ok), name

@@ -63,6 +63,14 @@ def test_js_adapter_host_side():
     assert r["verdicts_ok"] and r["max_call_sets"] == 1024 and 4 <= r["calls"] <= 6
     assert r["rejected"] == "BLST_ERROR: BLST_INVALID_SIZE" and r["others_true"]
     assert r["closed"] == "QUEUE_ABORTED" and r["inflight_at_close"] == 0
+    # batchRetries, batchSigsSuccess, latencyToWorker, latencyFromWorker move (calls with a
+    # failing chunk), queueLength is sampled on collect (multithread/index.ts:130,357-366)
+    assert all(x > 0 for x in r["series"]) and not r["series_bad"] and r["queue_length_metric"]
+    assert r["stats_retries"] > 0
+    # raw-key calls stay one worker message each (prepareWork: jobs until >= 128 sets)
+    assert r["raw_max_call_sets"] == 128
+    # verifyOnMainThread runs on the dedicated high-priority context
+    assert r["main_handles"] == 1 and r["main_calls"] == [1] and r["pool_high"] == 2
 
 
 @pytest.mark.gpu
