@@ -127,6 +127,12 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
         sh8 = (os.environ.get("BLS_ML_SHARE") != "4" and os.environ.get("BLS_ML_SMALL_FRAME", "1") != "0"
                and "ml1s_8" in m)
         ml = (m["ml1s_8"] / 8 if sh8 else m["ml1s_4"] / 4) if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
+        simt = int(os.environ.get("BLS_ML_SIMT", "2") or 2)
+        if simt == 2:    # k_mlq lines + k_mlf (two pairs per f): kernels/k_mlq.hip
+            ml = wm["ml_lines"] + wm["ml_f_pair"]
+        elif simt == 1:  # fused one-lane loop: kernels/k_mls.hip
+            ml = wm["ml_simt"]
+            ml1 = ml
         # the signature sums: one group sum over the pass and ONE signature Miller loop
         # (merged signature sum, $BLS_SIG_TOTAL), or one per chunk
         if os.environ.get("BLS_SIG_TOTAL", "1") != "0" and chunks > 1:

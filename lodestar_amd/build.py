@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -40,19 +41,71 @@ def sources() -> list[Path]:
 # A/B build variants: extra defines -> lodestar_amd/_native/liblodestar_bls_<name>.so
 VARIANTS = {"mul32": ["-DBLS_FP_MUL32", "-DBLS_CHAIN_INL32"], "chain_inl32": ["-DBLS_CHAIN_INL32"],
             "chain_occ1": ["-DBLS_CHAIN_OCC1"], "chain_occ3": ["-DBLS_CHAIN_OCC3"],
-            "chain_binr": ["-DBLS_CHAIN_BINARY_R"]}
+            "chain_binr": ["-DBLS_CHAIN_BINARY_R"], "chain_w4": ["-DBLS_CHAIN_W4"]}
+
+
+# Scratch budget (the guard against the round-2 "kernel never finished"): the HIP runtime
+# backs each hardware queue with scratch for a full device of the kernel's wavefronts,
+# scratch bytes/lane x 64 x resident waves (occupancy x 1024 SIMDs), and past ~8 GiB over
+# the queues in use it aborts the queue with HSA_STATUS_ERROR_OUT_OF_RESOURCES
+# (profiles/r03_scratch_out_of_resources.txt: 4,160 B/lane at 2 waves/SIMD, 16 contexts).
+# The verify path runs up to 16 contexts (queues), so a kernel it launches may reserve at
+# most 8 GiB / 16 = 512 MiB; the build refuses one that needs more.
+SCRATCH_BUDGET = 512 << 20
+SIMDS = 1024
+FIXTURE_KERNELS = ("k_sign", "k_sk_to_pk", "k_probe_")  # input synthesis / probes, one context
+
+
+def _resources(remarks: str) -> list[dict]:
+    """Per kernel: name, scratch bytes/lane, occupancy (waves/SIMD) from hipcc's
+    -Rpass-analysis=kernel-resource-usage remarks."""
+    out, cur = [], None
+    for line in remarks.splitlines():
+        if "remark:" not in line:
+            continue
+        body = line.split("remark:", 1)[1].strip()
+        if body.startswith("Function Name:"):
+            cur = {"name": body.split(":", 1)[1].strip().split(" ")[0]}
+            out.append(cur)
+        elif cur is not None and body.startswith("ScratchSize"):
+            cur["scratch"] = int(body.split(":", 1)[1].split()[0])
+        elif cur is not None and body.startswith("Occupancy"):
+            cur["occupancy"] = int(body.split(":", 1)[1].split()[0])
+        elif cur is not None and body.startswith("VGPRs:"):
+            cur["vgprs"] = int(body.split(":", 1)[1].split()[0])
+        elif cur is not None and body.startswith("AGPRs:"):
+            cur["agprs"] = int(body.split(":", 1)[1].split()[0])
+    for k in out:
+        k["device_scratch_bytes"] = k.get("scratch", 0) * 64 * k.get("occupancy", 1) * SIMDS
+    return out
+
+
+def _check_scratch(src: Path, kernels: list[dict]) -> None:
+    for k in kernels:
+        if k["device_scratch_bytes"] > SCRATCH_BUDGET and not any(f in k["name"] for f in FIXTURE_KERNELS):
+            raise SystemExit(f"{src.name}: kernel {k['name']} reserves {k['device_scratch_bytes'] >> 20} MiB of "
+                             f"scratch per queue ({k.get('scratch')} B/lane x 64 x {k.get('occupancy')} waves/SIMD "
+                             f"x {SIMDS} SIMDs) > {SCRATCH_BUDGET >> 20} MiB: the runtime aborts queues past ~8 GiB "
+                             "over 16 contexts (lodestar_amd/build.py SCRATCH_BUDGET)")
 
 
 def _compile(src: Path, hdr: str, verbose: bool, extra: list[str] | None = None) -> Path:
     flags = FLAGS + (extra or [])
     key = hashlib.sha256((hdr + " ".join(flags)).encode() + src.read_bytes()).hexdigest()[:16]
     obj = OBJ_DIR / f"{src.stem}.{key}.o"
-    if obj.exists():
+    res = obj.with_suffix(".res.json")
+    if obj.exists() and res.exists():
         return obj
-    cmd = [HIPCC, *flags, "-c", str(src), "-o", str(obj) + ".tmp"]
+    cmd = [HIPCC, *flags, "-Rpass-analysis=kernel-resource-usage", "-c", str(src), "-o", str(obj) + ".tmp"]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        sys.stderr.write(p.stderr)
+        raise subprocess.CalledProcessError(p.returncode, cmd)
+    kernels = _resources(p.stderr)
+    _check_scratch(src, kernels)
+    res.write_text(json.dumps(kernels, indent=1))
     os.replace(str(obj) + ".tmp", obj)
     return obj
 
@@ -109,6 +162,9 @@ def build(jobs: int | None = None, verbose: bool = True, variant: str | None = N
     jobs = jobs or min(len(srcs), os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hdr, verbose, extra), srcs))
+    if not variant:  # every kernel's registers, occupancy and scratch reservation, for the record
+        table = [dict(k, tu=o.stem.split(".")[0]) for o in objs for k in json.loads(o.with_suffix(".res.json").read_text())]
+        (OUT_DIR / "kernel_resources.json").write_text(json.dumps(table, indent=1))
     stamp = hashlib.sha256("".join(str(o) for o in objs).encode()).hexdigest()
     stamp_file = OUT_DIR / (f".lib_stamp_{variant}" if variant else ".lib_stamp")
     if lib.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:

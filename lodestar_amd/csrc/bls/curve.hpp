@@ -332,6 +332,64 @@ BLS_HD G2J g2_clear_cofactor(const G2J& p) {
   return jac_add(t3, jac_neg(p));
 }
 
+// ---- GLV/GLS scalar multiplication by the batch scalar r = a + b mu ----------------
+// mu = -x^2 mod r is the eigenvalue of both cheap endomorphisms:
+//   G1: sigma(x, y) = (beta x, y) = [-x^2]P                (g1_in_subgroup above)
+//   G2: -psi^2(Q) = [-x^2]Q   (psi = [x] on G2, Scott's test above)
+// so [a + b mu]P = [a]P + [b]endo(P) with a, b the two 32-bit halves of the set's
+// 64-bit random value: 32 doublings instead of 63.  a + b mu is a uniformly drawn
+// scalar from 2^64 distinct non-zero values (the lattice {(u, v): u + v mu = 0 mod r}
+// has no vector with |u|, |v| < 2^33 but 0, since v x^2 < r for |v| < 2^33), the
+// same soundness as blst's 64-bit randomBytesNonZero(8) scalars; the SAME scalar
+// multiplies pk in G1 and sig in G2, as the batch equation needs.
+BLS_HD G1J g1_sigma(const G1J& p) {
+  G1J r = p;
+  r.x = fp_mul(p.x, c_g1_beta());  // x = X / Z^2: beta x <-> beta X
+  return r;
+}
+
+BLS_HD G2J g2_mu(const G2J& p) { return jac_neg(g2_psi(g2_psi(p))); }
+
+// the group's [mu] endomorphism, by point type
+BLS_HD G1J jac_endo_mu(const G1J& p) { return g1_sigma(p); }
+BLS_HD G2J jac_endo_mu(const G2J& p) { return g2_mu(p); }
+
+// The joint 2-bit-window table T[4 j + i - 1] = [i]P + [j]endo(P), i, j in 0..3, not
+// both 0 (15 entries, caller-provided memory) and the 16 windows of (a, b): 33
+// doublings and 9 + 1 + 16 additions, whatever a and b (per-lane scalars: the
+// wavefront runs every addition anyway).  Complete formulas: the same group element as
+// jac_mul on the full scalar.
+template <class F>
+BLS_HD Jac<F> jac_mul_glv(const Jac<F>& p, uint32_t a, uint32_t b, Jac<F>* T) {
+  const Jac<F> p2 = jac_dbl(p);
+  const Jac<F> p3 = jac_add(p2, p);
+  T[0] = p;
+  T[1] = p2;
+  T[2] = p3;
+  // loops kept rolled: one copy of each formula (the table lives in the caller's memory)
+#pragma unroll 1
+  for (int j = 1; j < 4; ++j) {
+    const Jac<F> e = jac_endo_mu(T[j - 1]);  // [j] endo(P)
+    T[4 * j - 1] = e;
+#pragma unroll 1
+    for (int i = 1; i < 4; ++i) T[4 * j + i - 1] = jac_add(e, T[i - 1]);
+  }
+  Jac<F> acc = jac_infinity<F>();
+#pragma unroll 1
+  for (int w = 15; w >= 0; --w) {
+    acc = jac_dbl(jac_dbl(acc));
+    const uint32_t d = ((a >> (2 * w)) & 3u) | (((b >> (2 * w)) & 3u) << 2);
+    if (d) acc = jac_add(acc, T[d - 1]);
+  }
+  return acc;
+}
+
+// the scalar a + b mu mod r as 8 little-endian words (tests / the oracle side)
+BLS_HD void glv_split(uint64_t r64, uint32_t& a, uint32_t& b) {
+  a = (uint32_t)r64;
+  b = (uint32_t)(r64 >> 32);
+}
+
 // ---- serialization (ZCash format) ---------------------------------------------
 // Error codes follow blst's BLST_ERROR enum; values >= 8 are Lodestar/chainsafe-level.
 enum BlsCode : int32_t {

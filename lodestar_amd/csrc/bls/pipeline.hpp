@@ -114,6 +114,7 @@ struct PipeBufs {
   // consecutive live items of one domain run ONE loop over their four pairs and keep
   // the product in the first item's f (the other three f = 1).  Nullable.
   const uint32_t* ml_dom;
+  uint32_t* ml_lines;  // line buffer of the split SIMT Miller loops (k_mlq -> k_mlf), nullable
   uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
   uint32_t* flag_count;  // 1 word: sets flagged by the cooperative kernel (GPU path)
   // outputs

@@ -826,6 +826,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.set_flag = c.take<uint32_t>(n);
     b.flag_count = c.take<uint32_t>(1);
     b.f = c.take<Fp12>(n_total);
+    b.ml_lines = sigagg ? c.take<uint32_t>(mlq_line_words(n_total)) : nullptr;
     b.req_status = c.take<int32_t>(R);
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);

@@ -62,7 +62,21 @@ __device__ __noinline__ void g2_mul_aff(G2J* out, const G2A* in, uint64_t k) { *
 // differ across the wavefront, so double-and-add executes an addition at every bit
 // (some lane has a 1 there): 63 doublings + 63 additions per chain; the window
 // executes 63 doublings + 28 additions (profiles/r02c_ab_chain_window.json).
-#ifndef BLS_CHAIN_BINARY_R
+// Default: GLV/GLS (curve.hpp jac_mul_glv): the set's scalar is a + b mu with a, b its
+// two 32-bit halves and mu = -x^2, applied as [a]P + [b]endo(P) through a joint 2-bit
+// window -- 33 doublings instead of 63 (G1: sigma(x, y) = (beta x, y); G2: -psi^2).
+#if !defined(BLS_CHAIN_BINARY_R) && !defined(BLS_CHAIN_W4)
+__device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J* T) {
+  uint32_t a, b;
+  glv_split(k, a, b);
+  *out = in->inf ? jac_infinity<Fp2>() : jac_mul_glv<Fp2>(jac_from_aff(*in), a, b, T);
+}
+__device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J* T) {
+  uint32_t a, b;
+  glv_split(k, a, b);
+  *out = jac_mul_glv<Fp>(*in, a, b, T);
+}
+#elif !defined(BLS_CHAIN_BINARY_R)  // build variant chain_w4: 64-bit scalars, 4-bit windows
 __device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J* T) {
   *out = in->inf ? jac_infinity<Fp2>() : jac_mul_u64_w4<Fp2>(jac_from_aff(*in), in, k, T);
 }
@@ -109,6 +123,68 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
          b.set_flag[i];
 }
 
+// The four roles, each out of line: the kernel's scratch is then the largest role's
+// frame, not the kernel frame holding role 0's points plus the deepest callee (the
+// runtime reserves scratch per queue for a full device of wavefronts,
+// lodestar_amd/build.py SCRATCH_BUDGET).
+__device__ __noinline__ void chain_role_h(const PipeBufs& b, uint32_t i) {
+  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
+  // H = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P), P = iso(q0) + iso(q1)
+  const Fp* q = b.q + 8ull * i;
+  const G2J P = g2_add_v(iso_jac(q), iso_jac(q + 4));
+  const G2J t1 = g2_mul_x(P);
+  const G2J t2 = g2_psi(P);
+  G2J t3 = g2_psi(g2_psi(jac_dbl(P)));
+  t3 = g2_add_v(t3, jac_neg(t2));
+  t3 = g2_add_v(t3, g2_mul_x(g2_add_v(t1, t2)));
+  t3 = g2_add_v(t3, jac_neg(t1));
+  const G2J Hj = g2_add_v(t3, jac_neg(P));
+  b.chain_st[4 * i + 0] = jac_is_inf(Hj) ? 1 : 0;
+  if (jac_is_inf(Hj)) return;
+  // HQ = affine H: one Fp inversion of N(Z)
+  const Fp ni = fp_inv_gcd(fp_add(fp_sqr(Hj.z.c0), fp_sqr(Hj.z.c1)));
+  const Fp2 zi = Fp2{fp_mul(Hj.z.c0, ni), fp_neg(fp_mul(Hj.z.c1, ni))};
+  const Fp2 zi2 = fp2_sqr(zi);
+  const Fp2 hx = fp2_mul(Hj.x, zi2);
+  const Fp2 hy = fp2_mul(Hj.y, fp2_mul(zi2, zi));
+  o[CH_HQ + 0] = hx.c0;
+  o[CH_HQ + 1] = hx.c1;
+  o[CH_HQ + 2] = hy.c0;
+  o[CH_HQ + 3] = hy.c1;
+}
+
+__device__ __noinline__ void chain_role_sub(const PipeBufs& b, uint32_t i) {
+  const G2A sig = b.sig[i];
+  G2J xs;
+  g2_mul_aff(&xs, &sig, (uint64_t)BLS_X_ABS);
+  b.chain_st[4 * i + 1] = jac_eq(g2_psi(jac_from_aff(sig)), jac_neg(xs)) ? 0 : 1;
+}
+
+__device__ __noinline__ void chain_role_rs(const PipeBufs& b, uint32_t i) {
+  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
+  const G2A sig = b.sig[i];
+  G2J RS;
+  g2_mul_r(&RS, &sig, set_scalar(b.seed, b.scalar_base + i), b.rtab2 + 15ull * i);
+  o[CH_RS + 0] = RS.x.c0;
+  o[CH_RS + 1] = RS.x.c1;
+  o[CH_RS + 2] = RS.y.c0;
+  o[CH_RS + 3] = RS.y.c1;
+  o[CH_RS + 4] = RS.z.c0;
+  o[CH_RS + 5] = RS.z.c1;
+}
+
+__device__ __noinline__ void chain_role_rp(const PipeBufs& b, uint32_t i) {
+  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
+  G1J RP;
+  const G1J pk = b.pk[i];
+  g1_mul_r(&RP, &pk, set_scalar(b.seed, b.scalar_base + i), b.rtab1 + 15ull * i);
+  b.chain_st[4 * i + 3] = jac_is_inf(RP) ? 1 : 0;
+  if (jac_is_inf(RP)) return;
+  o[CH_RP + 0] = RP.x;
+  o[CH_RP + 1] = RP.y;
+  o[CH_RP + 2] = RP.z;
+}
+
 // Four roles per set, one wavefront per (role, 64 sets), so a call of n sets runs
 // 4 n / 64 wavefronts and its latency is the longest chain, not their sum:
 //   role 0  H = clear_cofactor(iso(q0) + iso(q1)) -> HQ (affine)   ~2.9k Fp products,
@@ -137,56 +213,10 @@ __global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, 
   // (plan_msg_dedup) runs role 0, whatever its own pubkey / signature status, unless
   // its SSWU points went to the exact path; k_chain_done shares the result
   if (role == 0 ? ((b.msg_rep && b.msg_rep[i] != i) || b.set_flag[i]) : chain_skip(b, i)) return;
-  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
-  if (role == 0) {
-    // H = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P), P = iso(q0) + iso(q1)
-    const Fp* q = b.q + 8ull * i;
-    const G2J P =
-        g2_add_v(iso_jac(q), iso_jac(q + 4));
-    const G2J t1 = g2_mul_x(P);
-    const G2J t2 = g2_psi(P);
-    G2J t3 = g2_psi(g2_psi(jac_dbl(P)));
-    t3 = g2_add_v(t3, jac_neg(t2));
-    t3 = g2_add_v(t3, g2_mul_x(g2_add_v(t1, t2)));
-    t3 = g2_add_v(t3, jac_neg(t1));
-    const G2J Hj = g2_add_v(t3, jac_neg(P));
-    b.chain_st[4 * i + 0] = jac_is_inf(Hj) ? 1 : 0;
-    if (jac_is_inf(Hj)) return;
-    // HQ = affine H: one Fp inversion (binary GCD) of N(Z)
-    const Fp ni = fp_inv_gcd(fp_add(fp_sqr(Hj.z.c0), fp_sqr(Hj.z.c1)));
-    const Fp2 zi = Fp2{fp_mul(Hj.z.c0, ni), fp_neg(fp_mul(Hj.z.c1, ni))};
-    const Fp2 zi2 = fp2_sqr(zi);
-    const Fp2 hx = fp2_mul(Hj.x, zi2);
-    const Fp2 hy = fp2_mul(Hj.y, fp2_mul(zi2, zi));
-    o[CH_HQ + 0] = hx.c0;
-    o[CH_HQ + 1] = hx.c1;
-    o[CH_HQ + 2] = hy.c0;
-    o[CH_HQ + 3] = hy.c1;
-  } else if (role == 1) {
-    const G2A sig = b.sig[i];
-    G2J xs;
-    g2_mul_aff(&xs, &sig, (uint64_t)BLS_X_ABS);
-    b.chain_st[4 * i + 1] = jac_eq(g2_psi(jac_from_aff(sig)), jac_neg(xs)) ? 0 : 1;
-  } else if (role == 2) {
-    const G2A sig = b.sig[i];
-    G2J RS;
-    g2_mul_r(&RS, &sig, set_scalar(b.seed, b.scalar_base + i), b.rtab2 + 15ull * i);
-    o[CH_RS + 0] = RS.x.c0;
-    o[CH_RS + 1] = RS.x.c1;
-    o[CH_RS + 2] = RS.y.c0;
-    o[CH_RS + 3] = RS.y.c1;
-    o[CH_RS + 4] = RS.z.c0;
-    o[CH_RS + 5] = RS.z.c1;
-  } else {
-    G1J RP;
-    const G1J pk = b.pk[i];
-    g1_mul_r(&RP, &pk, set_scalar(b.seed, b.scalar_base + i), b.rtab1 + 15ull * i);
-    b.chain_st[4 * i + 3] = jac_is_inf(RP) ? 1 : 0;
-    if (jac_is_inf(RP)) return;
-    o[CH_RP + 0] = RP.x;
-    o[CH_RP + 1] = RP.y;
-    o[CH_RP + 2] = RP.z;
-  }
+  if (role == 0) chain_role_h(b, i);
+  else if (role == 1) chain_role_sub(b, i);
+  else if (role == 2) chain_role_rs(b, i);
+  else chain_role_rp(b, i);
 }
 
 // One lane per set after the four roles: the set's fate.

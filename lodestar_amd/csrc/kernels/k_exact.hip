@@ -6,7 +6,10 @@
 
 using namespace bls;
 
-__global__ __launch_bounds__(BLS_BLOCK, 2) void k_exact(PipeBufs b) {
+// One wavefront per SIMD: the full 512-register budget keeps its scratch within the
+// per-queue budget (lodestar_amd/build.py SCRATCH_BUDGET; at two per SIMD it spilled
+// 7.3 KB/lane); the kernel is rare and its lanes mostly idle, so occupancy is moot.
+__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_exact(PipeBufs b) {
   stage_exact_set(b, blockIdx.x * BLS_BLOCK + threadIdx.x);
 }
 

@@ -1,0 +1,184 @@
+// Miller loops split in two SIMT kernels (the aggregated-signature path's default):
+//
+//   k_mlq  one lane per item: the twist point T runs from Q = HQ through the 63
+//          doubling and 5 addition steps of |x| = 0xd201000000010000 (bls/pairing.hpp
+//          miller_dbl_step / miller_add_step) and writes each step's line, already
+//          evaluated at P = RP (l0 z^3, l2 XZ, l3 Y: 6 Fp), to a line buffer -- 68
+//          lines x 288 B per item, laid out line-major and lane-minor so a wavefront's
+//          stores and loads are 256-byte rows;
+//   k_mlf  one lane per TWO items of one product domain (a chunk, or a non-batchable
+//          request: PipeBufs::ml_dom): f = prod over both pairs' lines with ONE
+//          squaring of f per bit (blst's miller_loop_n likewise shares the
+//          squarings), conjugated (x < 0); f of the first item, 1 in the second.  Items
+//          of different domains, or the individually verified pass (units_paired = 0),
+//          run one f per item.
+//
+// Against the fused one-lane loop (k_mls: 6,803 Fp products per pair, f + T + lines
+// live together in one lane, 512 registers and spills): the line side takes ~1,920
+// products per pair with T, P and Q only; the f side 62 squarings (36) per two pairs
+// plus 68 sparse line products (39) per pair -> ~5,700 products per pair, each kernel
+// with half the live state.
+#define BLS_FP_D28 1
+#include <stdlib.h>
+
+#include "../launchers.hpp"
+#include "bls/pairing.hpp"
+
+using namespace bls;
+
+namespace {
+
+constexpr int ML_EVENTS = 68;          // 63 doublings + 5 additions
+constexpr int LINE_WORDS = 6 * 12;     // l0, l2, l3 (Fp2 each) as 32-bit words
+
+__device__ __forceinline__ bool ml_live(const PipeBufs& b, uint32_t i, uint32_t units_paired) {
+  if (!b.chain_live[i]) return false;
+  return !(units_paired && b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE);
+}
+
+// word w of line e of item k (stride = the launch's item count, padded to a wavefront)
+__device__ __forceinline__ size_t line_at(uint32_t stride, uint32_t k, int e, int w) {
+  return ((size_t)e * LINE_WORDS + w) * stride + k;
+}
+
+__device__ __forceinline__ void store_line(uint32_t* L, uint32_t stride, uint32_t k, int e, const G1Eval& P,
+                                           const Fp2& c0, const Fp2& c1, const Fp2& c2) {
+  const Fp2 l[3] = {fp2_mul_fp(c0, P.z3), fp2_mul_fp(c1, P.xz), fp2_mul_fp(c2, P.y)};
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int w = 0; w < 12; ++w) {
+      L[line_at(stride, k, e, 24 * j + w)] = l[j].c0.l[w];
+      L[line_at(stride, k, e, 24 * j + 12 + w)] = l[j].c1.l[w];
+    }
+}
+
+__device__ __forceinline__ void load_line(const uint32_t* L, uint32_t stride, uint32_t k, int e, Fp2& l0, Fp2& l2,
+                                          Fp2& l3) {
+  Fp2* l[3] = {&l0, &l2, &l3};
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int w = 0; w < 12; ++w) {
+      l[j]->c0.l[w] = L[line_at(stride, k, e, 24 * j + w)];
+      l[j]->c1.l[w] = L[line_at(stride, k, e, 24 * j + 12 + w)];
+    }
+}
+
+// Inlined copies of field.hpp's fp12_sqr / fp12_mul_line (out of line there, which puts
+// f on the stack at every call): here f stays in registers and only the Fp products are
+// calls.
+__device__ __forceinline__ Fp12 sqr12(const Fp12& a) {
+  const Fp6 ab = fp6_mul(a.c0, a.c1);
+  const Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  return Fp12{fp6_sub(fp6_sub(s, ab), fp6_mul_v(ab)), fp6_add(ab, ab)};
+}
+
+__device__ __forceinline__ Fp12 mul_line12(const Fp12& f, const Fp2& l0, const Fp2& l2, const Fp2& l3) {
+  const Fp6 aa = fp6_mul_01(f.c0, l0, l2);
+  const Fp6 bb = fp6_mul_1(f.c1, l3);
+  const Fp6 c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l2, l3)), aa), bb);
+  return Fp12{fp6_add(aa, fp6_mul_v(bb)), c1};
+}
+
+// prod over the lanes' G items (kk[0..G)) of their line products, one squaring per bit
+template <int G>
+__device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, const uint32_t* kk) {
+  Fp12 f = fp12_one();
+  int e = 0;
+  const uint64_t X = BLS_X_ABS;
+  for (int bit = 62; bit >= 0; --bit) {
+    if (bit != 62) f = sqr12(f);
+    const int adds = (int)((X >> bit) & 1ull);
+    for (int a = 0; a <= adds; ++a) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        Fp2 l0, l2, l3;
+        load_line(L, stride, kk[g], e, l0, l2, l3);
+        f = mul_line12(f, l0, l2, l3);
+      }
+      ++e;
+    }
+  }
+  return fp12_conj(f);
+}
+
+}  // namespace
+
+template <int W>
+__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlq(
+    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, uint32_t* L, uint32_t stride) {
+  const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (k >= count) return;
+  const uint32_t i = first + k;
+  if (!ml_live(b, i, units_paired)) return;
+  const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
+  G1J rp;
+  rp.x = ch[CH_RP + 0];
+  rp.y = ch[CH_RP + 1];
+  rp.z = ch[CH_RP + 2];
+  const G1Eval P = g1_eval_from_jac(rp);
+  G2A q;
+  q.x = Fp2{ch[CH_HQ + 0], ch[CH_HQ + 1]};
+  q.y = Fp2{ch[CH_HQ + 2], ch[CH_HQ + 3]};
+  q.inf = false;
+  G2Proj T;
+  T.x = q.x;
+  T.y = q.y;
+  T.z = fp2_one();
+  Fp2 c0, c1, c2;
+  int e = 0;
+  const uint64_t X = BLS_X_ABS;
+  for (int bit = 62; bit >= 0; --bit) {
+    miller_dbl_step(T, c0, c1, c2);
+    store_line(L, stride, k, e++, P, c0, c1, c2);
+    if ((X >> bit) & 1ull) {
+      miller_add_step(T, q, c0, c1, c2);
+      store_line(L, stride, k, e++, P, c0, c1, c2);
+    }
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlf(
+    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, const uint32_t* L, uint32_t stride) {
+  const uint32_t k0 = 2u * (blockIdx.x * BLS_BLOCK + threadIdx.x), k1 = k0 + 1u;
+  if (k0 >= count) return;
+  const uint32_t i0 = first + k0, i1 = first + k1;
+  const bool live0 = ml_live(b, i0, units_paired), live1 = k1 < count && ml_live(b, i1, units_paired);
+  if (live0 && live1 && units_paired && b.ml_dom && b.ml_dom[i0] == b.ml_dom[i1]) {
+    const uint32_t kk[2] = {k0, k1};
+    b.f[i0] = ml_f<2>(L, stride, kk);
+    b.f[i1] = fp12_one();
+    return;
+  }
+  if (live0) b.f[i0] = ml_f<1>(L, stride, &k0);
+  if (live1) b.f[i1] = ml_f<1>(L, stride, &k1);
+}
+
+// line buffer words for a launch of `count` items (stride padded to a wavefront)
+size_t mlq_line_words(uint32_t count) {
+  const size_t stride = ((size_t)count + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
+  return stride * ML_EVENTS * LINE_WORDS;
+}
+
+hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool own_only, uint32_t* lines,
+                         hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  const uint32_t stride = (count + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
+  static const int wq = [] {
+    const char* e = getenv("BLS_MLQ_WAVES");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  static const int wf = [] {
+    const char* e = getenv("BLS_MLF_WAVES");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  const uint32_t up = own_only ? 0u : 1u;
+  if (wq == 1) k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
+  else k_mlq<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
+  const uint32_t pairs = (count + 1) / 2;
+  if (wf == 2) k_mlf<2><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
+  else k_mlf<1><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
+  return hipGetLastError();
+}

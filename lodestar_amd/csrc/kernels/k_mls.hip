@@ -46,12 +46,8 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
 
 hipError_t launch_k_mls(const PipeBufs& b, uint32_t first, uint32_t count, bool own_only, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  // $BLS_MLS_WAVES=2: a 256-register budget (two wavefronts per SIMD, more spills)
-  static const int waves = [] {
-    const char* e = getenv("BLS_MLS_WAVES");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
-  if (waves == 2) k_mls<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, own_only ? 0u : 1u);
-  else k_mls<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, own_only ? 0u : 1u);
+  // one wavefront per SIMD: at two (256 registers) the loop spills 4,160 B/lane, and 16
+  // contexts of that exhausted the runtime's scratch (profiles/r03_scratch_out_of_resources.txt)
+  k_mls<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, own_only ? 0u : 1u);
   return hipGetLastError();
 }

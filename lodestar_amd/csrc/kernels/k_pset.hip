@@ -396,13 +396,15 @@ static uint32_t ml_pack(const PipeBufs& b) {
 hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s,
                         bool own_only) {
   if (count == 0) return hipSuccess;
-  // SIMT Miller loops (kernels/k_mls.hip) unless $BLS_ML_SIMT=0 or a test forces a
-  // cooperative packing (BLS_DEBUG_PACK)
-  static const bool simt = [] {
+  // SIMT Miller loops unless a test forces a cooperative packing (BLS_DEBUG_PACK):
+  // $BLS_ML_SIMT = 2 (default): lines then f (kernels/k_mlq.hip); 1: the fused
+  // one-lane loop (kernels/k_mls.hip); 0: the cooperative kernels below
+  static const int simt = [] {
     const char* e = getenv("BLS_ML_SIMT");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 2;
   }();
-  if (simt && b.pack == 0) return launch_k_mls(b, first, count, own_only, s);
+  if (simt == 2 && b.pack == 0 && b.ml_lines) return launch_k_mlqf(b, first, count, own_only, b.ml_lines, s);
+  if (simt >= 1 && b.pack == 0) return launch_k_mls(b, first, count, own_only, s);
   const uint32_t S = ml_pack(b), up = own_only ? 0u : 1u;
   static const bool small_frame = [] {
     const char* e = getenv("BLS_ML_SMALL_FRAME");

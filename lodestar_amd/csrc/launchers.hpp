@@ -58,3 +58,6 @@ hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStr
 hipError_t launch_k_mln(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_t first, uint32_t count,
                         hipStream_t s, bool own_only = false);
 hipError_t launch_k_mls(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, hipStream_t s);
+size_t mlq_line_words(uint32_t count);
+hipError_t launch_k_mlqf(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, uint32_t* lines,
+                         hipStream_t s);

@@ -103,6 +103,20 @@ int hs_mul_window_check(unsigned long long seed, int n) {
   return bad;
 }
 
+// curve.hpp jac_mul_glv (k_chain's [r] pk / [r] sig): [a + b mu]P for the G1 / G2 base
+// [m]g against [k]P by double-and-add over k = (a + b mu) mod r (k8: 8 little-endian
+// words, computed by the test); 1 when equal
+int hs_glv_check(uint32_t a, uint32_t b, const uint32_t* k8, uint64_t m, int g2) {
+  if (!g2) {
+    const G1A base = jac_to_aff(jac_mul_u64(jac_from_aff(g1_generator()), m));
+    G1J T[15];
+    return jac_eq(jac_mul_glv<Fp>(jac_from_aff(base), a, b, T), aff_mul_u256(base, k8)) ? 1 : 0;
+  }
+  const G2A base = jac_to_aff(jac_mul_u64(jac_from_aff(g2_generator()), m));
+  G2J T[15];
+  return jac_eq(jac_mul_glv<Fp2>(jac_from_aff(base), a, b, T), aff_mul_u256(base, k8)) ? 1 : 0;
+}
+
 unsigned long long hs_fpm_count(void) { return bls_fpm_counter; }
 void hs_fpm_reset(void) { bls_fpm_counter = 0; }
 

@@ -287,3 +287,23 @@ def test_windowed_scalar_mul_matches_double_and_add(hostsim):
     hostsim.hs_mul_window_check.restype = ctypes.c_int
     hostsim.hs_mul_window_check.argtypes = [ctypes.c_ulonglong, ctypes.c_int]
     assert hostsim.hs_mul_window_check(20261017, 24) == 0
+
+
+def test_glv_scalar_mul_matches_full_scalar(hostsim):
+    """k_chain's [r] pk / [r] sig as [a]P + [b]endo(P) (curve.hpp jac_mul_glv) equals [k]P
+    by double-and-add for k = (a + b mu) mod r, mu = -x^2: the G1 endomorphism sigma and
+    -psi^2 on G2 both act as [mu] (the eigenvalue the scalar split relies on)."""
+    import random
+
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    X = -0xD201000000010000
+    mu = (-X * X) % R
+    hostsim.hs_glv_check.restype = ctypes.c_int
+    hostsim.hs_glv_check.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int]
+    rng = random.Random(7)
+    cases = [(0, 1), (1, 0), (0xFFFFFFFF, 0xFFFFFFFF), (1, 1), (3, 0), (0, 3)] + \
+            [(rng.getrandbits(32), rng.getrandbits(32)) for _ in range(10)]
+    for k, (a, b) in enumerate(cases):
+        kk = ((a + b * mu) % R).to_bytes(32, "little")
+        for g2 in (0, 1):
+            assert hostsim.hs_glv_check(a, b, kk, 1000003 + k, g2) == 1, (a, b, g2)

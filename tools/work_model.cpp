@@ -25,7 +25,7 @@ static unsigned long long tick() {
 
 int main() {
   const int N = 64;  // sets (messages, scalars) averaged over
-  double pre = 0, h = 0, c = 0, rs = 0, rp = 0, gadd = 0, vset = 0, ml = 0, f12m = 0;
+  double pre = 0, h = 0, c = 0, rs = 0, rp = 0, gadd = 0, vset = 0, ml = 0, f12m = 0, mlq = 0, mlf = 0;
   uint32_t seed[8] = {1, 2, 3, 4, 5, 6, 7, 8};
   G2J prev = jac_infinity<Fp2>();
   for (int k = 0; k < N; ++k) {
@@ -58,12 +58,42 @@ int main() {
     // role 1: psi(sig) == [x] sig
     (void)jac_eq(g2_psi(jac_from_aff(sig)), jac_neg(aff_mul_u64(sig, (uint64_t)BLS_X_ABS)));
     c += tick();
-    // role 2: [r] sig (affine base, mixed additions: k_chain's g2_mul_aff)
-    const G2J RS = aff_mul_u64(sig, r);
+    // role 2: [r] sig, r = a + b mu applied as [a] sig + [b] (-psi^2 sig) (curve.hpp
+    // jac_mul_glv, k_chain's g2_mul_r)
+    uint32_t ga, gb;
+    glv_split(r, ga, gb);
+    G2J T2[15];
+    const G2J RS = jac_mul_glv<Fp2>(jac_from_aff(sig), ga, gb, T2);
     rs += tick();
-    // role 3: [r] pk
-    const G1J rpk = jac_mul_u64(pk, r);
+    // role 3: [r] pk (sigma = [mu] on G1)
+    G1J T1[15];
+    const G1J rpk = jac_mul_glv<Fp>(pk, ga, gb, T1);
     rp += tick();
+    // k_mlq: the twist-point chain and its 68 lines evaluated at P
+    {
+      const G1Eval P = g1_eval_from_jac(rpk);
+      G2Proj T;
+      T.x = sig.x;
+      T.y = sig.y;
+      T.z = fp2_one();
+      Fp2 c0, c1, c2;
+      for (int bit = 62; bit >= 0; --bit) {
+        miller_dbl_step(T, c0, c1, c2);
+        (void)fp2_mul_fp(c0, P.z3), (void)fp2_mul_fp(c1, P.xz), (void)fp2_mul_fp(c2, P.y);
+        if ((BLS_X_ABS >> bit) & 1ull) {
+          miller_add_step(T, sig, c0, c1, c2);
+          (void)fp2_mul_fp(c0, P.z3), (void)fp2_mul_fp(c1, P.xz), (void)fp2_mul_fp(c2, P.y);
+        }
+      }
+      mlq += tick();
+      // k_mlf: two pairs per f -- 62 squarings and 2 x 68 sparse line products, per pair
+      Fp12 g = fp12_one();
+      for (int bit = 62; bit >= 0; --bit) {
+        if (bit != 62) g = fp12_sqr(g);
+        for (int rep = 0; rep < (((BLS_X_ABS >> bit) & 1ull) ? 4 : 2); ++rep) g = fp12_mul_line(g, c0, c1, c2);
+      }
+      mlf += tick() / 2.0;
+    }
     // k_mls: one SIMT Miller loop per set (f of its own, no squaring shared)
     const Fp12 f = miller_loop(g1_eval_from_jac(rpk), sig);
     ml += tick();
@@ -81,7 +111,7 @@ int main() {
   }
   printf("{\"sets_averaged\": %d, \"k_pre\": %.1f, \"chain_h\": %.1f, \"chain_subgroup\": %.1f, "
          "\"chain_r_sig\": %.1f, \"chain_r_pk\": %.1f, \"gsum_add\": %.1f, \"vset\": %.1f, \"ml_simt\": %.1f, "
-         "\"fp12_mul\": %.1f}\n",
-         N, pre / N, h / N, c / N, rs / N, rp / N, gadd / N, vset / N, ml / N, f12m / N);
+         "\"fp12_mul\": %.1f, \"ml_lines\": %.1f, \"ml_f_pair\": %.1f}\n",
+         N, pre / N, h / N, c / N, rs / N, rp / N, gadd / N, vset / N, ml / N, f12m / N, mlq / N, mlf / N);
   return 0;
 }
