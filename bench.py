@@ -24,7 +24,15 @@ Multi-GPU (torchrun, one process per GPU):
   --mode sharded: cfg4/cfg5 shape -- ONE call of (sets x world) sets split across
       the ranks (lodestar_amd.shard.verify_call_sharded): per rank an Fp12 partial of
       its shard, an all-gather of 588-byte records over RCCL/xGMI, one final
-      exponentiation; a step is one such call.
+      exponentiation; a step is one such call.  --shape cfg4 / cfg5: four calls of the
+      cfg4 mix (aggregates of --cfg4-agg-k keys, invalid sets) or of committee-shared
+      roots, each split over the ranks, failing calls localised to their bad shards
+      inside the timed region.
+  --mode cfg4 / cfg5: BASELINE configs 4 and 5 sharded by call -- rank r verifies
+      calls c with c % world == r of the range-sync job (--cfg4-sets per GPU, 1 %
+      invalid, 128-set non-batchable calls) or its own epoch slice (--cfg5-sets over
+      --cfg5-roots committee roots, 1024-set batchable calls, invalid sets); no
+      data-path collective; verdicts checked every pass.
   --mode napi: the same cfg2 workload driven through the N-API addon and the JS
       GpuBlsVerifier (integration/js), one verifySignatureSets([set], {batchable})
       per set, as gossip validation calls it (N = 1 only).
@@ -411,6 +419,124 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
     return res
 
 
+def run_job_slice(ctxs, w, calls_per_pass: int, steps: int, warmup: int, dist=None) -> dict:
+    """--mode cfg4 / cfg5 (shard by call): this rank's calls of the job
+    (workloads.cfg4_slice / cfg5_slice with rank / world), `calls_per_pass` per
+    bls_gpu_verify_many pass on every context; `steps` passes over the whole slice
+    inside the timed region, verdicts checked against the sets' validity by
+    construction after each.  Invalid sets run the merged-check failure and
+    per-request fallback paths inside the region.  `ctxs` are GpuContexts on the box (any
+    object with verify_many(list[PackedBatch]) -> (verdicts, stats) in the gloo dry
+    run).  Returns elapsed (s, this rank), sets verified, stats totals."""
+    from lodestar_amd import workloads as W
+
+    pbs = W.packed_calls(w)
+    for _ in range(warmup):
+        run_calls(ctxs, pbs[: len(ctxs) * calls_per_pass], calls_per_pass)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    tot = {"batch_retries": 0, "batch_sigs_success": 0, "merged_fail": 0}
+    false_req = 0
+    for _ in range(steps):
+        _, out, st = run_calls(ctxs, pbs, calls_per_pass)
+        bad = [k for k in range(len(pbs)) if not W.verdicts_ok(w, k, out[k])]
+        assert not bad, f"{len(bad)} calls with wrong verdicts (first {bad[0]})"
+        for k in tot:
+            tot[k] += st[k]
+        false_req += sum(int((o == 0).sum()) for o in out)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    return {"elapsed_s": elapsed, "sets": w.n_sets * steps, "calls": len(pbs) * steps, "false_requests": false_req,
+            **tot}
+
+
+def expected_bad_shards(valid: list[bool], world: int) -> list[int]:
+    """Ranks whose contiguous slice (shard.shard_bounds) of a sharded call holds an
+    invalid set: what verify_call_sharded's localisation must report."""
+    from lodestar_amd.shard import shard_bounds
+
+    return [k for k, (b, e) in enumerate(shard_bounds(len(valid), world)) if not all(valid[b:e])]
+
+
+def run_sharded_job(be, w, seed, steps, warmup, dist, device) -> dict:
+    """--mode sharded --shape cfg4 / cfg5: every call of workload `w` (identical on every
+    rank) is ONE call split over the ranks (verify_call_sharded): per-rank Fp12 partials,
+    one all-gather of 588-byte records, one final exponentiation, and for a failing call
+    the localisation (each rank's own final exponentiation + an all-gather of one byte),
+    all inside the timed region.  The verdict and bad_shards of every call are checked
+    against the sets' validity by construction."""
+    from lodestar_amd.shard import verify_call_sharded
+
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+
+    def one_pass():
+        for sets, valid in zip(w.calls, w.valid):
+            ok, info = verify_call_sharded(sets, seed, be, dist, device, localize=True)
+            assert ok is all(valid), f"sharded call verdict {ok}, expected {all(valid)}"
+            assert info["bad_shards"] == expected_bad_shards(valid, world), info
+    for _ in range(warmup):
+        one_pass()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_pass()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    return {"elapsed_s": elapsed, "sets": w.n_sets * steps, "calls": len(w.calls) * steps,
+            "failing_calls": sum(not all(v) for v in w.valid) * steps}
+
+
+def bench_job(args, ctxs, rank: int, world: int, dist, device, make_backend) -> dict:
+    """--mode cfg4 / cfg5 (shard by call) and --mode sharded --shape cfg4 / cfg5 (each
+    call split over the ranks).  The device pubkey table (args.table_keys interop keys)
+    is loaded into every context first.  Returns rank 0's JSON record (value: all
+    ranks' sets / the slowest rank's timed region)."""
+    from lodestar_amd import workloads as W
+    from lodestar_amd.shard import global_throughput
+
+    W.load_table(ctxs, args.table_keys)
+    if args.mode == "cfg4":
+        w = W.cfg4_slice(ctxs[0], args.table_keys, args.cfg4_sets * world, rank=rank, world=world,
+                         call_sets=args.cfg4_call_sets, agg_k=args.cfg4_agg_k, invalid_frac=args.cfg4_invalid)
+        res = run_job_slice(ctxs, w, max(1, 4096 // args.cfg4_call_sets), args.steps, args.warmup, dist)
+        workload = (f"cfg4 range-sync job of {args.cfg4_sets * world} sets sharded by call over {world} GPU(s) "
+                    f"(this rank: {w.note})")
+        par = f"shard-by-call x{world}"
+    elif args.mode == "cfg5":
+        w = W.cfg5_slice(ctxs[0], args.table_keys, args.cfg5_sets, args.cfg5_roots, call_sets=args.cfg5_call_sets,
+                         invalid=max(1, args.cfg5_sets // 2048), rank=rank)
+        res = run_job_slice(ctxs, w, 8, args.steps, args.warmup, dist)
+        workload = f"cfg5 epoch slice per GPU, shard by call over {world} GPU(s) (this rank: {w.note})"
+        par = f"shard-by-call x{world}"
+    else:  # sharded
+        n_call = args.sets * world
+        if args.shape == "cfg4":
+            w = W.cfg4_slice(ctxs[0], args.table_keys, 4 * n_call, call_sets=n_call, agg_k=args.cfg4_agg_k,
+                             invalid_frac=args.cfg4_invalid / 50)
+        else:
+            w = W.cfg5_slice(ctxs[0], args.table_keys, 4 * n_call, 8, call_sets=n_call, invalid=2)
+        seed = hashlib.sha256(b"sharded-job").digest()
+        res = run_sharded_job(make_backend(ctxs[0]), w, seed, args.steps, args.warmup, dist, device)
+        workload = (f"{args.shape} sharded calls: each of {len(w.calls)} calls of {n_call} sets split over {world} "
+                    f"GPU(s) (per-rank Fp12 partial, 588-byte all-gather, one final exponentiation, bad-shard "
+                    f"localisation of failing calls); {w.note}")
+        par = f"sharded-call x{world}"
+    value, elapsed = global_throughput(res["sets"] if args.mode != "sharded" else res["sets"] / world,
+                                       res["elapsed_s"], dist, device=device)
+    return {"metric": METRIC, "value": round(value, 2), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u32 (381-bit Fp, 12x32-bit Montgomery limbs)",
+            "data": "synthetic: interop keys, sha256 messages, GPU-made signatures, invalid sets by construction",
+            "config": {"workload": workload, "parallelism": par, "table_keys": args.table_keys,
+                       "contexts_per_gpu": len(ctxs)},
+            "job": {k: v for k, v in res.items() if k != "elapsed_s"}}
+
+
 def run_sharded(be, sets, seed, steps, warmup, dist, device):
     """--mode sharded: `steps` calls, each ONE call of every rank's sets (world x sets),
     verified as one random-scalar batch through verify_call_sharded with the partial
@@ -466,7 +592,16 @@ def main() -> None:
     ap.add_argument("--calls-per-pass", type=int, default=8,
                     help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "
                          "its own chunks and verdicts)")
-    ap.add_argument("--mode", choices=("cfg2", "sharded", "napi"), default="cfg2")
+    ap.add_argument("--mode", choices=("cfg2", "sharded", "napi", "cfg4", "cfg5"), default="cfg2")
+    ap.add_argument("--shape", choices=("cfg2", "cfg4", "cfg5"), default="cfg2",
+                    help="--mode sharded: the sets of the split call (cfg2 all-valid single sets; cfg4 the range-sync "
+                         "mix with aggregates and invalid sets; cfg5 committee-shared roots with invalid sets)")
+    ap.add_argument("--cfg4-call-sets", type=int, default=128, help="sets per cfg4 call (range sync's batches)")
+    ap.add_argument("--cfg4-agg-k", type=int, default=128, help="keys per cfg4 aggregate set")
+    ap.add_argument("--cfg4-invalid", type=float, default=0.01, help="fraction of invalid cfg4 sets")
+    ap.add_argument("--cfg5-sets", type=int, default=131_072, help="sets per GPU of --mode cfg5 (1M / 8)")
+    ap.add_argument("--cfg5-call-sets", type=int, default=1024, help="sets per cfg5 call (gossip buffering)")
+    ap.add_argument("--cfg5-roots", type=int, default=256, help="committee roots per GPU of --mode cfg5 (2048 / 8)")
     ap.add_argument("--roots", type=int, default=0,
                     help="distinct signing roots per call (0: all distinct, cfg2; 2: the cfg5 committee shape)")
     ap.add_argument("--no-dedup", action="store_true", help="hash every set's root (BLS_DEBUG_NO_MSG_DEDUP)")
@@ -501,9 +636,23 @@ def main() -> None:
 
     from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK, DEBUG_NO_MSG_DEDUP, DEBUG_NO_UNITS
     from lodestar_amd.native import GpuContext
-    from lodestar_amd.shard import global_throughput
+    from lodestar_amd.shard import GpuPartialBackend, global_throughput
 
-    flags = ((DEBUG_NO_MSG_DEDUP if args.no_dedup else 0) | (DEBUG_NO_MERGED_CHECK if args.no_merged_check else 0)
+    if args.mode in ("cfg4", "cfg5") or (args.mode == "sharded" and args.shape != "cfg2"):
+        ctxs = [GpuContext(local_rank) for _ in range(args.inflight if args.mode != "sharded" else 1)]
+        try:
+            out = bench_job(args, ctxs, rank, world, dist, device,
+                            lambda c: GpuPartialBackend(c))
+        finally:
+            for c in ctxs:
+                c.close()
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    flags =((DEBUG_NO_MSG_DEDUP if args.no_dedup else 0) | (DEBUG_NO_MERGED_CHECK if args.no_merged_check else 0)
              | (DEBUG_NO_UNITS if args.no_units else 0))
     inflight = args.inflight if args.mode == "cfg2" else 1
     ctxs = [GpuContext(local_rank) for _ in range(inflight)]

@@ -641,6 +641,53 @@ static void plan_batch_msgs(const bls_batch* in, const std::vector<uint32_t>& re
   }
 }
 
+// Host-side shape checks of one caller batch (0, or -2 with ctx->err).  The kernels and
+// the verify_many join index sets and key lists through these offsets, so they must
+// start at 0, be monotone and end at the array sizes.
+static int check_batch(bls_gpu_ctx* ctx, const bls_batch* in, const char* what) {
+  const uint32_t n = in->n_sets, R = in->n_reqs;
+  if (R == 0) return 0;
+  if (!in->req_set_offsets) {
+    snprintf(ctx->err, sizeof(ctx->err), "%s: req_set_offsets missing", what);
+    return -2;
+  }
+  if (in->req_set_offsets[0] != 0 || in->req_set_offsets[R] != n) {
+    snprintf(ctx->err, sizeof(ctx->err), "%s: req_set_offsets must run from 0 to n_sets", what);
+    return -2;
+  }
+  if (in->set_pk_offsets == nullptr && in->pubkeys == nullptr && n > 0) {
+    snprintf(ctx->err, sizeof(ctx->err), "%s: no pubkeys given", what);
+    return -2;
+  }
+  if (n > 0 && (!in->messages || !in->signatures)) {
+    snprintf(ctx->err, sizeof(ctx->err), "%s: messages / signatures missing", what);
+    return -2;
+  }
+  for (uint32_t r = 0; r < R; ++r) {
+    if (in->req_set_offsets[r] > in->req_set_offsets[r + 1]) {
+      snprintf(ctx->err, sizeof(ctx->err), "%s: req_set_offsets not monotone at %u", what, r);
+      return -2;
+    }
+  }
+  if (in->set_pk_offsets) {
+    if (in->set_pk_offsets[0] != 0) {
+      snprintf(ctx->err, sizeof(ctx->err), "%s: set_pk_offsets[0] != 0", what);
+      return -2;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      if (in->set_pk_offsets[i] > in->set_pk_offsets[i + 1]) {
+        snprintf(ctx->err, sizeof(ctx->err), "%s: set_pk_offsets not monotone at %u", what, i);
+        return -2;
+      }
+    }
+    if (in->set_pk_offsets[n] > 0 && !in->pk_indices) {
+      snprintf(ctx->err, sizeof(ctx->err), "%s: pk_indices missing", what);
+      return -2;
+    }
+  }
+  return 0;
+}
+
 static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats,
                        uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status,
                        uint32_t* partial_err = nullptr, const std::vector<uint32_t>* req_bounds = nullptr) {
@@ -650,37 +697,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   const uint32_t n = in->n_sets, R = in->n_reqs;
   if (stats) memset(stats, 0, sizeof(*stats));
   if (R == 0) return 0;
-  if (in->req_set_offsets[R] != n) {
-    snprintf(ctx->err, sizeof(ctx->err), "req_set_offsets[n_reqs] != n_sets");
-    return -2;
-  }
-  if (in->set_pk_offsets == nullptr && in->pubkeys == nullptr && n > 0) {
-    snprintf(ctx->err, sizeof(ctx->err), "no pubkeys given");
-    return -2;
-  }
-  if (n > 0 && (!in->messages || !in->signatures)) {
-    snprintf(ctx->err, sizeof(ctx->err), "messages / signatures missing");
-    return -2;
-  }
-  // the kernels index sets and key lists through these offsets: they must be monotone
-  for (uint32_t r = 0; r < R; ++r) {
-    if (in->req_set_offsets[r] > in->req_set_offsets[r + 1]) {
-      snprintf(ctx->err, sizeof(ctx->err), "req_set_offsets not monotone at %u", r);
-      return -2;
-    }
-  }
-  if (in->set_pk_offsets) {
-    if (in->set_pk_offsets[0] != 0) {
-      snprintf(ctx->err, sizeof(ctx->err), "set_pk_offsets[0] != 0");
-      return -2;
-    }
-    for (uint32_t i = 0; i < n; ++i) {
-      if (in->set_pk_offsets[i] > in->set_pk_offsets[i + 1]) {
-        snprintf(ctx->err, sizeof(ctx->err), "set_pk_offsets not monotone at %u", i);
-        return -2;
-      }
-    }
-  }
+  if (const int rc = check_batch(ctx, in, "batch")) return rc;
   BatchPlan plan;
   if (req_bounds) plan_batch_msgs(in, *req_bounds, plan);
   else plan_batch(in, plan);
@@ -1198,13 +1215,17 @@ int bls_gpu_verify_many(bls_gpu_ctx* ctx, const bls_batch* batches, uint32_t n_b
     }
     return 0;
   }
-  // one pass over the concatenated messages (SoA arrays joined, offsets rebased)
+  // one pass over the concatenated messages (SoA arrays joined, offsets rebased); each
+  // message passes verify_impl's shape checks before anything is read through it
   uint32_t n = 0, R = 0, n_idx = 0;
   bool lens = false;
   for (uint32_t k = 0; k < n_batches; ++k) {
     const bls_batch& b = batches[k];
-    if (b.n_reqs && b.req_set_offsets[b.n_reqs] != b.n_sets) {
-      snprintf(ctx->err, sizeof(ctx->err), "batch %u: req_set_offsets[n_reqs] != n_sets", k);
+    char what[32];
+    snprintf(what, sizeof(what), "batch %u", k);
+    if (const int rc = check_batch(ctx, &b, what)) return rc;
+    if (b.n_reqs == 0 && b.n_sets != 0) {
+      snprintf(ctx->err, sizeof(ctx->err), "%s: sets without requests", what);
       return -2;
     }
     n += b.n_sets;

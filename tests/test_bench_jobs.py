@@ -1,0 +1,172 @@
+"""bench.py's multi-GPU job modes, dry run on CPU (gloo, world_size 2):
+
+  --mode cfg4     the range-sync job sharded by call (aggregates, invalid sets, the
+                  non-batchable 128-set calls at reduced size);
+  --mode cfg5     each rank's epoch slice (committee-shared roots, invalid sets);
+  --mode sharded  --shape cfg4 / cfg5: every call split over the ranks, Fp12 partials,
+                  one final exponentiation, bad-shard localisation of failing calls.
+
+The bench's own functions (bench_job -> run_job_slice / run_sharded_job, the verdict
+checks against validity by construction, the max-over-ranks reduction) run unchanged;
+only the per-rank device is replaced by the oracle (test infrastructure, never the
+product): OracleCtx restates bls_gpu_verify_many with oracle.verify_many_signature_sets
+(worker.ts:32-108) over the same packed calls, OraclePartialBackend the shard partials.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+
+class OracleCtx:
+    """The GpuContext calls bench_job makes, answered by the oracle on the CPU."""
+
+    def __init__(self):
+        from oracle import bls_oracle as O
+
+        self.O = O
+        self.table = []
+
+    def sk_to_pk(self, blob: bytes) -> np.ndarray:
+        O = self.O
+        sks = [int.from_bytes(blob[k:k + 32], "big") for k in range(0, len(blob), 32)]
+        return np.array([list(O.g1_compress(O.sk_to_pk(s))) for s in sks], dtype=np.uint8)
+
+    def load_pubkeys(self, pks: bytes, width: int) -> np.ndarray:
+        assert width == 48
+        for k in range(0, len(pks), 48):
+            code, pt = self.O.g1_decompress(pks[k:k + 48])
+            assert code == self.O.E_OK
+            self.table.append(pt)
+        return np.zeros(len(pks) // 48, dtype=np.int32)
+
+    def sign(self, sks: bytes, msgs: bytes) -> np.ndarray:
+        O = self.O
+        out = [O.g2_compress(O.sign(int.from_bytes(sks[32 * k:32 * k + 32], "big"), msgs[32 * k:32 * k + 32]))
+               for k in range(len(sks) // 32)]
+        return np.array([list(s) for s in out], dtype=np.uint8)
+
+    def aggregate(self, idx):
+        return self.O.aggregate_pubkeys([self.table[i] for i in idx])
+
+    def _requests(self, pb):
+        reqs = []
+        for r in range(len(pb.req_batchable)):
+            sets = []
+            for i in range(int(pb.req_set_offsets[r]), int(pb.req_set_offsets[r + 1])):
+                idx = pb.pk_indices[pb.set_pk_offsets[i]:pb.set_pk_offsets[i + 1]]
+                n = int(pb.signature_lens[i]) if pb.signature_lens is not None else 96
+                sets.append((self.aggregate([int(x) for x in idx]), pb.messages[32 * i:32 * i + 32].tobytes(),
+                             pb.signatures[96 * i:96 * i + n].tobytes()))
+            reqs.append((bool(pb.req_batchable[r]), sets))
+        return reqs
+
+    def verify_many(self, pbs):
+        verdicts, retries, ok = [], 0, 0
+        for pb in pbs:
+            res, rt, good = self.O.verify_many_signature_sets(self._requests(pb))
+            verdicts.append(np.array([(1 if v else 0) if kind == "success" else -v.code for kind, v in res],
+                                     dtype=np.int32))
+            retries += rt
+            ok += good
+        return verdicts, SimpleNamespace(batch_retries=retries, batch_sigs_success=ok, merged_check=0)
+
+
+class OraclePartialBackend:
+    """shard.GpuPartialBackend's two calls over table-index sets, by the oracle."""
+
+    def __init__(self, ctx: OracleCtx):
+        self.ctx = ctx
+        self.O = ctx.O
+
+    def partial(self, sets, base, seed):
+        import hashlib
+
+        O = self.O
+        f = O.F12_ONE
+        for k, (idx, msg, sig) in enumerate(sets):
+            s = O.signature_from_bytes(sig, validate=True)
+            r = int.from_bytes(hashlib.sha256(seed + (base + k).to_bytes(4, "little")).digest()[:8], "big") or 1
+            f = O.f12_mul(f, O.miller_loop(O.E1.mul(self.ctx.aggregate(idx), r), O.hash_to_g2(msg)))
+            f = O.f12_mul(f, O.miller_loop(O.E1.neg(O.G1), O.E2.mul(s, r)))
+        return b"".join(v.to_bytes(48, "big") for c in f for v in c), 0, None
+
+    def final_check(self, partials):
+        O = self.O
+        f = O.F12_ONE
+        for p in partials:
+            w = [int.from_bytes(p[48 * k: 48 * k + 48], "big") for k in range(12)]
+            f = O.f12_mul(f, [(w[2 * j], w[2 * j + 1]) for j in range(6)])
+        return O.f12_is_one(O.final_exponentiation(f))
+
+
+def _args(**kw):
+    base = dict(mode="cfg4", shape="cfg2", table_keys=16, steps=1, warmup=0, sets=4, cfg4_sets=16,
+                cfg4_call_sets=8, cfg4_agg_k=4, cfg4_invalid=0.1, cfg5_sets=16, cfg5_roots=2, cfg5_call_sets=8)
+    base.update(kw)
+    return argparse.Namespace(**base)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+CASES = {"cfg4": dict(mode="cfg4"), "cfg5": dict(mode="cfg5"),
+         "sharded_cfg4": dict(mode="sharded", shape="cfg4", cfg4_invalid=3.0),
+         "sharded_cfg5": dict(mode="sharded", shape="cfg5")}
+
+
+def _job_rank(rank, world, port, case, q):
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = bench.bench_job(_args(**CASES[case]), [OracleCtx()], rank, world, dist, None, OraclePartialBackend)
+        q.put((rank, out))
+    except BaseException as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_bench_job_modes_gloo_world2(case):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_job_rank, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert isinstance(res[r], dict), res[r]
+        assert p.exitcode == 0
+    out = res[0]
+    job0, job1 = res[0]["job"], res[1]["job"]
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    if case == "cfg4":
+        # 32 sets in 4 calls of 8, two per rank; the aggregates and invalid sets of the draw
+        assert job0["sets"] + job1["sets"] == 32 and job0["calls"] == job1["calls"] == 2
+        assert job0["false_requests"] + job1["false_requests"] >= 1
+    elif case == "cfg5":
+        assert job0["sets"] == job1["sets"] == 16
+        assert job0["false_requests"] >= 1 and job0["batch_retries"] >= 1
+    else:
+        assert job0["calls"] == 4 and job0["sets"] == 32
+        if case == "sharded_cfg4":
+            assert job0["failing_calls"] >= 1

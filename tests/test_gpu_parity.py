@@ -788,3 +788,59 @@ def test_verify_many_matches_separate_calls(gpu, oracle, table):
                            (True, [(raw[1], msgs[0][1], sigs[1].tobytes())])])
     many2, _ = gpu.verify_many([pbs[0], rawpb])
     assert list(many2[0]) == list(sep[0][0]) and list(many2[1]) == [1, 1]
+
+
+def test_verify_many_merged_signature_sum_fails(gpu, oracle, table, verify_path):
+    """bls_gpu_verify_many with every request batchable across four messages (the
+    bench's pass shape): the merged check (one final exponentiation over the pass, one
+    summed signature pairing) runs over the joined messages; one invalid set makes it
+    fail (merged_check == 2), each chunk's signature sum is rebuilt and paired, and every
+    message still gets the verdicts and stats of its own call (worker.ts:56-88)."""
+    sks = _keys(oracle, 16)
+    sizes = [64, 48, 80, 33]
+    msgs = [[_h(b"mmany%d-%d" % (k, i)) for i in range(n)] for k, n in enumerate(sizes)]
+    flat = [m for ms in msgs for m in ms]
+    sigs = gpu.sign(b"".join(sks[j % 16] for j in range(len(flat))), b"".join(flat))
+    pbs, j = [], 0
+    for k, n in enumerate(sizes):
+        reqs = []
+        for i in range(n):
+            m = msgs[k][i] if (k, i) != (2, 41) else _h(b"mtampered")
+            reqs.append((True, [([j % 16], m, sigs[j].tobytes())]))
+            j += 1
+        pbs.append(pack_requests(reqs))
+    sep = [gpu.verify_packed(pb) for pb in pbs]
+    many, st = gpu.verify_many(pbs)
+    for (v, _), w in zip(sep, many):
+        assert list(v) == list(w)
+    assert many[2][41] == 0 and sum(int((w == 1).sum()) for w in many) == sum(sizes) - 1
+    assert st.merged_check == 2
+    exp = [_expected_stats(oracle, [0 if (k, i) == (2, 41) else 1 for i in range(n)]) for k, n in enumerate(sizes)]
+    assert st.batch_retries == sum(e[0] for e in exp) and st.batch_sigs_success == sum(e[1] for e in exp)
+    # all valid: the merged check passes over the joined messages
+    good = []
+    j = 0
+    for k, n in enumerate(sizes):
+        good.append(pack_requests([(True, [([(j + i) % 16], msgs[k][i], sigs[j + i].tobytes())]) for i in range(n)]))
+        j += n
+    many, st = gpu.verify_many(good)
+    assert all((w == 1).all() for w in many) and st.merged_check == 1
+
+
+@pytest.mark.parametrize("n,bad", [(80, 41), (128, 70), (256, 130), (80, 1), (80, 79)])
+def test_failed_chunk_requests_verified_alone(gpu, oracle, table, n, bad):
+    """One invalid set in a middle chunk: the merged check fails, the chunk fails, and
+    its 16 requests are verified alone (worker.ts:81-87) -- every other request of the
+    chunk is true.  Regression: the split SIMT Miller loops (kernels/k_mlq.hip k_mlf)
+    read the product-domain table past its end for the individual requests' signature
+    sums and paired two requests into one f, so at these sizes every request of the
+    failed chunk came back false."""
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"alone%d-%d" % (n, i)) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    reqs = [(True, [([i % 16], msgs[i] if i != bad else _h(b"alone-x"), sigs[i].tobytes())]) for i in range(n)]
+    expect = [0 if i == bad else 1 for i in range(n)]
+    v, st = gpu.verify_packed(pack_requests(reqs))
+    assert list(v) == expect
+    retries, ok = _expected_stats(oracle, expect)
+    assert (st.batch_retries, st.batch_sigs_success, st.merged_check) == (retries, ok, 2)
