@@ -608,6 +608,9 @@ def main() -> None:
     ap.add_argument("--no-units", action="store_true",
                     help="one Miller loop per set even for shared roots (BLS_DEBUG_NO_UNITS)")
     ap.add_argument("--no-sub-records", action="store_true", help="skip the cfg3 / cfg4 sub-records")
+    ap.add_argument("--probe-only", action="store_true",
+                    help="counter / trace runs: the warm-up and timed passes only (no latency, solo, peak or CPU "
+                         "legs), so a profile holds exactly those launches")
     ap.add_argument("--table-keys", type=int, default=1 << 20, help="device pubkey table of the cfg3 / cfg4 records")
     ap.add_argument("--cfg4-sets", type=int, default=125_000,
                     help="sets of this GPU's cfg4 slice (1M sets over 8 GPUs by call)")
@@ -759,6 +762,14 @@ def main() -> None:
                "data": "synthetic: interop keys, sha256 messages, GPU-made signatures", "config": config}
         out.update(extra)
 
+    if args.probe_only:
+        for c in ctxs:
+            c.close()
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     if args.mode != "napi":
         # p50 latency of one 128-set non-batchable call (cfg1 shape)
         lat = []

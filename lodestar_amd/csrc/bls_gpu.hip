@@ -796,6 +796,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   uint32_t* tseg_dev = nullptr;          // the merged signature sum's plan
   G2J* gtmp[2] = {nullptr, nullptr};
   uint32_t *unit_rep_dev = nullptr, *ugsets_dev = nullptr, *useg_dev = nullptr;  // Miller-loop units
+  uint32_t* own_sets_dev = nullptr;      // the individually verified sets' own Miller loops (one launch)
   G1J* utmp[2] = {nullptr, nullptr};
   auto carve = [&](Carver& c, PipeBufs& b, size_t& input_end) {
     b.req_off = c.take<uint32_t>(R + 1);
@@ -812,6 +813,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.sigs = c.take<uint8_t>(96ull * n);
     b.sig_lens = in->signature_lens ? c.take<uint32_t>(n) : nullptr;
     b.indiv_reqs = c.take<uint32_t>(R);
+    own_sets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
     b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
     b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
     gsets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
@@ -1105,7 +1107,15 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       // each individually verified request pairs the sum of its own r sig:
       // virtual sets indiv_vbase + t; a request whose sets were paired in their
       // chunk's units or shared loops (its chunk failed) now runs their own Miller loops
-      if (use_units || ml_shared) {
+      std::vector<uint32_t> own;  // outlives the staged copy (the stream is synchronised below)
+      if ((use_units || ml_shared) && k_mln_list_ok(b)) {
+        // one launch over every set of the failed chunks' requests
+        for (size_t t = plan.nonbatch_reqs.size(); t < indiv.size(); ++t)
+          for (uint32_t i = in->req_set_offsets[indiv[t]]; i < in->req_set_offsets[indiv[t] + 1]; ++i) own.push_back(i);
+        stage_copy(ctx, own_sets_dev, own.data(), sizeof(uint32_t) * own.size());
+        HIPC(ctx, launch_k_mln_list(b, own_sets_dev, (uint32_t)own.size(), s));
+        dbg_sync(s, "k_mln own (list)");
+      } else if (use_units || ml_shared) {
         // one launch per run of consecutive sets (a failed chunk's requests are adjacent)
         uint32_t run_beg = 0, run_end = 0;
         for (size_t t = plan.nonbatch_reqs.size(); t <= indiv.size(); ++t) {

@@ -31,6 +31,11 @@
 // variant chain_inl32 restores that one.
 #ifdef BLS_CHAIN_INL32
 #define BLS_FP_INLINE 1
+#elif defined(BLS_CHAIN_INL28)
+// build variant chain_inl28: the round-2 configuration that never finished (d28 product
+// inlined into the chains); the build's scratch guard rejects it
+#define BLS_FP_INLINE 1
+#define BLS_FP_D28 1
 #else
 #define BLS_FP_D28 1
 #endif
@@ -186,7 +191,10 @@ __device__ __noinline__ void chain_role_rp(const PipeBufs& b, uint32_t i) {
 }
 
 // Four roles per set, one wavefront per (role, 64 sets), so a call of n sets runs
-// 4 n / 64 wavefronts and its latency is the longest chain, not their sum:
+// 4 n / 64 wavefronts and its latency is the longest chain, not their sum (one kernel
+// per role, each with its own register budget, measured 5 % slower at 14 and 16
+// contexts x 8 calls: the four launches serialise on the context's stream,
+// profiles/r03_ab_chain_roles.json):
 //   role 0  H = clear_cofactor(iso(q0) + iso(q1)) -> HQ (affine)   ~2.9k Fp products,
 //           once per distinct signing root
 //   role 1  psi(sig) == [x] sig                                     ~1.2k

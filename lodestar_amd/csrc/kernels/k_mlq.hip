@@ -107,10 +107,11 @@ __device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, const u
 
 template <int W>
 __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlq(
-    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, uint32_t* L, uint32_t stride) {
+    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, uint32_t* L, uint32_t stride,
+    const uint32_t* items) {
   const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (k >= count) return;
-  const uint32_t i = first + k;
+  const uint32_t i = items ? items[k] : first + k;
   if (!ml_live(b, i, units_paired)) return;
   const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
   G1J rp;
@@ -141,10 +142,12 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
 
 template <int W>
 __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlf(
-    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, const uint32_t* L, uint32_t stride) {
+    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, const uint32_t* L, uint32_t stride,
+    const uint32_t* items) {
   const uint32_t k0 = 2u * (blockIdx.x * BLS_BLOCK + threadIdx.x), k1 = k0 + 1u;
   if (k0 >= count) return;
-  const uint32_t i0 = first + k0, i1 = first + k1;
+  // items: an index list (the individually verified pass: own loops only, no sharing)
+  const uint32_t i0 = items ? items[k0] : first + k0, i1 = items ? (k1 < count ? items[k1] : 0u) : first + k1;
   const bool live0 = ml_live(b, i0, units_paired), live1 = k1 < count && ml_live(b, i1, units_paired);
   // ml_dom covers the first-pass items [0, indiv_vbase) only: the individually verified
   // requests' signature sums after it never share (reading past it paired two requests'
@@ -166,7 +169,7 @@ size_t mlq_line_words(uint32_t count) {
 }
 
 hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool own_only, uint32_t* lines,
-                         hipStream_t s) {
+                         hipStream_t s, const uint32_t* items) {
   if (count == 0) return hipSuccess;
   const uint32_t stride = (count + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
   static const int wq = [] {
@@ -177,11 +180,11 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
     const char* e = getenv("BLS_MLF_WAVES");
     return e && atoi(e) == 2 ? 2 : 1;
   }();
-  const uint32_t up = own_only ? 0u : 1u;
-  if (wq == 1) k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
-  else k_mlq<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
+  const uint32_t up = (own_only || items) ? 0u : 1u;
+  if (wq == 1) k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
+  else k_mlq<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
   const uint32_t pairs = (count + 1) / 2;
-  if (wf == 2) k_mlf<2><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
-  else k_mlf<1><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride);
+  if (wf == 2) k_mlf<2><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
+  else k_mlf<1><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
   return hipGetLastError();
 }

@@ -393,16 +393,29 @@ static uint32_t ml_pack(const PipeBufs& b) {
 
 // own_only: sets run their own Miller loop even when they belong to a unit (requests
 // verified alone after their chunk failed)
-hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s,
-                        bool own_only) {
-  if (count == 0) return hipSuccess;
-  // SIMT Miller loops unless a test forces a cooperative packing (BLS_DEBUG_PACK):
-  // $BLS_ML_SIMT = 2 (default): lines then f (kernels/k_mlq.hip); 1: the fused
-  // one-lane loop (kernels/k_mls.hip); 0: the cooperative kernels below
+// SIMT Miller loops unless a test forces a cooperative packing (BLS_DEBUG_PACK):
+// $BLS_ML_SIMT = 2 (default): lines then f (kernels/k_mlq.hip); 1: the fused one-lane
+// loop (kernels/k_mls.hip); 0: the cooperative kernels below
+static int ml_simt() {
   static const int simt = [] {
     const char* e = getenv("BLS_ML_SIMT");
     return e ? atoi(e) : 2;
   }();
+  return simt;
+}
+
+bool k_mln_list_ok(const PipeBufs& b) { return ml_simt() == 2 && b.pack == 0 && b.ml_lines; }
+
+hipError_t launch_k_mln_list(const PipeBufs& b, const uint32_t* items, uint32_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  if (!k_mln_list_ok(b) || !items) return hipErrorInvalidValue;
+  return launch_k_mlqf(b, 0, count, true, b.ml_lines, s, items);
+}
+
+hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s,
+                        bool own_only) {
+  if (count == 0) return hipSuccess;
+  const int simt = ml_simt();
   if (simt == 2 && b.pack == 0 && b.ml_lines) return launch_k_mlqf(b, first, count, own_only, b.ml_lines, s);
   if (simt >= 1 && b.pack == 0) return launch_k_mls(b, first, count, own_only, s);
   const uint32_t S = ml_pack(b), up = own_only ? 0u : 1u;

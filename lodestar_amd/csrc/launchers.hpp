@@ -57,7 +57,12 @@ hipError_t launch_k_fprod(const bls::Fp12* in, uint32_t n, bls::Fp12* out, int32
 hipError_t launch_k_pset(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 hipError_t launch_k_mln(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_t first, uint32_t count,
                         hipStream_t s, bool own_only = false);
+// own Miller loops of the listed items (items[0, count)) in one launch: the split SIMT
+// kernels only (k_mln_list_ok); the individually verified pass uses it for every set of
+// the failed chunks at once
+bool k_mln_list_ok(const bls::PipeBufs& b);
+hipError_t launch_k_mln_list(const bls::PipeBufs& b, const uint32_t* items, uint32_t count, hipStream_t s);
 hipError_t launch_k_mls(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, hipStream_t s);
 size_t mlq_line_words(uint32_t count);
 hipError_t launch_k_mlqf(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, uint32_t* lines,
-                         hipStream_t s);
+                         hipStream_t s, const uint32_t* items = nullptr);
