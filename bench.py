@@ -143,15 +143,30 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
             ml1 = ml
         # the signature sums: one group sum over the pass and ONE signature Miller loop
         # (merged signature sum, $BLS_SIG_TOTAL), or one per chunk
-        if os.environ.get("BLS_SIG_TOTAL", "1") != "0" and chunks > 1:
+        total = os.environ.get("BLS_SIG_TOTAL", "1") != "0" and chunks > 1
+        msm = total and os.environ.get("BLS_MSM", "0") == "1" and "msm_madd" in wm
+        r_sig = wm["chain_r_sig"]
+        if msm:
+            # kernels/k_msm.hip: 8 (window, digit) entries per set, one mixed addition each
+            # (255 of 256 digits are non-zero), the mu image for the 4 b-half entries, a
+            # bucket addition per segment, and per pass 4 windows x (256 x 8 + 255)
+            # additions + 36 doublings + 3 additions
+            seg = 8
+            while seg * seg < (8 * n_sets + 1019) // 1020:
+                seg *= 2
+            fixed = (4 * (256 * 8 + 255) + 3) * wm["gsum_add"] + 36 * wm["g2_dbl"]
+            r_sig = 0.0
+            sums = (8 * 255 / 256 * wm["msm_madd"] + 4 * wm["msm_mu"] + 8 / seg * wm["gsum_add"] + fixed / n_sets
+                    + (m["ml1_1"] + wm["vset"]) / n_sets)
+        elif total:
             sums = (m["ml1_1"] + wm["vset"]) / n_sets + (n_sets - 1) / n_sets * wm["gsum_add"]
         else:
             sums = chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"]
-        per = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"] + ml
+        per = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + r_sig + wm["chain_r_pk"] + ml
                + sums + merged / n_sets)
-        return per, ("k_pre %.0f + k_chain %.0f + k_mln %.0f + signature sums/ML %.0f + merged check %.0f" %
-                     (wm["k_pre"], wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"], ml,
-                      sums, merged / n_sets))
+        return per, ("k_pre %.0f + k_chain %.0f + k_mln %.0f + signature sums%s %.0f + merged check %.0f" %
+                     (wm["k_pre"], wm["chain_h"] + wm["chain_subgroup"] + r_sig + wm["chain_r_pk"], ml,
+                      " (Pippenger MSM + one ML)" if msm else "/ML", sums, merged / n_sets))
     S = pack_of(n_sets)
     ps = pset_products_per_set(S)
     return wm["k_pre"] + ps + merged / n_sets, "k_pre %.0f + k_pset %.0f + merged check %.0f" % (
@@ -583,13 +598,15 @@ def main() -> None:
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--inflight", type=int, default=10, help="verifier contexts (HIP streams) per GPU")
-    # default 10 contexts x 8 calls: the knee of profiles/r02c_knee_final.json with the
-    # final kernels (8 x 8 2.0M at 33 ms per pass, 10 x 8 2.09M at 39 ms, 12 x 8 2.09M at
-    # 47 ms); a call's verdicts arrive when its pass ends, well inside the reference's
-    # 100 ms job buffering
-    # (multithread/index.ts:57 MAX_BUFFER_WAIT_MS)
-    ap.add_argument("--calls-per-pass", type=int, default=8,
+    ap.add_argument("--inflight", type=int, default=12, help="verifier contexts (HIP streams) per GPU")
+    # default 12 contexts x 16 calls (profiles/r03_knee.json): the rate follows the sets in
+    # flight up to ~3M sets/s (16 x 8 2.76M at 47 ms per pass, 12 x 16 2.94M at 67 ms,
+    # 16 x 16 3.03M at 87 ms); a call's verdicts arrive when its pass ends, inside the
+    # reference's 100 ms job buffering (multithread/index.ts:57 MAX_BUFFER_WAIT_MS).  12
+    # contexts keep the scratch the runtime reserves per hardware queue (k_chain: 464 MiB)
+    # well under the ~8 GiB at which it aborts queues (20 contexts did,
+    # profiles/r03_scratch_out_of_resources.txt)
+    ap.add_argument("--calls-per-pass", type=int, default=16,
                     help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "
                          "its own chunks and verdicts)")
     ap.add_argument("--mode", choices=("cfg2", "sharded", "napi", "cfg4", "cfg5"), default="cfg2")

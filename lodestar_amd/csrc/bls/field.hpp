@@ -531,7 +531,19 @@ BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_sqr_d28_lazy(a));
 __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_d28_lazy(a, b)); }
 __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_d28_lazy(a, b); }
 #endif
-BLS_FP_MUL_ATTR Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
+// The out-of-line product takes its operands as 24 scalar words: passed as two Fp
+// structs, the gfx950 calling convention hands the first one over by reference in
+// private memory (the caller stores 48 B per lane to scratch, the callee loads them back
+// at every product -- most of k_chain's ~380 KB of scratch traffic per set); scalars
+// travel in v0-v23 and the result returns in v0-v11.
+#define BLS_W12(x) uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, \
+                   uint32_t x##6, uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11
+#define BLS_FP_OF(x) Fp{{x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11}}
+#define BLS_L12(v) (v).l[0], (v).l[1], (v).l[2], (v).l[3], (v).l[4], (v).l[5], (v).l[6], (v).l[7], (v).l[8], \
+                   (v).l[9], (v).l[10], (v).l[11]
+BLS_FP_MUL_ATTR Fp fp_mul_w(BLS_W12(a), BLS_W12(b)) { return fp_mul_inl(BLS_FP_OF(a), BLS_FP_OF(b)); }
+BLS_FP_MUL_ATTR Fp fp_sqr_w(BLS_W12(a)) { return fp_sqr_dev(BLS_FP_OF(a)); }
+__device__ __forceinline__ Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_w(BLS_L12(a), BLS_L12(b)); }
 #else
 // Host build: Montgomery product a*b/R mod p (R = 2^384) over 6 x 64-bit words,
 // separated operand scanning (the 36 partial products of a*b first, then the word-by-
@@ -574,7 +586,7 @@ BLS_HD Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul(a, b); }
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
-BLS_HD Fp fp_sqr(const Fp& a) { return fp_sqr_dev(a); }
+BLS_HD Fp fp_sqr(const Fp& a) { return fp_sqr_w(BLS_L12(a)); }
 #else
 BLS_HD Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }
 #endif

@@ -475,6 +475,19 @@ static void dbg_sync(hipStream_t s, const char* what) {
   fflush(stderr);
 }
 
+// Pippenger merged signature sum (k_msm): off unless $BLS_MSM=1.  It removes k_chain role 2
+// (~1.6k Fp products per set) but its serial stages (segments, buckets, the windows' 16
+// dependent additions) lengthen the pass by ~3 ms, and with the calls in flight the pass
+// latency, not the work, sets the rate: 2.39M vs 2.79M sets/s at 16 x 8
+// (profiles/r03_ab_msm.json)
+static bool msm_on() {
+  static const bool on = [] {
+    const char* e = getenv("BLS_MSM");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // Shared Miller loops in k_mln (PipeBufs::ml_dom): on unless $BLS_ML_SHARED=0
 static bool ml_shared_on() {
   static const bool on = [] {
@@ -738,6 +751,10 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // pairs it once.  A failing merged check re-sums per chunk and pairs each sum before
   // the per-chunk final exponentiations (k_chunk_coop), so chunk verdicts are unchanged.
   const bool use_total = sigagg && merged && n_chunks > 1 && sig_total_on();
+  // ... and under it the sum is one Pippenger MSM over the live sets (kernels/k_msm.hip)
+  // instead of per-set [r] sig chains + k_gsum levels; the per-set RS are made (k_chain
+  // role 2 alone) only when the merged check fails and the chunks' own sums are needed
+  const bool use_msm = use_total && msm_on();
   GsumPlan total_gsum;
   if (use_total) {
     std::vector<uint32_t> goff(n_chunks + 1, (uint32_t)chunk_gsum.gsets.size());
@@ -797,6 +814,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   G2J* gtmp[2] = {nullptr, nullptr};
   uint32_t *unit_rep_dev = nullptr, *ugsets_dev = nullptr, *useg_dev = nullptr;  // Miller-loop units
   uint32_t* own_sets_dev = nullptr;      // the individually verified sets' own Miller loops (one launch)
+  MsmBufs msm;
+  memset(&msm, 0, sizeof(msm));
   G1J* utmp[2] = {nullptr, nullptr};
   auto carve = [&](Carver& c, PipeBufs& b, size_t& input_end) {
     b.req_off = c.take<uint32_t>(R + 1);
@@ -846,6 +865,16 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.flag_count = c.take<uint32_t>(1);
     b.f = c.take<Fp12>(n_total);
     b.ml_lines = sigagg ? c.take<uint32_t>(mlq_line_words(n_total)) : nullptr;
+    if (use_msm) {
+      msm.cnt = c.take<uint32_t>(MSM_BUCKETS);
+      msm.off = c.take<uint32_t>(MSM_BUCKETS + 1);
+      msm.seg_off = c.take<uint32_t>(MSM_BUCKETS + 1);
+      msm.ent = c.take<uint32_t>(8ull * n);
+      msm.sorted = c.take<uint32_t>(8ull * n);
+      msm.seg_sum = c.take<G2J>(msm_seg_cap(n));
+      msm.bucket = c.take<G2J>(MSM_BUCKETS);
+      msm.win = c.take<G2J>(4);
+    }
     b.req_status = c.take<int32_t>(R);
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
@@ -949,10 +978,14 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     if (sigagg) {
       // per-set chains, the chunks' sums of r sig -> virtual sets n + c, then every
       // Miller loop (sets and virtual sets) in one launch
-      HIPC(ctx, launch_k_chain(b, s)); dbg_sync(s, "k_chain");
-      if (launch_gsum(ctx, b, use_total ? total_gsum : chunk_gsum, use_total ? tseg_dev : gseg_dev, gsets_dev, gtmp,
-                      n, s))
+      HIPC(ctx, launch_k_chain(b, s, use_msm ? 0xBu : 0xFu)); dbg_sync(s, "k_chain");
+      if (use_msm) {
+        HIPC(ctx, launch_k_msm(b, msm, gtmp[0], n_chunks, s)); dbg_sync(s, "k_msm");
+        HIPC(ctx, launch_k_vset(b, gtmp[0], n_chunks, n, s)); dbg_sync(s, "k_vset");
+      } else if (launch_gsum(ctx, b, use_total ? total_gsum : chunk_gsum, use_total ? tseg_dev : gseg_dev, gsets_dev,
+                             gtmp, n, s)) {
         return -1;
+      }
       if (use_units) {
         // sum r_i pk_i per unit (levels over the members), then the units' chain entries
         b.gsets = ugsets_dev;
@@ -995,6 +1028,16 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   if (merged && launch_merged()) return -1;
   HIPC(ctx, hipEventRecord(ctx->ev[6], s));
 
+  // the per-set RS = [r] sig (chain CH_RS) the fallback sums need: made by the first pass
+  // unless the MSM replaced role 2 there
+  bool rs_done = !use_msm;
+  auto ensure_rs = [&]() -> int {
+    if (!rs_done) {
+      HIPC(ctx, launch_k_chain(b, s, 0x4u)); dbg_sync(s, "k_chain rs");
+      rs_done = true;
+    }
+    return 0;
+  };
   std::vector<int32_t> chunk_ok(n_chunks + 1, 0);
   std::vector<int32_t> merged_status(merged ? R : 0, 0);
   int32_t merged_verdict = 0;
@@ -1023,6 +1066,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     for (uint32_t ch = 0; ch < n_chunks; ++ch) chunk_ok[ch] = 1;
   } else if (n_chunks > 0 && !partial) {
     // some set is invalid or erroneous (or no merged check): the per-chunk verdicts decide
+    if (ensure_rs()) return -1;
     if (use_total) {
       // the chunks' own signature sums and their Miller loops (virtual sets n + c)
       if (launch_gsum(ctx, b, chunk_gsum, gseg_dev, gsets_dev, gtmp, n, s)) return -1;
@@ -1136,6 +1180,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       std::vector<uint32_t> goff(indiv.size() + 1);
       for (size_t t = 0; t <= indiv.size(); ++t) goff[t] = (uint32_t)t;
       plan_gsum(in, goff, indiv, indiv_gsum);
+      if (ensure_rs()) return -1;
       if (indiv_gsum.seg.size() > gseg_cap) {
         snprintf(ctx->err, sizeof(ctx->err), "group-sum plan exceeds its workspace");
         return -3;

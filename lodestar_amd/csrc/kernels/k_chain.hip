@@ -213,8 +213,16 @@ __device__ __noinline__ void chain_role_rp(const PipeBufs& b, uint32_t i) {
 #else
 #define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
-__global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, uint32_t blocks_per_role) {
-  const uint32_t role = blockIdx.x / blocks_per_role;
+__global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, uint32_t blocks_per_role,
+                                                                   uint32_t roles) {
+  // the (blockIdx / blocks_per_role)-th role present in the mask
+  uint32_t role = 0, nth = blockIdx.x / blocks_per_role;
+  for (uint32_t m = roles;; m &= m - 1) {
+    if (nth-- == 0) {
+      role = (uint32_t)__builtin_ctz(m);
+      break;
+    }
+  }
   const uint32_t i = (blockIdx.x % blocks_per_role) * BLS_BLOCK + threadIdx.x;
   if (i >= b.n_sets) return;
   // H(m) once per distinct signing root: only the root's first set
@@ -261,9 +269,11 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_chain_done(PipeBufs b) {
   b.chain_live[i] = 1u;
 }
 
-hipError_t launch_k_chain(const PipeBufs& b, hipStream_t s) {
+hipError_t launch_k_chain(const PipeBufs& b, hipStream_t s, uint32_t roles) {
   const uint32_t nb = bls_grid_for(b.n_sets);
-  k_chain<<<4 * nb, BLS_BLOCK, 0, s>>>(b, nb);
-  k_chain_done<<<nb, BLS_BLOCK, 0, s>>>(b);
+  roles &= 0xFu;
+  if (roles == 0) return hipSuccess;
+  k_chain<<<(uint32_t)__builtin_popcount(roles) * nb, BLS_BLOCK, 0, s>>>(b, nb, roles);
+  if (roles != 0x4u) k_chain_done<<<nb, BLS_BLOCK, 0, s>>>(b);
   return hipGetLastError();
 }

@@ -1,0 +1,217 @@
+// The merged signature sum S = sum_i [r_i] sig_i over a pass's live sets as a Pippenger
+// multi-scalar multiplication (bucket method), replacing k_chain role 2 ([r] sig per set,
+// ~1.6k Fp products) and the k_gsum levels in the merged-check path.
+//
+// Scalars: the set's batch scalar is r_i = a_i + b_i mu (curve.hpp glv_split / jac_mul_glv:
+// a, b the two 32-bit halves of set_scalar, mu = -x^2 with [mu]Q = -psi^2(Q) on G2), so
+//   S = sum_i [a_i] sig_i + [b_i] mu(sig_i):
+// 2 n affine points with 32-bit scalars, four 8-bit windows, 255 buckets per window.
+//
+//   k_msm_bin      one lane per set: its 8 (window, digit) entries, bucket slot by atomic count
+//   k_msm_scan     one workgroup: bucket offsets and level-0 segment offsets (prefix sums)
+//   k_msm_scatter  one lane per set: point references into bucket order
+//   k_msm_seg      one lane per segment of <= seg points of one bucket: mixed additions
+//   k_msm_bucket   one lane per bucket: the sum of its segments
+//   k_msm_window   one workgroup of 256 lanes per window: T_w = sum_d d B_{w,d} as the sum
+//                  of the suffix sums of the buckets (Hillis-Steele scan + tree in LDS,
+//                  16 dependent additions), then [2^(8w)] T_w
+//   k_msm_final    S = sum_w [2^(8w)] T_w into the pass's signature-sum slot (group 0;
+//                  the other chunk groups are infinity, so k_vset gives them f = 1)
+//
+// Work per pass of n sets: ~8 n mixed additions (29 Fp products each) + n/seg * ... + a
+// fixed ~4k additions for the windows -- ~300 Fp products per set against ~1.6k for the
+// per-set [r] sig chains.  The per-set RS are still produced (k_chain role 2 alone) when
+// the merged check fails and the chunks' own sums are needed (bls_gpu.hip ensure_rs).
+#define BLS_FP_D28 1
+#include "../launchers.hpp"
+
+using namespace bls;
+
+namespace {
+
+constexpr uint32_t MSM_W = 4, MSM_D = 255, MSM_NB = MSM_W * MSM_D;
+constexpr uint32_t ENT_NONE = 0xFFFFFFFFu;
+
+__device__ __noinline__ void msm_madd(G2J* acc, const G2A* p) { *acc = jac_add_aff(*acc, *p); }
+__device__ __noinline__ void msm_add(G2J* acc, const G2J* p) { *acc = jac_add(*acc, *p); }
+__device__ __noinline__ void msm_dbl(G2J* acc) { *acc = jac_dbl(*acc); }
+
+// point reference: set index, top bit = the mu image
+__device__ G2A msm_point(const PipeBufs& b, uint32_t ref) {
+  const G2A s = b.sig[ref & 0x7FFFFFFFu];
+  if (!(ref >> 31)) return s;
+  const G2J m = g2_mu(jac_from_aff(s));  // z stays 1: psi conjugates it
+  G2A r;
+  r.x = m.x;
+  r.y = m.y;
+  r.inf = false;
+  return r;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_msm_bin(PipeBufs b, MsmBufs m) {
+  const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (i >= b.n_sets) return;
+  uint32_t* ent = m.ent + 8ull * i;
+  if (!b.chain_live[i]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ent[j] = ENT_NONE;
+    return;
+  }
+  uint32_t sc[2];
+  glv_split(set_scalar(b.seed, b.scalar_base + i), sc[0], sc[1]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t w = (uint32_t)j >> 1, d = (sc[j & 1] >> (8 * w)) & 255u;
+    if (d == 0) {
+      ent[j] = ENT_NONE;
+      continue;
+    }
+    const uint32_t key = w * MSM_D + d - 1;
+    ent[j] = (key << 22) | atomicAdd(&m.cnt[key], 1u);
+  }
+}
+
+// one workgroup of 1024 lanes: off[k] = sum_{j<k} cnt[j]; seg_off likewise over
+// ceil(cnt / seg) segments per bucket
+__global__ __launch_bounds__(1024) void k_msm_scan(MsmBufs m, uint32_t seg) {
+  __shared__ uint32_t a[1024], c[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t cnt = t < MSM_NB ? m.cnt[t] : 0u;
+  a[t] = cnt;
+  c[t] = (cnt + seg - 1) / seg;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t x = t >= off ? a[t - off] : 0u, y = t >= off ? c[t - off] : 0u;
+    __syncthreads();
+    a[t] += x;
+    c[t] += y;
+    __syncthreads();
+  }
+  if (t < MSM_NB) {
+    m.off[t + 1] = a[t];
+    m.seg_off[t + 1] = c[t];
+  }
+  if (t == 0) {
+    m.off[0] = 0;
+    m.seg_off[0] = 0;
+  }
+}
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_msm_scatter(PipeBufs b, MsmBufs m) {
+  const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (i >= b.n_sets) return;
+  const uint32_t* ent = m.ent + 8ull * i;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t e = ent[j];
+    if (e == ENT_NONE) continue;
+    m.sorted[m.off[e >> 22] + (e & 0x3FFFFFu)] = i | ((uint32_t)(j & 1) << 31);
+  }
+}
+
+// lane s: segment s of the bucket whose [seg_off[k], seg_off[k + 1]) holds it
+__global__ __launch_bounds__(BLS_BLOCK) void k_msm_seg(PipeBufs b, MsmBufs m, uint32_t seg) {
+  const uint32_t s = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (s >= m.seg_off[MSM_NB]) return;
+  uint32_t lo = 0, hi = MSM_NB;  // largest k with seg_off[k] <= s
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (m.seg_off[mid] <= s) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t beg = m.off[lo] + (s - m.seg_off[lo]) * seg;
+  const uint32_t end = min(beg + seg, m.off[lo + 1]);
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t e = beg; e < end; ++e) {
+    const G2A p = msm_point(b, m.sorted[e]);
+    msm_madd(&acc, &p);
+  }
+  m.seg_sum[s] = acc;
+}
+
+__global__ __launch_bounds__(BLS_BLOCK) void k_msm_bucket(MsmBufs m) {
+  const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (k >= MSM_NB) return;
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t s = m.seg_off[k]; s < m.seg_off[k + 1]; ++s) {
+    const G2J p = m.seg_sum[s];
+    msm_add(&acc, &p);
+  }
+  m.bucket[k] = acc;
+}
+
+// workgroup w, lane d: v_d = B_{w,d} (v_0 = O); suffix sums S_d = sum_{k >= d} v_k, then
+// T_w = sum_{d >= 1} S_d = sum_d d B_{w,d}; lane 0 scales by 2^(8 w)
+__global__ __launch_bounds__(256) void k_msm_window(MsmBufs m) {
+  __shared__ G2J L[256];
+  const uint32_t w = blockIdx.x, d = threadIdx.x;
+  G2J x = d ? m.bucket[w * MSM_D + d - 1] : jac_infinity<Fp2>();
+  L[d] = x;
+  __syncthreads();
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    G2J y = d + off < 256 ? L[d + off] : jac_infinity<Fp2>();
+    __syncthreads();
+    msm_add(&x, &y);
+    L[d] = x;
+    __syncthreads();
+  }
+  if (d == 0) L[0] = jac_infinity<Fp2>();
+  __syncthreads();
+  for (uint32_t off = 128; off >= 1; off >>= 1) {
+    if (d < off) {
+      G2J y = L[d + off];
+      G2J z = L[d];
+      msm_add(&z, &y);
+      L[d] = z;
+    }
+    __syncthreads();
+  }
+  if (d == 0) {
+    G2J t = L[0];
+    for (uint32_t k = 0; k < 8 * w; ++k) msm_dbl(&t);
+    m.win[w] = t;
+  }
+}
+
+// out[0] = sum_w win[w]; out[1 .. groups) = O
+__global__ __launch_bounds__(BLS_BLOCK) void k_msm_final(MsmBufs m, G2J* out, uint32_t groups) {
+  const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (g >= groups) return;
+  if (g) {
+    out[g] = jac_infinity<Fp2>();
+    return;
+  }
+  G2J acc = m.win[0];
+  for (uint32_t w = 1; w < MSM_W; ++w) {
+    const G2J p = m.win[w];
+    msm_add(&acc, &p);
+  }
+  out[0] = acc;
+}
+
+uint32_t msm_seg_len(uint32_t n_sets) {
+  // ~sqrt(entries per bucket): the per-segment mixed additions and the per-bucket
+  // segment additions are about equally deep
+  const uint32_t per_bucket = (8u * n_sets + MSM_NB - 1) / MSM_NB;
+  uint32_t seg = 8;
+  while (seg * seg < per_bucket) seg *= 2;
+  return seg;
+}
+
+size_t msm_seg_cap(uint32_t n_sets) { return (8ull * n_sets) / msm_seg_len(n_sets) + MSM_NB + 1; }
+
+hipError_t launch_k_msm(const PipeBufs& b, const MsmBufs& m, G2J* out, uint32_t groups, hipStream_t s) {
+  const uint32_t n = b.n_sets, seg = msm_seg_len(n);
+  hipError_t e = hipMemsetAsync(m.cnt, 0, sizeof(uint32_t) * MSM_NB, s);
+  if (e != hipSuccess) return e;
+  k_msm_bin<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);
+  k_msm_scan<<<1, 1024, 0, s>>>(m, seg);
+  k_msm_scatter<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);
+  k_msm_seg<<<bls_grid_for((uint32_t)msm_seg_cap(n)), BLS_BLOCK, 0, s>>>(b, m, seg);
+  k_msm_bucket<<<bls_grid_for(MSM_NB), BLS_BLOCK, 0, s>>>(m);
+  k_msm_window<<<MSM_W, 256, 0, s>>>(m);
+  k_msm_final<<<bls_grid_for(groups), BLS_BLOCK, 0, s>>>(m, out, groups);
+  return hipGetLastError();
+}

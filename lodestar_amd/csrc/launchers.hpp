@@ -20,7 +20,23 @@ hipError_t launch_k_status(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk_len, int32_t* codes, hipStream_t s);
 hipError_t launch_k_pre(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_exact(const bls::PipeBufs& b, hipStream_t s);
-hipError_t launch_k_chain(const bls::PipeBufs& b, hipStream_t s);
+// roles: bit k runs k_chain role k (0 H, 1 subgroup, 2 [r] sig, 3 [r] pk); k_chain_done
+// follows unless only role 2 runs (the merged check's fallback needs the per-set RS)
+hipError_t launch_k_chain(const bls::PipeBufs& b, hipStream_t s, uint32_t roles = 0xFu);
+// Pippenger sum of [r_i] sig_i over the live sets (kernels/k_msm.hip)
+struct MsmBufs {
+  uint32_t* cnt;      // 1020 bucket counts
+  uint32_t* off;      // 1021 bucket offsets into sorted
+  uint32_t* seg_off;  // 1021 segment offsets
+  uint32_t* ent;      // 8 n_sets (bucket << 22 | slot) entries
+  uint32_t* sorted;   // 8 n_sets point references in bucket order
+  bls::G2J* seg_sum;  // msm_seg_cap(n_sets)
+  bls::G2J* bucket;   // 1020
+  bls::G2J* win;      // 4
+};
+#define MSM_BUCKETS 1020u
+size_t msm_seg_cap(uint32_t n_sets);
+hipError_t launch_k_msm(const bls::PipeBufs& b, const MsmBufs& m, bls::G2J* out, uint32_t groups, hipStream_t s);
 hipError_t launch_k_gsum(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const bls::G2J* in,
                          bls::G2J* out, hipStream_t s);
 hipError_t launch_k_vset(const bls::PipeBufs& b, const bls::G2J* sums, uint32_t n_groups, uint32_t vbase,

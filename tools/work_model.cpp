@@ -25,7 +25,8 @@ static unsigned long long tick() {
 
 int main() {
   const int N = 64;  // sets (messages, scalars) averaged over
-  double pre = 0, h = 0, c = 0, rs = 0, rp = 0, gadd = 0, vset = 0, ml = 0, f12m = 0, mlq = 0, mlf = 0;
+  double pre = 0, h = 0, c = 0, rs = 0, rp = 0, gadd = 0, vset = 0, ml = 0, f12m = 0, mlq = 0, mlf = 0, madd = 0, mu = 0,
+         dbl = 0;
   uint32_t seed[8] = {1, 2, 3, 4, 5, 6, 7, 8};
   G2J prev = jac_infinity<Fp2>();
   for (int k = 0; k < N; ++k) {
@@ -102,6 +103,14 @@ int main() {
     // k_gsum: one G2 addition per summed point; k_vset: one affine conversion per group
     prev = jac_add(prev, RS);
     gadd += tick();
+    // k_msm: one mixed addition per (window, digit) entry, the mu image of the b-half
+    // point, doublings of the window scaling
+    G2J acc2 = jac_add_aff(RS, sig);
+    madd += tick();
+    (void)g2_mu(jac_from_aff(sig));
+    mu += tick();
+    acc2 = jac_dbl(acc2);
+    dbl += tick();
     const Fp vi = fp_inv_gcd(fp_add(fp_sqr(RS.z.c0), fp_sqr(RS.z.c1)));
     const Fp2 vz = Fp2{fp_mul(RS.z.c0, vi), fp_neg(fp_mul(RS.z.c1, vi))};
     const Fp2 vz2 = fp2_sqr(vz);
@@ -111,7 +120,9 @@ int main() {
   }
   printf("{\"sets_averaged\": %d, \"k_pre\": %.1f, \"chain_h\": %.1f, \"chain_subgroup\": %.1f, "
          "\"chain_r_sig\": %.1f, \"chain_r_pk\": %.1f, \"gsum_add\": %.1f, \"vset\": %.1f, \"ml_simt\": %.1f, "
-         "\"fp12_mul\": %.1f, \"ml_lines\": %.1f, \"ml_f_pair\": %.1f}\n",
-         N, pre / N, h / N, c / N, rs / N, rp / N, gadd / N, vset / N, ml / N, f12m / N, mlq / N, mlf / N);
+         "\"fp12_mul\": %.1f, \"ml_lines\": %.1f, \"ml_f_pair\": %.1f, \"msm_madd\": %.1f, \"msm_mu\": %.1f, "
+         "\"g2_dbl\": %.1f}\n",
+         N, pre / N, h / N, c / N, rs / N, rp / N, gadd / N, vset / N, ml / N, f12m / N, mlq / N, mlf / N, madd / N,
+         mu / N, dbl / N);
   return 0;
 }
