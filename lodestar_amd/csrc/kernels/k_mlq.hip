@@ -143,8 +143,10 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
 template <int W>
 __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlf(
     PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, const uint32_t* L, uint32_t stride,
-    const uint32_t* items) {
-  const uint32_t k0 = 2u * (blockIdx.x * BLS_BLOCK + threadIdx.x), k1 = k0 + 1u;
+    const uint32_t* items, uint32_t per_lane) {
+  // per_lane = 2: a lane takes items k0, k0 + 1 (one f when they share a domain);
+  // 1: one item per lane (twice the lanes, no shared squarings: shorter, not less work)
+  const uint32_t k0 = per_lane * (blockIdx.x * BLS_BLOCK + threadIdx.x), k1 = per_lane == 2u ? k0 + 1u : count;
   if (k0 >= count) return;
   // items: an index list (the individually verified pass: own loops only, no sharing)
   const uint32_t i0 = items ? items[k0] : first + k0, i1 = items ? (k1 < count ? items[k1] : 0u) : first + k1;
@@ -172,9 +174,12 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
                          hipStream_t s, const uint32_t* items) {
   if (count == 0) return hipSuccess;
   const uint32_t stride = (count + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
+  // k_mlq at one wavefront per SIMD (256 VGPRs, no spills around the products) by default:
+  // +3 % at 12 x 16 over two (1,088 B of scratch per lane), profiles/r03_ab_mlq_mlf.json;
+  // $BLS_MLQ_WAVES=2 restores two
   static const int wq = [] {
     const char* e = getenv("BLS_MLQ_WAVES");
-    return e && atoi(e) == 1 ? 1 : 2;
+    return e && atoi(e) == 2 ? 2 : 1;
   }();
   static const int wf = [] {
     const char* e = getenv("BLS_MLF_WAVES");
@@ -183,8 +188,13 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   const uint32_t up = (own_only || items) ? 0u : 1u;
   if (wq == 1) k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
   else k_mlq<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
-  const uint32_t pairs = (count + 1) / 2;
-  if (wf == 2) k_mlf<2><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
-  else k_mlf<1><<<bls_grid_for(pairs), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
+  // $BLS_MLF_PER_LANE=1: one item per lane (pass latency against shared squarings)
+  static const uint32_t per_lane = [] {
+    const char* e = getenv("BLS_MLF_PER_LANE");
+    return e && atoi(e) == 1 ? 1u : 2u;
+  }();
+  const uint32_t lanes = (count + per_lane - 1) / per_lane;
+  if (wf == 2) k_mlf<2><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
+  else k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
   return hipGetLastError();
 }
