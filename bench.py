@@ -68,7 +68,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
     os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-STAGE_NAMES = ["h2d", "k_pk", "k_pre", "per_set", "k_exact", "-", "k_status+k_chunk", "k_indiv"]
+STAGE_NAMES = ["h2d", "k_pk", "k_pre", "k_chain", "sig_sums", "miller_loops", "k_status+k_chunk", "k_indiv"]
 X_ABS = 0xD201000000010000
 MADS_PER_FPM = 288   # 12x12 limb products + 12x12 reduction products per Montgomery product
 METRIC = "BLS signature sets verified/sec (1-8 GPUs) + p50 latency @128-set batch"
@@ -173,16 +173,32 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
         wm["k_pre"], ps, merged / n_sets)
 
 
-def pmc_summary(kernel_prefix: str):
-    """The newest committed SQ-counter summary for the kernel (profiles/r*_pmc_*.json,
-    rocprofv3 --pmc passes; tools/pmc_summary.py), or None."""
-    files = sorted((ROOT / "profiles").glob("r*_pmc_k_*.json"), key=lambda p: p.name)
-    for p in reversed(files):
-        d = json.loads(p.read_text())
-        for k, v in d.get("kernels", {}).items():
-            if k.startswith(kernel_prefix):
-                return {**v, "source": p.name}
-    return None
+PMC_FILE = "r03_pmc_pass32.json"   # the committed counter summary the bench line cites
+VERIFY_KERNELS = ("k_pk", "k_pre", "k_chain", "k_gsum", "k_vset", "k_mlq", "k_mlf", "k_msm", "k_status", "k_fprod",
+                  "k_chunk_coop", "k_indiv_coop", "k_fold", "k_exact", "k_uset", "k_gsum1", "k_mln")
+
+
+def committed_pmc():
+    """The SQ / HBM counters of one 32768-set pass (profiles/PMC_FILE: rocprofv3 --pmc
+    passes over bench.py --probe-only, tools/pmc_summary.py), per verify kernel -- copied
+    from the committed file, labelled as such; None if absent."""
+    p = ROOT / "profiles" / PMC_FILE
+    if not p.exists():
+        return None
+    d = json.loads(p.read_text())
+    out, total = {}, 0
+    for name, v in d.get("kernels", {}).items():
+        if not name.startswith(VERIFY_KERNELS):
+            continue
+        total += v.get("hbm_bytes_per_launch", 0)
+        wc = v.get("SQ_WAVE_CYCLES")
+        if name.startswith(("k_chain", "k_mlf", "k_mlq", "k_pre")) and wc:
+            out[name] = {"valu_issue_frac": round(v["SQ_ACTIVE_INST_VALU"] / wc, 3),
+                         "waves_per_simd": v.get("waves_per_simd"), "valu_busy": v.get("valu_busy"),
+                         "valu_insts_per_wave": round(v["SQ_INSTS_VALU"] / max(1.0, v["SQ_WAVES"])),
+                         "hbm_bytes_per_launch": v.get("hbm_bytes_per_launch")}
+    return {"source": f"profiles/{PMC_FILE} (copied, not measured by this run)", "kernels": out,
+            "hbm_bytes_per_pass": total, "note": next(iter(d.get("kernels", {}).values()), {}).get("note")}
 
 
 def interop_sk(i: int) -> bytes:
@@ -795,48 +811,71 @@ def main() -> None:
             v, _ = gpu.verify_packed(call128)
             lat.append((time.perf_counter() - t1) * 1e3)
             assert v[0] == 1
-        # roofline of the dominant kernel, the per-set cooperative kernel (VALU integer
-        # multiply-add bound).  achieved = the device-wide useful MAD rate of that kernel in
-        # the timed region: sets/s per GPU x its MADs per set (launches overlap across the
-        # in-flight streams, so wall time per launch = timed region / launches); the solo
-        # launch time of one call is reported beside it.
+        # Roofline (VALU integer multiply-add bound; unit = v_mad_u64_u32, peak measured by
+        # bls_gpu_mad_peak).  Algorithmic work = Fp Montgomery products x 288 MADs, per set
+        # and per kernel from work_model.json / coop_programs.json (work_per_set).
+        #   achieved / frac: the device-wide useful MAD rate over the timed region (every
+        #     kernel of the pass; the contexts' launches overlap, so this is the figure that
+        #     says how much of the chip the pipeline uses);
+        #   kernels: per dominant kernel, its algorithmic MADs per launch / its average launch
+        #     time from HIP events on its context's stream (stage_ms: in the timed region,
+        #     where ~contexts launches share the device, and in solo passes of the same
+        #     K calls with the device to itself).
         fpm_set, fpm_note = work_per_set(args.sets * K)  # one device pass: K calls
         mad_set = fpm_set * MADS_PER_FPM
-        agg = sigagg_of(args.sets)
-        solo = []
-        for _ in range(5):
-            _, st = gpu.verify_packed(batch)
-            solo.append(st.stage_ms[STAGE_NAMES.index("per_set")])
-        solo_ms = statistics.median(solo)
+        agg = sigagg_of(args.sets * K)
+        solo_st = []
+        for _ in range(3):
+            if K > 1:
+                _, st = gpu.verify_many(works[0][0])
+            else:
+                _, st = gpu.verify_packed(batch)
+            solo_st.append(np.array(st.stage_ms[:]))
+        solo_stage = np.median(np.array(solo_st), axis=0)
         peak_rate, _ = gpu.mad_peak()
         peak = peak_rate / 1e12
         per_gpu = value / world
         achieved = per_gpu * mad_set / 1e12
         if rank == 0:
-            small = os.environ.get("BLS_ML_SMALL_FRAME", "1") != "0"
-            share = "4" if os.environ.get("BLS_ML_SHARE") == "4" else "8"
-            kern = (f"k_mlns<{share}>" if small else "k_mln<4>") if agg else (f"k_psetn<{S}" if S > 1 else "k_pset")
-            pmc = pmc_summary(kern.rstrip(">") if agg else kern)
+            wm = json.loads((ROOT / "lodestar_amd" / "_native" / "work_model.json").read_text())
+            pass_sets = args.sets * K
+            kern = {}
+            if agg:
+                simt = int(os.environ.get("BLS_ML_SIMT", "2") or 2)
+                per_k = {"k_chain": wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_pk"]
+                         + (0.0 if os.environ.get("BLS_MSM", "0") == "1" else wm["chain_r_sig"]),
+                         "miller_loops": (wm["ml_lines"] + wm["ml_f_pair"]) if simt == 2 else
+                         (wm["ml_simt"] if simt == 1 else None)}
+                for name, fpm in per_k.items():
+                    if fpm is None:
+                        continue
+                    i = STAGE_NAMES.index(name)
+                    mads = pass_sets * fpm * MADS_PER_FPM
+                    t_timed, t_solo = float(stage_ms[i]), float(solo_stage[i])
+                    kern[name] = {
+                        "mad_per_launch": round(mads),
+                        "fp_products_per_set": round(fpm, 1),
+                        "launch_ms_timed": round(t_timed, 3), "launch_ms_solo": round(t_solo, 3),
+                        "achieved_timed": round(mads / (t_timed * 1e-3) / 1e12, 4) if t_timed > 0 else None,
+                        "achieved_solo": round(mads / (t_solo * 1e-3) / 1e12, 4) if t_solo > 0 else None,
+                        "frac_solo": round(mads / (t_solo * 1e-3) / 1e12 / peak, 4) if t_solo > 0 else None}
             roof = {"bound": "valu",
-                    "kernel": (f"every kernel of the call; dominant: {kern} (cooperative Miller loops) and k_chain "
-                               "(scalar chains, one lane per set)") if agg else kern,
+                    "kernel": ("every kernel of the pass; dominant: k_chain (per-set scalar chains) and the split "
+                               "SIMT Miller loops (k_mlq + k_mlf)") if agg else "k_pset",
                     "achieved": round(achieved, 4),
                     "peak": round(peak, 3), "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5),
                     "traffic": None,
                     "work": f"{fpm_set:.0f} Fp products/set ({fpm_note}) x {MADS_PER_FPM} MAD x "
-                            f"{per_gpu:.0f} sets/s per GPU (timed region; launch wall time = region / launches)",
-                    "solo_launch_ms": round(solo_ms, 3),
-                    "solo_achieved": round(args.sets * mad_set / (solo_ms * 1e-3) / 1e12, 4),
+                            f"{per_gpu:.0f} sets/s per GPU over the timed region",
+                    "kernels": kern,
                     "peak_note": "measured: bls_gpu_mad_peak, every CU at 8 waves/SIMD"}
+            pmc = committed_pmc()
             if pmc:
-                wc = pmc.get("SQ_WAVE_CYCLES")
-                roof["pmc"] = {"source": pmc["source"],
-                               "valu_issue_frac": round(pmc["SQ_ACTIVE_INST_VALU"] / wc, 3) if wc else None,
-                               "wait_frac": round(pmc["SQ_WAIT_ANY"] / wc, 3) if wc else None,
-                               "waves_per_simd": pmc.get("waves_per_simd"),
-                               "valu_insts_per_wave": round(pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"]),
-                               "note": pmc.get("note")}
-                roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+                roof["pmc"] = pmc
+                roof["traffic"] = pmc["hbm_bytes_per_pass"]
+                roof["traffic_note"] = ("HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md) summed over every "
+                                        "verify kernel of one pass of the committed counter run, NOT measured by this "
+                                        f"run: {pmc['source']}")
             out["p50_latency_ms_128"] = round(statistics.median(lat), 3)
             out["stage_ms"] = {k: round(float(x), 3) for k, x in zip(STAGE_NAMES, stage_ms)}
             out["roofline"] = roof

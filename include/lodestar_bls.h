@@ -66,7 +66,9 @@ typedef struct bls_stats {
   uint32_t n_individual;       /* requests verified on their own */
   uint32_t n_flagged;          /* sets finished by the exact single-lane path */
   double device_ms;            /* device time of the call (HIP events) */
-  double stage_ms[8];          /* per stage: h2d, pk, pre (SSWU + sig decode), per-set (k_pset, or k_chain .. k_mln), exact, -, status+chunk, individual */
+  double stage_ms[8];          /* per stage (HIP events on the context's stream): h2d, pk, pre (SSWU + sig decode),
+                                  k_chain (or k_pset), signature sums, Miller loops (k_mlq + k_mlf),
+                                  status + merged / chunk checks, individual */
   uint32_t n_unique_msgs;      /* distinct signing roots hashed to the curve (== n_sets without dedup) */
   uint32_t merged_check;       /* 0 not run, 1 passed (per-chunk checks skipped), 2 failed (chunks checked) */
   uint32_t n_ml_units;         /* Miller-loop units (chunk x shared signing root pairings), 0 = one per set */

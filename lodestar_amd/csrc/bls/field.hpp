@@ -283,19 +283,61 @@ BLS_HD void fp_to_d28(const Fp& a, uint32_t d[14]) {
   }
 }
 
+// t += a b (unsigned / signed 32 x 32 -> 64 multiply-add).  On the device each is one
+// ordered v_mad_{u,i}64_i32: left to the compiler, the products were reassociated into
+// trees held all at once (~230 VGPRs in fp2_mul_d28, which every caller must free)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BLS_D28_MAC(t, a, b)                                                        \
+  do {                                                                              \
+    uint64_t cc_;                                                                   \
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(t), "=&s"(cc_) : "v"(a), "v"(b)); \
+  } while (0)
+#define BLS_D28_MACS(t, a, b)                                                       \
+  do {                                                                              \
+    uint64_t cc_;                                                                   \
+    asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(t), "=&s"(cc_) : "v"(a), "v"(b)); \
+  } while (0)
+// c is computed before any later asm block (the second half's multiply-adds): without it
+// the compiler sank the first reduction below them, keeping both column sets live
+#define BLS_PIN_FP(c)                                                                                \
+  asm volatile("" ::"v"((c).l[0]), "v"((c).l[1]), "v"((c).l[2]), "v"((c).l[3]), "v"((c).l[4]),     \
+               "v"((c).l[5]), "v"((c).l[6]), "v"((c).l[7]), "v"((c).l[8]), "v"((c).l[9]), "v"((c).l[10]), \
+               "v"((c).l[11]))
+#define BLS_D28_MACK(t, a, k)                                                                        \
+  do {                                                                                               \
+    uint64_t cc_;                                                                                    \
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(t), "=&s"(cc_) : "v"(a), "s"(k));        \
+  } while (0)
+#else
+#define BLS_D28_MACK(t, a, k) ((t) += (uint64_t)(a) * (k))
+#define BLS_PIN_FP(c) ((void)0)
+#define BLS_D28_MAC(t, a, b) ((t) += (uint64_t)(a) * (b))
+#define BLS_D28_MACS(t, a, b) ((t) = (uint64_t)((int64_t)(t) + (int64_t)(int32_t)(a) * (int64_t)(int32_t)(b)))
+#endif
+
 // t: the 27 columns of a 14 x 14-digit product; returns t / 2^384 mod p (< 2p)
+// ORDERED: the m p multiply-adds as ordered asm (fp2_mul_d28, where the compiler otherwise
+// holds them as product trees); the lone products keep the compiler's schedule (ordered,
+// they measured ~10 % slower)
+template <bool ORDERED = false>
 BLS_HD Fp fp_redc_d28(uint64_t t[27]) {
 #pragma unroll
   for (int i = 0; i < 13; ++i) {
     const uint32_t m = ((uint32_t)t[i] * BLS_NP28) & BLS_D28_MASK;
 #pragma unroll
-    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)m * p28_digit(j);
+    for (int j = 0; j < 14; ++j) {
+      if (ORDERED) BLS_D28_MACK(t[i + j], m, p28_digit(j));
+      else t[i + j] += (uint64_t)m * p28_digit(j);
+    }
     t[i + 1] += t[i] >> 28;  // column i is now 0 mod 2^28
   }
   {
     const uint32_t m = ((uint32_t)t[13] * BLS_NP28) & 0xFFFFFu;  // the last 20 bits
 #pragma unroll
-    for (int j = 0; j < 14; ++j) t[13 + j] += (uint64_t)m * p28_digit(j);
+    for (int j = 0; j < 14; ++j) {
+      if (ORDERED) BLS_D28_MACK(t[13 + j], m, p28_digit(j));
+      else t[13 + j] += (uint64_t)m * p28_digit(j);
+    }
   }
   // result = t[13] / 2^20 + sum_{k >= 14} t[k] 2^(8 + 28 (k - 14)): normalise the
   // digits from bit 8 on, then pack them into 32-bit limbs
@@ -356,6 +398,110 @@ BLS_HD Fp fp_sqr_d28_lazy(const Fp& a) {
     for (int j = i + 1; j < 14; ++j) t[i + j] += (uint64_t)x2[i] * x[j];
   }
   return fp_redc_d28(t);
+}
+
+// Fp2 product with ONE Montgomery reduction per coefficient (lazy reduction), for
+// canonical inputs (< p):
+//   c0 = (a0 b0 - a1 b1) / R,  c1 = (a0 b1 + a1 b0) / R
+// as 27-column 28-bit-digit products (4 x 196 digit products, 2 reductions of 196 --
+// the same multiply-adds as three reduced products, without the third reduction, two
+// operand conversions, the Karatsuba additions and the final subtractions).  c0's
+// columns start from C2_COL, a multiple of p whose column k is at least the largest
+// column k of a1 b1 for canonical digits (digits 0..12 < 2^28, digit 13 <= p >> 364),
+// so every column stays >= 0 through the signed multiply-subtract of a1 b1 and the
+// unsigned reduction applies: c0 value < p^2 + 2^762 -> output < 1.21 p; c1 < 2 p^2 ->
+// < 1.42 p; one conditional subtraction each makes them canonical.  tests:
+// test_hostsim.py::test_fp2_mul_lazy (C2_COL generated and checked there).
+BLS_HD uint64_t c2_col(int k) {
+  const uint64_t t[27] = {
+      0x00ffffffe1cc48ddull, 0x01ffffffcec8d82dull, 0x02ffffffa9e42d7cull, 0x03ffffff8c5f88ffull, 0x04ffffff683c5c79ull,
+      0x05ffffff4a84a061ull, 0x06ffffff2f404920ull, 0x07ffffff0efefe3bull, 0x08fffffee90b358cull, 0x09fffffec66cc7e1ull,
+      0x0afffffea7af04abull, 0x0bfffffe892c9c2eull, 0x0cfffffe6149107bull, 0x0c0034009ffe581bull, 0x0b003400bffcbfe9ull,
+      0x0a003400dffcbfe8ull, 0x09003400fffcbfe7ull, 0x080034011ffcbfe6ull, 0x070034013ffcbfe5ull, 0x060034015ffcbfe4ull,
+      0x050034017ffcbfe3ull, 0x040034019ffcbfe2ull, 0x03003401bffcbfe1ull, 0x02003401dffcbfe0ull, 0x01003401fffcbfdfull,
+      0x000034021ffcbfdeull, 0x00000002a4374121ull};
+  return t[k];
+}
+
+// the device scheduler may not move instructions across (keeps the two halves of
+// fp2_mul_d28 apart: interleaved they held ~250 VGPRs, which every caller must free)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BLS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define BLS_SCHED_FENCE() ((void)0)
+#endif
+
+BLS_HD Fp2 fp2_mul_d28(const Fp& a0, const Fp& a1, const Fp& b0, const Fp& b1) {
+  uint32_t x0[14], x1[14], y0[14], y1[14];
+  fp_to_d28(a0, x0);
+  fp_to_d28(a1, x1);
+  fp_to_d28(b0, y0);
+  fp_to_d28(b1, y1);
+  uint64_t t[27];
+  int32_t ny1[14];  // -b1's digits: a1 b1 leaves the columns by signed multiply-adds
+#pragma unroll
+  for (int j = 0; j < 14; ++j) ny1[j] = -(int32_t)y1[j];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) t[k] = c2_col(k);
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      BLS_D28_MAC(t[i + j], x0[i], y0[j]);
+      BLS_D28_MACS(t[i + j], x1[i], ny1[j]);
+    }
+  const Fp c0 = fp_reduce_once(fp_redc_d28<true>(t));
+  BLS_PIN_FP(c0);
+  BLS_SCHED_FENCE();
+#pragma unroll
+  for (int k = 0; k < 27; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      BLS_D28_MAC(t[i + j], x0[i], y1[j]);
+      BLS_D28_MAC(t[i + j], x1[i], y0[j]);
+    }
+  return Fp2{c0, fp_reduce_once(fp_redc_d28<true>(t))};
+}
+
+// Fp2 square with one reduction per coefficient (canonical inputs): c0 = (a0^2 - a1^2)/R
+// from the two symmetric squares (105 digit products each) on the C2_COL offset (a1^2's
+// columns are bounded like a1 b1's), c1 = 2 a0 a1 / R from the doubled digits of a0
+// (< 2^29).  tests: test_hostsim.py::test_fp2_mul_lazy.
+BLS_HD Fp2 fp2_sqr_d28(const Fp& a0, const Fp& a1) {
+  uint32_t x0[14], x1[14];
+  fp_to_d28(a0, x0);
+  fp_to_d28(a1, x1);
+  uint64_t t[27];
+  int32_t n1[14], n2[14];  // -a1 and -2 a1 digits
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    n1[j] = -(int32_t)x1[j];
+    n2[j] = -(int32_t)(x1[j] << 1);
+  }
+#pragma unroll
+  for (int k = 0; k < 27; ++k) t[k] = c2_col(k);
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    BLS_D28_MAC(t[2 * i], x0[i], x0[i]);
+    BLS_D28_MACS(t[2 * i], x1[i], n1[i]);
+#pragma unroll
+    for (int j = i + 1; j < 14; ++j) {
+      BLS_D28_MAC(t[i + j], x0[i] << 1, x0[j]);
+      BLS_D28_MACS(t[i + j], x1[i], n2[j]);
+    }
+  }
+  const Fp c0 = fp_reduce_once(fp_redc_d28<true>(t));
+  BLS_PIN_FP(c0);
+  BLS_SCHED_FENCE();
+#pragma unroll
+  for (int k = 0; k < 27; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) BLS_D28_MAC(t[i + j], x0[i] << 1, x1[j]);
+  return Fp2{c0, fp_reduce_once(fp_redc_d28<true>(t))};
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -544,6 +690,16 @@ __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_
 BLS_FP_MUL_ATTR Fp fp_mul_w(BLS_W12(a), BLS_W12(b)) { return fp_mul_inl(BLS_FP_OF(a), BLS_FP_OF(b)); }
 BLS_FP_MUL_ATTR Fp fp_sqr_w(BLS_W12(a)) { return fp_sqr_dev(BLS_FP_OF(a)); }
 __device__ __forceinline__ Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_w(BLS_L12(a), BLS_L12(b)); }
+#if defined(BLS_FP_D28) && !defined(BLS_FP_MUL32) && defined(BLS_FP2_FUSED)
+// the lazy Fp2 product and square out of line (build variant fp2fused: 48 words, 32 in
+// v0-v31 and 16 on the stack; the callee spans ~210 VGPRs, which its callers then spill
+// around every call: 2.62M vs 3.12M sets/s at 12 x 16, profiles/r03_ab_fp2_lazy.json)
+BLS_FP_MUL_ATTR Fp2 fp2_mul_w(BLS_W12(a), BLS_W12(c), BLS_W12(b), BLS_W12(d)) {
+  return fp2_mul_d28(BLS_FP_OF(a), BLS_FP_OF(c), BLS_FP_OF(b), BLS_FP_OF(d));
+}
+#define BLS_FP2_MUL_FUSED 1
+BLS_FP_MUL_ATTR Fp2 fp2_sqr_w(BLS_W12(a), BLS_W12(c)) { return fp2_sqr_d28(BLS_FP_OF(a), BLS_FP_OF(c)); }
+#endif
 #else
 // Host build: Montgomery product a*b/R mod p (R = 2^384) over 6 x 64-bit words,
 // separated operand scanning (the 36 partial products of a*b first, then the word-by-
@@ -888,6 +1044,9 @@ BLS_HD Fp2 fp2_half(const Fp2& a) { return Fp2{fp_half(a.c0), fp_half(a.c1)}; }
 BLS_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& b) { return Fp2{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 
 BLS_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+#ifdef BLS_FP2_MUL_FUSED
+  return fp2_mul_w(BLS_L12(a.c0), BLS_L12(a.c1), BLS_L12(b.c0), BLS_L12(b.c1));
+#endif
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
   Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
@@ -895,6 +1054,9 @@ BLS_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
 }
 
 BLS_HD Fp2 fp2_sqr(const Fp2& a) {
+#ifdef BLS_FP2_MUL_FUSED
+  return fp2_sqr_w(BLS_L12(a.c0), BLS_L12(a.c1));
+#endif
   Fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
   Fp t1 = fp_mul(a.c0, a.c1);
   return Fp2{t0, fp_dbl(t1)};

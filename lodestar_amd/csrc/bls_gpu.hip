@@ -979,6 +979,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       // per-set chains, the chunks' sums of r sig -> virtual sets n + c, then every
       // Miller loop (sets and virtual sets) in one launch
       HIPC(ctx, launch_k_chain(b, s, use_msm ? 0xBu : 0xFu)); dbg_sync(s, "k_chain");
+      HIPC(ctx, hipEventRecord(ctx->ev[3], s));
       if (use_msm) {
         HIPC(ctx, launch_k_msm(b, msm, gtmp[0], n_chunks, s)); dbg_sync(s, "k_msm");
         HIPC(ctx, launch_k_vset(b, gtmp[0], n_chunks, n, s)); dbg_sync(s, "k_vset");
@@ -999,12 +1000,15 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
         HIPC(ctx, launch_k_uset(b, uin, unit_rep_dev, s)); dbg_sync(s, "k_uset");
         b.gsets = gsets_dev;
       }
+      HIPC(ctx, hipEventRecord(ctx->ev[4], s));
       HIPC(ctx, launch_k_mln(b, ctx->coop, 0, indiv_vbase, s)); dbg_sync(s, "k_mln");
     } else {
       HIPC(ctx, launch_k_pset(b, ctx->coop, s)); dbg_sync(s, "k_pset");
+      HIPC(ctx, hipEventRecord(ctx->ev[3], s));
+      HIPC(ctx, hipEventRecord(ctx->ev[4], s));
     }
-    HIPC(ctx, hipEventRecord(ctx->ev[3], s));
-    HIPC(ctx, hipEventRecord(ctx->ev[4], s));
+    // stage_ms[3] k_chain (or k_pset), [4] the signature sums (k_gsum / k_msm, units),
+    // [5] the Miller loops (k_mlq + k_mlf): the per-kernel launch times bench.py prices
     HIPC(ctx, hipEventRecord(ctx->ev[5], s));
   } else {
     for (int i = 1; i <= 5; ++i) HIPC(ctx, hipEventRecord(ctx->ev[i], s));

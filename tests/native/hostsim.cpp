@@ -143,6 +143,25 @@ int hs_fp_sqrt(const uint8_t* a, uint8_t* out) {
 }
 
 void hs_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp2(fp2_mul(rd_fp2(a), rd_fp2(b)), out); }
+// the device's lazy Fp2 product (field.hpp fp2_mul_d28) on raw limbs (Montgomery form in, out)
+void hs_fp2_mul_d28_raw(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  Fp a0, a1, b0, b1;
+  memcpy(a0.l, a, 48);
+  memcpy(a1.l, a + 48, 48);
+  memcpy(b0.l, b, 48);
+  memcpy(b1.l, b + 48, 48);
+  const Fp2 r = fp2_mul_d28(a0, a1, b0, b1);
+  memcpy(out, r.c0.l, 48);
+  memcpy(out + 48, r.c1.l, 48);
+}
+void hs_fp2_sqr_d28_raw(const uint8_t* a, uint8_t* out) {
+  Fp a0, a1;
+  memcpy(a0.l, a, 48);
+  memcpy(a1.l, a + 48, 48);
+  const Fp2 r = fp2_sqr_d28(a0, a1);
+  memcpy(out, r.c0.l, 48);
+  memcpy(out + 48, r.c1.l, 48);
+}
 void hs_fp2_sqr(const uint8_t* a, uint8_t* out) { wr_fp2(fp2_sqr(rd_fp2(a)), out); }
 void hs_fp2_inv(const uint8_t* a, uint8_t* out) { wr_fp2(fp2_inv(rd_fp2(a)), out); }
 int hs_fp2_sqrt(const uint8_t* a, uint8_t* out) {

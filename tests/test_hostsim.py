@@ -48,6 +48,40 @@ def test_fp_mul_d28_lazy(hostsim):
             assert r % P == (a * (a if sqr else b) * rinv) % P
 
 
+def test_fp2_mul_lazy(hostsim):
+    """The device Fp2 product with one reduction per coefficient (field.hpp fp2_mul_d28):
+    canonical inputs -> canonical (a0 b0 - a1 b1) / R, (a0 b1 + a1 b0) / R, including the
+    extremes, and its column offset C2_COL regenerated here: a multiple of p whose every
+    column dominates the largest column of a1 b1 for canonical digits."""
+    rinv = pow(2, -384, P)
+    D = [(1 << 28) - 1] * 13 + [(P - 1) >> 364]
+    maxcol = [sum(D[i] * D[k - i] for i in range(14) if 0 <= k - i < 14) for k in range(27)]
+    delta = (-sum(c << (28 * k) for k, c in enumerate(maxcol))) % P
+    cols = [c + (((delta >> (28 * k)) & ((1 << 28) - 1)) if k < 14 else 0) for k, c in enumerate(maxcol)]
+    assert sum(c << (28 * k) for k, c in enumerate(cols)) % P == 0 and max(cols) < 2 ** 61
+    src = (__import__("pathlib").Path(__file__).resolve().parent.parent / "lodestar_amd" / "csrc" / "bls" /
+           "field.hpp").read_text()
+    assert all(("0x%016xull" % c) in src for c in cols)
+    rng = random.Random(2)
+    o = _buf(96)
+    edge = [0, 1, P - 1, P - 2, (P - 1) >> 1, 2 ** 380, P - 2 ** 364]
+    vals = edge + [rng.randrange(P) for _ in range(200)]
+    for k in range(len(vals)):
+        a0, a1 = vals[k], vals[(k * 5 + 1) % len(vals)]
+        b0, b1 = vals[(k * 11 + 2) % len(vals)], vals[(k * 3 + 4) % len(vals)]
+        le = [v.to_bytes(48, "little") for v in (a0, a1, b0, b1)]
+        hostsim.hs_fp2_mul_d28_raw(le[0] + le[1], le[2] + le[3], o)
+        c0, c1 = int.from_bytes(o.raw[:48], "little"), int.from_bytes(o.raw[48:], "little")
+        assert c0 < P and c1 < P
+        assert c0 == (a0 * b0 - a1 * b1) * rinv % P
+        assert c1 == (a0 * b1 + a1 * b0) * rinv % P
+        hostsim.hs_fp2_sqr_d28_raw(le[0] + le[1], o)
+        c0, c1 = int.from_bytes(o.raw[:48], "little"), int.from_bytes(o.raw[48:], "little")
+        assert c0 < P and c1 < P
+        assert c0 == (a0 * a0 - a1 * a1) * rinv % P
+        assert c1 == 2 * a0 * a1 * rinv % P
+
+
 def test_fp_inv_gcd(hostsim):
     rng = random.Random(7)
     o = _buf(48)
