@@ -319,6 +319,8 @@ BLS_HD void fp_to_d28(const Fp& a, uint32_t d[14]) {
 // ORDERED: the m p multiply-adds as ordered asm (fp2_mul_d28, where the compiler otherwise
 // holds them as product trees); the lone products keep the compiler's schedule (ordered,
 // they measured ~10 % slower)
+BLS_HD Fp fp_d28_tail(uint64_t t[27]);
+
 template <bool ORDERED = false>
 BLS_HD Fp fp_redc_d28(uint64_t t[27]) {
 #pragma unroll
@@ -339,8 +341,13 @@ BLS_HD Fp fp_redc_d28(uint64_t t[27]) {
       else t[13 + j] += (uint64_t)m * p28_digit(j);
     }
   }
-  // result = t[13] / 2^20 + sum_{k >= 14} t[k] 2^(8 + 28 (k - 14)): normalise the
-  // digits from bit 8 on, then pack them into 32-bit limbs
+  return fp_d28_tail(t);
+}
+
+// result = t[13] / 2^20 + sum_{k >= 14} t[k] 2^(8 + 28 (k - 14)) once columns 0..12 are
+// 0 mod 2^28 and column 13 is 0 mod 2^20: normalise the digits from bit 8 on, then
+// pack them into 32-bit limbs
+BLS_HD Fp fp_d28_tail(uint64_t t[27]) {
   const uint64_t u = t[13] >> 20;
   t[14] += u >> 8;
 #pragma unroll
@@ -380,6 +387,112 @@ BLS_HD Fp fp_mul_d28_lazy(const Fp& a, const Fp& b) {
 #pragma unroll
     for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)x[i] * y[j];
   return fp_redc_d28(t);
+}
+
+// The same product in product-scanning (FIPS) order with the reduction interleaved:
+// column k takes its a b and m p terms, and the column's m_k (k < 14) from its low
+// digit, so only the digits of a, b, m and one 64-bit column are live (~50 VGPRs
+// instead of ~130 for 27 columns at once).  Out of line, the product's register
+// footprint is what its callers must keep clear around every call (the compiler's
+// interprocedural register allocation): k_chain's G2 chains spill around the calls.
+// Result: (t + m p) / 2^384 with R = 2^(13*28 + 20): column 13's carry starts at result
+// bit 0 (after its low 20 bits), column k >= 14 at bit 8 + 28 (k - 14).  Inputs < 3p,
+// output < 2p.  tests: test_hostsim.py::test_fp_mul_fips.
+template <bool SQR>
+BLS_HD Fp fp_mul_fips(const Fp& a, const Fp& b) {
+  uint32_t x[14], y[14], m[14];
+  fp_to_d28(a, x);
+  if (SQR) {
+#pragma unroll
+    for (int k = 0; k < 14; ++k) y[k] = x[k];
+  } else {
+    fp_to_d28(b, y);
+  }
+  // per column: the a b terms and the m p terms of digits already known are summed
+  // off the critical path (two independent chains), then the carry in, m_{k-1} p_1 and
+  // m_k p_0 -- only those three are serial between columns
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = 0; i <= k; ++i) {
+      if (i & 1) s1 += (uint64_t)x[i] * y[k - i];
+      else s0 += (uint64_t)x[i] * y[k - i];
+    }
+#pragma unroll
+    for (int i = 0; i + 1 < k; ++i) {
+      if (i & 1) s1 += (uint64_t)m[i] * p28_digit(k - i);
+      else s0 += (uint64_t)m[i] * p28_digit(k - i);
+    }
+    acc += s0 + s1;
+    if (k > 0) acc += (uint64_t)m[k - 1] * p28_digit(1);
+    const uint32_t mask = k < 13 ? BLS_D28_MASK : 0xFFFFFu;
+    m[k] = ((uint32_t)acc * BLS_NP28) & mask;
+    acc += (uint64_t)m[k] * p28_digit(0);
+    if (k < 13) acc >>= 28;  // column k is 0 mod 2^28
+  }
+  // column 13 is 0 mod 2^20: the result starts at its bit 20
+  acc >>= 20;
+  const uint32_t low8 = (uint32_t)acc & 0xFFu;
+  acc >>= 8;  // now in units of 2^8, the weight of column 14
+  uint32_t e[14];
+#pragma unroll
+  for (int k = 14; k < 27; ++k) {
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = k - 13; i < 14; ++i) {
+      s0 += (uint64_t)x[i] * y[k - i];
+      s1 += (uint64_t)m[i] * p28_digit(k - i);
+    }
+    acc += s0 + s1;
+    e[k - 14] = (uint32_t)acc & BLS_D28_MASK;
+    acc >>= 28;
+  }
+  e[13] = (uint32_t)acc;  // < 2^(383 - 8 - 364) bits
+  // pack low8 + sum e_j 2^(8 + 28 j) into 12 x 32-bit limbs
+  Fp r;
+  uint64_t w = low8;
+  int nb = 8, li = 0;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    w |= (uint64_t)e[j] << nb;
+    nb += 28;
+    while (nb >= 32 && li < 12) {
+      r.l[li++] = (uint32_t)w;
+      w >>= 32;
+      nb -= 32;
+    }
+  }
+  while (li < 12) {
+    r.l[li++] = (uint32_t)w;
+    w >>= 32;
+  }
+  return r;
+}
+
+// The same product with the reduction interleaved row by row (CIOS): row i adds x_i y
+// into columns i..i+13, then m_i p, and carries column i into i+1 -- only ~15 columns
+// are live at once (~70 VGPRs instead of ~130), and each row's 14 multiply-adds are
+// independent (the column product's ILP).  Same output as fp_mul_d28_lazy.
+// tests: test_hostsim.py::test_fp_mul_fips.
+BLS_HD Fp fp_mul_cios(const Fp& a, const Fp& b) {
+  uint32_t x[14], y[14];
+  fp_to_d28(a, x);
+  fp_to_d28(b, y);
+  uint64_t t[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)x[i] * y[j];
+    const uint32_t m = ((uint32_t)t[i] * BLS_NP28) & (i < 13 ? BLS_D28_MASK : 0xFFFFFu);
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)m * p28_digit(j);
+    if (i < 13) t[i + 1] += t[i] >> 28;  // column i is now 0 mod 2^28
+  }
+  return fp_d28_tail(t);
 }
 
 // squaring: 14 squares + 91 cross products against doubled digits (< 2^29)
@@ -672,6 +785,14 @@ __device__ __forceinline__ Fp fp_sqr_cols(const Fp& a) {
 BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_sqr_cols(a); }
 __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul_cols<false>(a, b); }
 __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cols<true>(a, b); }
+#elif defined(BLS_FP_FIPS)
+BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_mul_fips<true>(a, a)); }
+__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_fips<false>(a, b)); }
+__device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_fips<false>(a, b); }
+#elif defined(BLS_FP_CIOS)
+BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_mul_cios(a, a)); }
+__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_cios(a, b)); }
+__device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cios(a, b); }
 #else
 BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_sqr_d28_lazy(a)); }
 __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_d28_lazy(a, b)); }
