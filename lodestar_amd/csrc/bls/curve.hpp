@@ -87,20 +87,22 @@ BLS_HD Jac<F> jac_neg(const Jac<F>& p) {
   return r;
 }
 
-// dbl-2009-l (a = 0)
+// dbl-2009-l (a = 0).  The order keeps few values live across the out-of-line products
+// (each product's callers must hold their live state outside its registers): Z3 first,
+// so Y and Z die at once; C8 as soon as C is known.
 template <class F>
 BLS_HD Jac<F> jac_dbl(const Jac<F>& p) {
-  F A = f_sqr(p.x);
-  F B = f_sqr(p.y);
-  F C = f_sqr(B);
-  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
-  F E = f_add(f_dbl(A), A);
-  F Fv = f_sqr(E);
   Jac<F> r;
-  r.x = f_sub(Fv, f_dbl(D));
-  F C8 = f_dbl(f_dbl(f_dbl(C)));
-  r.y = f_sub(f_mul(E, f_sub(D, r.x)), C8);
+  F B = f_sqr(p.y);
   r.z = f_dbl(f_mul(p.y, p.z));
+  F A = f_sqr(p.x);
+  F D = f_sqr(f_add(p.x, B));
+  F C = f_sqr(B);
+  D = f_dbl(f_sub(f_sub(D, A), C));
+  const F C8 = f_dbl(f_dbl(f_dbl(C)));
+  const F E = f_add(f_dbl(A), A);
+  r.x = f_sub(f_sqr(E), f_dbl(D));
+  r.y = f_sub(f_mul(E, f_sub(D, r.x)), C8);
   return r;
 }
 
@@ -109,26 +111,29 @@ template <class F>
 BLS_HD Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
-  F Z1Z1 = f_sqr(p.z);
-  F Z2Z2 = f_sqr(q.z);
-  F U1 = f_mul(p.x, Z2Z2);
-  F U2 = f_mul(q.x, Z1Z1);
-  F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
-  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
-  F H = f_sub(U2, U1);
+  // ordered so the inputs die early (see jac_dbl): (Z1 + Z2)^2 - Z1Z1 - Z2Z2 right
+  // after the Z's last other use
+  const F Z1Z1 = f_sqr(p.z);
+  const F Z2Z2 = f_sqr(q.z);
+  const F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
+  const F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  const F Zs = f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2);
+  const F U1 = f_mul(p.x, Z2Z2);
+  const F H = f_sub(f_mul(q.x, Z1Z1), U1);
   F rr = f_sub(S2, S1);
   if (f_is_zero(H)) {
     if (f_is_zero(rr)) return jac_dbl(p);
     return jac_infinity<F>();
   }
   rr = f_dbl(rr);
-  F I = f_sqr(f_dbl(H));
-  F J = f_mul(H, I);
-  F V = f_mul(U1, I);
   Jac<F> r;
+  r.z = f_mul(Zs, H);
+  const F I = f_sqr(f_dbl(H));
+  const F J = f_mul(H, I);
+  const F V = f_mul(U1, I);
+  const F S1J2 = f_dbl(f_mul(S1, J));
   r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
-  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(S1, J)));
-  r.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), S1J2);
   return r;
 }
 
@@ -137,24 +142,23 @@ template <class F>
 BLS_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   if (q.inf) return p;
   if (jac_is_inf(p)) return jac_from_aff(q);
-  F Z1Z1 = f_sqr(p.z);
-  F U2 = f_mul(q.x, Z1Z1);
-  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
-  F H = f_sub(U2, p.x);
-  F rr = f_sub(S2, p.y);
+  const F Z1Z1 = f_sqr(p.z);
+  const F H = f_sub(f_mul(q.x, Z1Z1), p.x);
+  F rr = f_sub(f_mul(f_mul(q.y, p.z), Z1Z1), p.y);
   if (f_is_zero(H)) {
     if (f_is_zero(rr)) return jac_dbl(p);
     return jac_infinity<F>();
   }
-  F HH = f_sqr(H);
-  F I = f_dbl(f_dbl(HH));
-  F J = f_mul(H, I);
-  rr = f_dbl(rr);
-  F V = f_mul(p.x, I);
   Jac<F> r;
+  const F HH = f_sqr(H);
+  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);  // Z1 and Z1Z1 die here
+  const F I = f_dbl(f_dbl(HH));
+  const F J = f_mul(H, I);
+  const F YJ2 = f_dbl(f_mul(p.y, J));
+  rr = f_dbl(rr);
+  const F V = f_mul(p.x, I);
   r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
-  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
-  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), YJ2);
   return r;
 }
 

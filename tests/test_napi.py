@@ -93,3 +93,28 @@ v.close();
     assert out.returncode == 0, out.stderr
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r == {"domain": g["domain"], "root": g["signing_root"]}
+
+
+@pytest.mark.gpu
+def test_js_main_thread_lane_not_behind_pool(gpu, tmp_path):
+    """verifyOnMainThread (multithread/index.ts:138-151) while a 4096-set pool call is in
+    flight: the adapter runs it on its own high-priority context, so it resolves before
+    the pool call does, in a fraction of the pool call's time."""
+    from lodestar_amd import workloads as W
+
+    n, keys = 4096, 1024
+    sks = W.interop_sks(keys)
+    pks48 = gpu.sk_to_pk(b"".join(s.to_bytes(32, "big") for s in sks)).tobytes()
+    msgs = [W.message(j, b"MAIN") for j in range(n)]
+    sigs = gpu.sign(b"".join(sks[j % keys].to_bytes(32, "big") for j in range(n)), b"".join(msgs))
+    f = tmp_path / "work.json"
+    f.write_text(json.dumps({"pubkeys48": pks48.hex(), "sets": [
+        {"idx": j % keys, "msg": msgs[j].hex(), "sig": sigs[j].tobytes().hex()} for j in range(n)]}))
+    out = subprocess.run([NODE, str(ROOT / "integration" / "js" / "mainLaneTest.js"), str(f)], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    for run in r["runs"]:
+        assert run["main_ok"] is True and run["pool_ok"] is True
+        assert run["main_before_pool"], run
+        assert run["main_ms"] < 0.7 * run["pool_ms"], run
