@@ -38,6 +38,19 @@ def oracle():
 
 
 @pytest.fixture(scope="session")
+def coop_programs():
+    """Every cooperative program (tools/gen_coop.py build_all), generated once per session
+    for the simulators of test_circuits.py and test_pset.py (~3 min)."""
+    root = Path(__file__).resolve().parent.parent / "tools"
+    if str(root) not in sys.path:
+        sys.path.insert(0, str(root))
+    import gen_coop
+
+    progs, consts = gen_coop.build_all()
+    return {p.name: p for p in progs}, consts
+
+
+@pytest.fixture(scope="session")
 def hostsim():
     from lodestar_amd.build import build_hostsim
     from lodestar_amd._abi import BlsBatch, BlsStats

@@ -14,9 +14,8 @@ from circuits import P, simulate  # noqa: E402
 
 
 @pytest.fixture(scope="module")
-def progs():
-    progs, consts = GC.build_all()
-    return {p.name: p for p in progs}, consts
+def progs(coop_programs):
+    return coop_programs
 
 
 def put12(frame, base, f):

@@ -16,9 +16,8 @@ from circuits import P, simulate  # noqa: E402
 
 
 @pytest.fixture(scope="module")
-def progs():
-    progs, consts = GC.build_all()
-    return {p.name: p for p in progs}, consts
+def progs(coop_programs):
+    return coop_programs
 
 
 def _frame_for(oracle, msg, sig_pt, pk_pt, zpk):
