@@ -81,9 +81,9 @@ __device__ __forceinline__ Fp12 mul_line12(const Fp12& f, const Fp2& l0, const F
   return Fp12{fp6_add(aa, fp6_mul_v(bb)), c1};
 }
 
-// prod over the lanes' G items (kk[0..G)) of their line products, one squaring per bit
-template <int G>
-__device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, const uint32_t* kk) {
+// prod over n consecutive items k0 .. k0 + n - 1 of their line products, one squaring of f
+// per bit (n at run time: one copy of the line product, whatever the sharing)
+__device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, uint32_t k0, uint32_t n) {
   Fp12 f = fp12_one();
   int e = 0;
   const uint64_t X = BLS_X_ABS;
@@ -91,10 +91,10 @@ __device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, const u
     if (bit != 62) f = sqr12(f);
     const int adds = (int)((X >> bit) & 1ull);
     for (int a = 0; a <= adds; ++a) {
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
+#pragma unroll 1
+      for (uint32_t g = 0; g < n; ++g) {
         Fp2 l0, l2, l3;
-        load_line(L, stride, kk[g], e, l0, l2, l3);
+        load_line(L, stride, k0 + g, e, l0, l2, l3);
         f = mul_line12(f, l0, l2, l3);
       }
       ++e;
@@ -144,24 +144,30 @@ template <int W>
 __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlf(
     PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, const uint32_t* L, uint32_t stride,
     const uint32_t* items, uint32_t per_lane) {
-  // per_lane = 2: a lane takes items k0, k0 + 1 (one f when they share a domain);
-  // 1: one item per lane (twice the lanes, no shared squarings: shorter, not less work)
-  const uint32_t k0 = per_lane * (blockIdx.x * BLS_BLOCK + threadIdx.x), k1 = per_lane == 2u ? k0 + 1u : count;
+  // per_lane items k0 .. k0 + per_lane - 1 per lane: when all are live and of one product
+  // domain they share one f (one squaring per bit for all of them), else each runs its
+  // own; items (an index list, the individually verified pass) never share
+  const uint32_t k0 = per_lane * (blockIdx.x * BLS_BLOCK + threadIdx.x);
   if (k0 >= count) return;
-  // items: an index list (the individually verified pass: own loops only, no sharing)
-  const uint32_t i0 = items ? items[k0] : first + k0, i1 = items ? (k1 < count ? items[k1] : 0u) : first + k1;
-  const bool live0 = ml_live(b, i0, units_paired), live1 = k1 < count && ml_live(b, i1, units_paired);
+  const uint32_t n = min(per_lane, count - k0);
+  const uint32_t i0 = items ? items[k0] : first + k0;
   // ml_dom covers the first-pass items [0, indiv_vbase) only: the individually verified
   // requests' signature sums after it never share (reading past it paired two requests'
   // sums into one f -- the verdict bug test_verify_many_merged_signature_sum_fails found)
-  if (live0 && live1 && units_paired && b.ml_dom && i1 < b.indiv_vbase && b.ml_dom[i0] == b.ml_dom[i1]) {
-    const uint32_t kk[2] = {k0, k1};
-    b.f[i0] = ml_f<2>(L, stride, kk);
-    b.f[i1] = fp12_one();
+  bool share = n > 1 && units_paired && b.ml_dom && !items && ml_live(b, i0, units_paired);
+  for (uint32_t g = 1; share && g < n; ++g) {
+    const uint32_t i = first + k0 + g;
+    share = ml_live(b, i, units_paired) && i < b.indiv_vbase && b.ml_dom[i] == b.ml_dom[i0];
+  }
+  if (share) {
+    b.f[i0] = ml_f(L, stride, k0, n);
+    for (uint32_t g = 1; g < n; ++g) b.f[first + k0 + g] = fp12_one();
     return;
   }
-  if (live0) b.f[i0] = ml_f<1>(L, stride, &k0);
-  if (live1) b.f[i1] = ml_f<1>(L, stride, &k1);
+  for (uint32_t g = 0; g < n; ++g) {
+    const uint32_t i = items ? items[k0 + g] : first + k0 + g;
+    if (ml_live(b, i, units_paired)) b.f[i] = ml_f(L, stride, k0 + g, 1);
+  }
 }
 
 // line buffer words for a launch of `count` items (stride padded to a wavefront)
@@ -188,10 +194,12 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   const uint32_t up = (own_only || items) ? 0u : 1u;
   if (wq == 1) k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
   else k_mlq<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
-  // $BLS_MLF_PER_LANE=1: one item per lane (pass latency against shared squarings)
+  // $BLS_MLF_PER_LANE = 1, 2 (default) or 4 items per lane: shorter f chains against
+  // squarings shared by more pairs
   static const uint32_t per_lane = [] {
     const char* e = getenv("BLS_MLF_PER_LANE");
-    return e && atoi(e) == 1 ? 1u : 2u;
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4) ? (uint32_t)v : 2u;
   }();
   const uint32_t lanes = (count + per_lane - 1) / per_lane;
   if (wf == 2) k_mlf<2><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
