@@ -27,6 +27,7 @@
 #include <stdlib.h>
 #include <zlib.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -298,6 +299,11 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
+// sets of the verify calls running now, over every context of the process (the Miller
+// loops pick their shape by it: kernels/k_mlq.hip launch_k_mlqf)
+static std::atomic<uint64_t> g_sets_in_flight{0};
+uint64_t bls_sets_in_flight() { return g_sets_in_flight.load(std::memory_order_relaxed); }
+
 extern "C" {
 
 int bls_gpu_device_count(void) {
@@ -701,6 +707,12 @@ static int check_batch(bls_gpu_ctx* ctx, const bls_batch* in, const char* what) 
   return 0;
 }
 
+struct InFlight {
+  uint64_t n;
+  explicit InFlight(uint64_t k) : n(k) { g_sets_in_flight.fetch_add(n, std::memory_order_relaxed); }
+  ~InFlight() { g_sets_in_flight.fetch_sub(n, std::memory_order_relaxed); }
+};
+
 static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats,
                        uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status,
                        uint32_t* partial_err = nullptr, const std::vector<uint32_t>* req_bounds = nullptr) {
@@ -711,6 +723,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   if (stats) memset(stats, 0, sizeof(*stats));
   if (R == 0) return 0;
   if (const int rc = check_batch(ctx, in, "batch")) return rc;
+  const InFlight in_flight(n);
   BatchPlan plan;
   if (req_bounds) plan_batch_msgs(in, *req_bounds, plan);
   else plan_batch(in, plan);

@@ -194,13 +194,23 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   const uint32_t up = (own_only || items) ? 0u : 1u;
   if (wq == 1) k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
   else k_mlq<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
-  // $BLS_MLF_PER_LANE = 1, 2 (default) or 4 items per lane: shorter f chains against
-  // squarings shared by more pairs
-  static const uint32_t per_lane = [] {
+  // Items per k_mlf lane: 2 shares f's squarings between two pairs (fewer instructions:
+  // the rate when the device is VALU-bound), 1 halves the f chain (the rate when few sets
+  // are in flight and the pass latency sets it): 2.22M vs 2.00M sets/s with 64k sets in
+  // flight, 2.76M vs 2.90M with 128k (profiles/r03_ab_mlq_mlf.json).  By default the
+  // process's sets in flight (every context's verify call, bls_sets_in_flight) pick:
+  // 2 above $BLS_MLF_PL2_MIN (default 98,304) sets, else 1.  $BLS_MLF_PER_LANE = 1, 2 or 4
+  // fixes it.
+  static const uint32_t fixed = [] {
     const char* e = getenv("BLS_MLF_PER_LANE");
-    const int v = e ? atoi(e) : 2;
-    return (v == 1 || v == 4) ? (uint32_t)v : 2u;
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
   }();
+  static const uint64_t pl2_min = [] {
+    const char* e = getenv("BLS_MLF_PL2_MIN");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 98304ull;
+  }();
+  const uint32_t per_lane = fixed ? fixed : (bls_sets_in_flight() > pl2_min ? 2u : 1u);
   const uint32_t lanes = (count + per_lane - 1) / per_lane;
   if (wf == 2) k_mlf<2><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
   else k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);

@@ -80,5 +80,7 @@ bool k_mln_list_ok(const bls::PipeBufs& b);
 hipError_t launch_k_mln_list(const bls::PipeBufs& b, const uint32_t* items, uint32_t count, hipStream_t s);
 hipError_t launch_k_mls(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, hipStream_t s);
 size_t mlq_line_words(uint32_t count);
+// sets in the verify calls currently running in this process (every context)
+uint64_t bls_sets_in_flight();
 hipError_t launch_k_mlqf(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, uint32_t* lines,
                          hipStream_t s, const uint32_t* items = nullptr);
