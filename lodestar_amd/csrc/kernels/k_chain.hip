@@ -237,6 +237,7 @@ __global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, 
 
 // One lane per set after the four roles: the set's fate.
 __global__ __launch_bounds__(BLS_BLOCK) void k_chain_done(PipeBufs b) {
+  BLS_TAIL_PRIO();
   const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (i >= b.n_sets) return;
   b.chain_live[i] = 0u;

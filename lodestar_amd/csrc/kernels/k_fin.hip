@@ -42,6 +42,7 @@ __device__ void fin_init(const CoopEnv& env, FinShared& sh) {
 }
 
 __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv env) {
+  BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t c = blockIdx.x;
   const uint32_t beg = b.chunk_off[c], end = b.chunk_off[c + 1];
@@ -69,6 +70,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv e
 }
 
 __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv env) {
+  BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t t = blockIdx.x;
   const uint32_t r = b.indiv_reqs[t];
@@ -91,6 +93,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
 // sequential product over a large request (a 128-set block call: 127 Fp12 products)
 // shrinks to one product per group.
 __global__ __launch_bounds__(COOP_LANES) void k_fold(PipeBufs b, CoopEnv env) {
+  BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t beg = b.fold_groups[2 * blockIdx.x], end = b.fold_groups[2 * blockIdx.x + 1];
   if (end - beg < 2) return;
@@ -114,6 +117,7 @@ hipError_t launch_k_fold(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
 // instead and writes FE(prod) == 1.
 __global__ __launch_bounds__(COOP_LANES) void k_fprod(const Fp12* in, uint32_t n, Fp12* out, int32_t* verdict,
                                                       CoopEnv env) {
+  BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t beg = blockIdx.x * FPROD_FAN;
   const uint32_t end = beg + FPROD_FAN < n ? beg + FPROD_FAN : n;

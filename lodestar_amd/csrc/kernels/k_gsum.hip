@@ -33,6 +33,7 @@ __device__ G2J chain_rs(const PipeBufs& b, uint32_t i) {
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_gsum(PipeBufs b, const uint32_t* seg, uint32_t n_seg, const G2J* in,
                                                     G2J* out) {
+  BLS_TAIL_PRIO();
   const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (k >= n_seg) return;
   const uint32_t beg = seg[2 * k], end = seg[2 * k + 1];
@@ -52,6 +53,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_gsum(PipeBufs b, const uint32_t* 
 }
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_vset(PipeBufs b, const G2J* sums, uint32_t n_groups, uint32_t vbase) {
+  BLS_TAIL_PRIO();
   const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (g >= n_groups) return;
   const uint32_t v = vbase + g;
@@ -87,6 +89,7 @@ __device__ __noinline__ void g1_add_p(G1J* acc, const G1J* p) { *acc = jac_add(*
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_gsum1(PipeBufs b, const uint32_t* seg, uint32_t n_seg, const G1J* in,
                                                      G1J* out) {
+  BLS_TAIL_PRIO();
   const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (k >= n_seg) return;
   const uint32_t beg = seg[2 * k], end = seg[2 * k + 1];
@@ -110,6 +113,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_gsum1(PipeBufs b, const uint32_t*
 
 // unit u of the call: rep = the set whose HQ the unit pairs (its root's first set)
 __global__ __launch_bounds__(BLS_BLOCK) void k_uset(PipeBufs b, const G1J* sums, const uint32_t* unit_rep) {
+  BLS_TAIL_PRIO();
   const uint32_t u = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (u >= b.n_units) return;
   const uint32_t v = b.unit_base + u;

@@ -103,6 +103,7 @@ hipError_t launch_k_validate_pubkeys(const uint8_t* pks, uint32_t n, uint32_t pk
 // context's host-mapped result area (read by the host after the stream syncs, no D2H
 // copy blits).
 __global__ __launch_bounds__(BLS_BLOCK) void k_status(PipeBufs b) {
+  BLS_TAIL_PRIO();
   const uint32_t r = blockIdx.x * BLS_BLOCK + threadIdx.x;
   stage_req_status(b, r);
   if (b.req_status_host && r < b.n_reqs) b.req_status_host[r] = b.req_status[r];

@@ -8,6 +8,16 @@
 
 #define BLS_BLOCK 64
 
+// Serial tails of a pass (signature sums, their affine form, the product tree and the
+// final exponentiations, status) run few wavefronts whose chains set the pass latency;
+// with other passes' wide kernels on the same SIMDs they raise their wave priority so the
+// SIMD issues them first (s_setprio 3).  $-free A/B: build variant "noprio".
+#ifdef BLS_NO_TAIL_PRIO
+#define BLS_TAIL_PRIO() ((void)0)
+#else
+#define BLS_TAIL_PRIO() __builtin_amdgcn_s_setprio(3)
+#endif
+
 static inline unsigned bls_grid_for(uint32_t n) { return (n + BLS_BLOCK - 1) / BLS_BLOCK; }
 
 hipError_t launch_k_pk(const bls::PipeBufs& b, hipStream_t s);
