@@ -51,6 +51,7 @@ __device__ G2A msm_point(const PipeBufs& b, uint32_t ref) {
 }  // namespace
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bin(PipeBufs b, MsmBufs m) {
+  BLS_TAIL_PRIO();
   const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (i >= b.n_sets) return;
   uint32_t* ent = m.ent + 8ull * i;
@@ -76,6 +77,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bin(PipeBufs b, MsmBufs m) {
 // one workgroup of 1024 lanes: off[k] = sum_{j<k} cnt[j]; seg_off likewise over
 // ceil(cnt / seg) segments per bucket
 __global__ __launch_bounds__(1024) void k_msm_scan(MsmBufs m, uint32_t seg) {
+  BLS_TAIL_PRIO();
   __shared__ uint32_t a[1024], c[1024];
   const uint32_t t = threadIdx.x;
   const uint32_t cnt = t < MSM_NB ? m.cnt[t] : 0u;
@@ -100,6 +102,7 @@ __global__ __launch_bounds__(1024) void k_msm_scan(MsmBufs m, uint32_t seg) {
 }
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_msm_scatter(PipeBufs b, MsmBufs m) {
+  BLS_TAIL_PRIO();
   const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (i >= b.n_sets) return;
   const uint32_t* ent = m.ent + 8ull * i;
@@ -113,6 +116,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_scatter(PipeBufs b, MsmBufs m
 
 // lane s: segment s of the bucket whose [seg_off[k], seg_off[k + 1]) holds it
 __global__ __launch_bounds__(BLS_BLOCK) void k_msm_seg(PipeBufs b, MsmBufs m, uint32_t seg) {
+  BLS_TAIL_PRIO();
   const uint32_t s = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (s >= m.seg_off[MSM_NB]) return;
   uint32_t lo = 0, hi = MSM_NB;  // largest k with seg_off[k] <= s
@@ -132,6 +136,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_seg(PipeBufs b, MsmBufs m, ui
 }
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bucket(MsmBufs m) {
+  BLS_TAIL_PRIO();
   const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (k >= MSM_NB) return;
   G2J acc = jac_infinity<Fp2>();
@@ -145,6 +150,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bucket(MsmBufs m) {
 // workgroup w, lane d: v_d = B_{w,d} (v_0 = O); suffix sums S_d = sum_{k >= d} v_k, then
 // T_w = sum_{d >= 1} S_d = sum_d d B_{w,d}; lane 0 scales by 2^(8 w)
 __global__ __launch_bounds__(256) void k_msm_window(MsmBufs m) {
+  BLS_TAIL_PRIO();
   __shared__ G2J L[256];
   const uint32_t w = blockIdx.x, d = threadIdx.x;
   G2J x = d ? m.bucket[w * MSM_D + d - 1] : jac_infinity<Fp2>();
@@ -177,6 +183,7 @@ __global__ __launch_bounds__(256) void k_msm_window(MsmBufs m) {
 
 // out[0] = sum_w win[w]; out[1 .. groups) = O
 __global__ __launch_bounds__(BLS_BLOCK) void k_msm_final(MsmBufs m, G2J* out, uint32_t groups) {
+  BLS_TAIL_PRIO();
   const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (g >= groups) return;
   if (g) {
