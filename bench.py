@@ -114,13 +114,15 @@ def sigagg_of(n_sets: int) -> bool:
     return (e != "0") if e not in (None, "") else n_sets >= SIGAGG_MIN_SETS
 
 
-def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
+def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None) -> tuple[float, str]:
     """Fp products the GPU executes per set for a cfg2 call of n_sets single-set
     batchable requests, every kernel of the call (k_pre, the per-set path, the chunks'
     signature sums and Miller loops, the merged check's product tree and final
     exponentiation): stage counts from lodestar_amd/_native/work_model.json
     (tools/work_model.cpp, host-compiled product math with the Fp-product counter) and
-    the cooperative programs' MUL ops (coop_programs.json)."""
+    the cooperative programs' MUL ops (coop_programs.json).  `shape`: the library's
+    bls_stats.pass_shape of the timed passes (bit 0 Pippenger signature sum, bits 8-15
+    items per k_mlf lane); None = the environment's fixed choices."""
     pg = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
     wm = json.loads((ROOT / "lodestar_amd" / "_native" / "work_model.json").read_text())
     m = {k: v["mul_ops"] for k, v in pg.items()}
@@ -136,15 +138,17 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16) -> tuple[float, str]:
                and "ml1s_8" in m)
         ml = (m["ml1s_8"] / 8 if sh8 else m["ml1s_4"] / 4) if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
         simt = int(os.environ.get("BLS_ML_SIMT", "2") or 2)
-        if simt == 2:    # k_mlq lines + k_mlf (two pairs per f): kernels/k_mlq.hip
-            ml = wm["ml_lines"] + wm["ml_f_pair"]
+        if simt == 2:    # k_mlq lines + k_mlf (two pairs per f, or one): kernels/k_mlq.hip
+            one = shape is not None and (shape >> 8) & 0xFF == 1 and "ml_f_one" in wm
+            ml = wm["ml_lines"] + (wm["ml_f_one"] if one else wm["ml_f_pair"])
         elif simt == 1:  # fused one-lane loop: kernels/k_mls.hip
             ml = wm["ml_simt"]
             ml1 = ml
         # the signature sums: one group sum over the pass and ONE signature Miller loop
         # (merged signature sum, $BLS_SIG_TOTAL), or one per chunk
         total = os.environ.get("BLS_SIG_TOTAL", "1") != "0" and chunks > 1
-        msm = total and os.environ.get("BLS_MSM", "0") == "1" and "msm_madd" in wm
+        msm = total and (bool(shape & 1) if shape is not None else os.environ.get("BLS_MSM", "0") == "1") \
+            and "msm_madd" in wm
         r_sig = wm["chain_r_sig"]
         if msm:
             # kernels/k_msm.hip: 8 (window, digit) entries per set, one mixed addition each
@@ -327,12 +331,14 @@ def timed_calls(ctxs, batches, steps: int):
     start = threading.Barrier(n + 1)
     stage_sum = np.zeros(8)
     ok = [True]
+    shapes: dict[int, int] = {}
     lock = threading.Lock()
 
     def worker(i):
         start.wait()
         acc = np.zeros(8)
         good = True
+        mine: dict[int, int] = {}
         for _ in range(steps):
             if isinstance(batches[i], list):
                 vs, st = ctxs[i].verify_many(batches[i])
@@ -341,9 +347,12 @@ def timed_calls(ctxs, batches, steps: int):
                 v, st = ctxs[i].verify_packed(batches[i])
                 good = good and bool((v == 1).all())
             acc += np.array(st.stage_ms[:])
+            mine[st.pass_shape] = mine.get(st.pass_shape, 0) + 1
         with lock:
             stage_sum[:] += acc
             ok[0] = ok[0] and good
+            for k, c in mine.items():
+                shapes[k] = shapes.get(k, 0) + c
 
     th = [threading.Thread(target=worker, args=(i,)) for i in range(n)]
     for t in th:
@@ -352,6 +361,7 @@ def timed_calls(ctxs, batches, steps: int):
     t0 = time.perf_counter()
     for t in th:
         t.join()
+    timed_calls.shapes = shapes  # pass_shape -> passes, for the roofline's work pricing
     return time.perf_counter() - t0, stage_sum / max(1, steps * n), ok[0]
 
 
@@ -615,14 +625,15 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--inflight", type=int, default=12, help="verifier contexts (HIP streams) per GPU")
-    # default 12 contexts x 16 calls (profiles/r03_knee.json): the rate follows the sets in
-    # flight up to ~3M sets/s (16 x 8 2.76M at 47 ms per pass, 12 x 16 2.94M at 67 ms,
-    # 16 x 16 3.03M at 87 ms); a call's verdicts arrive when its pass ends, inside the
+    # default 12 contexts x 22 calls (profiles/r03_knee.json): the rate follows the sets in
+    # flight (4 x 16 2.29M at 29 ms per pass, 12 x 16 3.09M at 64 ms, 12 x 22 3.34M at 81 ms,
+    # 16 x 16 3.30-3.38M at 78-79 ms: past 200k sets in flight the library switches to the
+    # Pippenger signature sum); a call's verdicts arrive when its pass ends, inside the
     # reference's 100 ms job buffering (multithread/index.ts:57 MAX_BUFFER_WAIT_MS).  12
     # contexts keep the scratch the runtime reserves per hardware queue (k_chain: 464 MiB)
     # well under the ~8 GiB at which it aborts queues (20 contexts did,
     # profiles/r03_scratch_out_of_resources.txt)
-    ap.add_argument("--calls-per-pass", type=int, default=16,
+    ap.add_argument("--calls-per-pass", type=int, default=22,
                     help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "
                          "its own chunks and verdicts)")
     ap.add_argument("--mode", choices=("cfg2", "sharded", "napi", "cfg4", "cfg5"), default="cfg2")
@@ -821,7 +832,9 @@ def main() -> None:
         #     time from HIP events on its context's stream (stage_ms: in the timed region,
         #     where ~contexts launches share the device, and in solo passes of the same
         #     K calls with the device to itself).
-        fpm_set, fpm_note = work_per_set(args.sets * K)  # one device pass: K calls
+        shapes = getattr(timed_calls, "shapes", {}) if args.mode == "cfg2" else {}
+        shape = max(shapes, key=shapes.get) if shapes else None  # the timed passes' usual shape
+        fpm_set, fpm_note = work_per_set(args.sets * K, shape=shape)  # one device pass: K calls
         mad_set = fpm_set * MADS_PER_FPM
         agg = sigagg_of(args.sets * K)
         solo_st = []
@@ -831,6 +844,7 @@ def main() -> None:
             else:
                 _, st = gpu.verify_packed(batch)
             solo_st.append(np.array(st.stage_ms[:]))
+            solo_shape = st.pass_shape
         solo_stage = np.median(np.array(solo_st), axis=0)
         peak_rate, _ = gpu.mad_peak()
         peak = peak_rate / 1e12
@@ -842,23 +856,35 @@ def main() -> None:
             kern = {}
             if agg:
                 simt = int(os.environ.get("BLS_ML_SIMT", "2") or 2)
-                per_k = {"k_chain": wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_pk"]
-                         + (0.0 if os.environ.get("BLS_MSM", "0") == "1" else wm["chain_r_sig"]),
-                         "miller_loops": (wm["ml_lines"] + wm["ml_f_pair"]) if simt == 2 else
-                         (wm["ml_simt"] if simt == 1 else None)}
-                for name, fpm in per_k.items():
+
+                def per_kernel(sh):  # Fp products per set of k_chain and the Miller loops
+                    msm = bool(sh & 1) if sh is not None else os.environ.get("BLS_MSM", "0") == "1"
+                    one = sh is not None and (sh >> 8) & 0xFF == 1 and "ml_f_one" in wm
+                    return {"k_chain": wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_pk"]
+                            + (0.0 if msm else wm["chain_r_sig"]),
+                            "miller_loops": (wm["ml_lines"] + (wm["ml_f_one"] if one else wm["ml_f_pair"]))
+                            if simt == 2 else (wm["ml_simt"] if simt == 1 else None)}
+
+                pk_timed, pk_solo = per_kernel(shape), per_kernel(solo_shape)
+                for name, fpm in pk_timed.items():
                     if fpm is None:
                         continue
                     i = STAGE_NAMES.index(name)
-                    mads = pass_sets * fpm * MADS_PER_FPM
+                    mads, mads_solo = pass_sets * fpm * MADS_PER_FPM, pass_sets * pk_solo[name] * MADS_PER_FPM
                     t_timed, t_solo = float(stage_ms[i]), float(solo_stage[i])
                     kern[name] = {
                         "mad_per_launch": round(mads),
                         "fp_products_per_set": round(fpm, 1),
+                        "fp_products_per_set_solo": round(pk_solo[name], 1),
                         "launch_ms_timed": round(t_timed, 3), "launch_ms_solo": round(t_solo, 3),
                         "achieved_timed": round(mads / (t_timed * 1e-3) / 1e12, 4) if t_timed > 0 else None,
-                        "achieved_solo": round(mads / (t_solo * 1e-3) / 1e12, 4) if t_solo > 0 else None,
-                        "frac_solo": round(mads / (t_solo * 1e-3) / 1e12 / peak, 4) if t_solo > 0 else None}
+                        "achieved_solo": round(mads_solo / (t_solo * 1e-3) / 1e12, 4) if t_solo > 0 else None,
+                        "frac_solo": round(mads_solo / (t_solo * 1e-3) / 1e12 / peak, 4) if t_solo > 0 else None}
+            if shapes:
+                extra_shape = {str(k): v for k, v in sorted(shapes.items())}
+                out["pass_shape"] = {"timed": extra_shape, "solo": solo_shape,
+                                     "note": "bls_stats.pass_shape -> passes: bit 0 Pippenger signature sum, "
+                                             "bits 8-15 items per k_mlf lane (both chosen by the sets in flight)"}
             roof = {"bound": "valu",
                     "kernel": ("every kernel of the pass; dominant: k_chain (per-set scalar chains) and the split "
                                "SIMT Miller loops (k_mlq + k_mlf)") if agg else "k_pset",

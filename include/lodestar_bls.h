@@ -72,6 +72,8 @@ typedef struct bls_stats {
   uint32_t n_unique_msgs;      /* distinct signing roots hashed to the curve (== n_sets without dedup) */
   uint32_t merged_check;       /* 0 not run, 1 passed (per-chunk checks skipped), 2 failed (chunks checked) */
   uint32_t n_ml_units;         /* Miller-loop units (chunk x shared signing root pairings), 0 = one per set */
+  uint32_t pass_shape;         /* how the aggregated path ran (0 on the per-set path): bit 0 the merged signature
+                                  sum by Pippenger MSM; bits 8-15 items per lane of the f side of the Miller loops */
 } bls_stats;
 
 typedef struct bls_gpu_ctx bls_gpu_ctx;
@@ -261,6 +263,9 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
 /* Test / bench hook: no Miller-loop units (one Miller loop per set even when sets of a
  * chunk share a signing root). */
 #define BLS_DEBUG_NO_UNITS 32u
+/* Test / bench hook: the merged signature sum as a Pippenger multi-scalar
+ * multiplication (kernels/k_msm.hip) whatever $BLS_MSM says. */
+#define BLS_DEBUG_MSM 64u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

@@ -81,6 +81,7 @@ DEBUG_NO_MERGED_CHECK = 4
 DEBUG_SIGAGG_ON = 8
 DEBUG_SIGAGG_OFF = 16
 DEBUG_NO_UNITS = 32
+DEBUG_MSM = 64
 
 
 def DEBUG_PACK(n: int) -> int:
@@ -116,6 +117,7 @@ class BlsStats(ctypes.Structure):
         ("n_unique_msgs", ctypes.c_uint32),
         ("merged_check", ctypes.c_uint32),
         ("n_ml_units", ctypes.c_uint32),
+        ("pass_shape", ctypes.c_uint32),
     ]
 
 

@@ -481,17 +481,24 @@ static void dbg_sync(hipStream_t s, const char* what) {
   fflush(stderr);
 }
 
-// Pippenger merged signature sum (k_msm): off unless $BLS_MSM=1.  It removes k_chain role 2
-// (~1.6k Fp products per set) but its serial stages (segments, buckets, the windows' 16
-// dependent additions) lengthen the pass by ~3 ms, and with the calls in flight the pass
-// latency, not the work, sets the rate: 2.39M vs 2.79M sets/s at 16 x 8
-// (profiles/r03_ab_msm.json)
+// Pippenger merged signature sum (k_msm) instead of the per-set [r] sig chains (k_chain
+// role 2, ~1.6k Fp products per set) and the k_gsum levels: ~10 % fewer instructions per
+// set, but its serial stages (segments, buckets, the windows' dependent additions) make
+// the pass ~5 ms longer.  So it pays only when the device is VALU-bound with many sets in
+// flight: 3.46M vs 3.21M sets/s at 16 x 16, level at 12 x 16, 1.89M vs 2.25M at 4 x 16
+// (profiles/r03_ab_msm.json).  By default on while the process has more than
+// $BLS_MSM_MIN (200,000) sets in flight; $BLS_MSM=1 / 0 forces it on / off.
 static bool msm_on() {
-  static const bool on = [] {
+  static const int forced = [] {
     const char* e = getenv("BLS_MSM");
-    return e && e[0] == '1';
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
   }();
-  return on;
+  static const uint64_t min_sets = [] {
+    const char* e = getenv("BLS_MSM_MIN");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 200000ull;
+  }();
+  if (forced >= 0) return forced == 1;
+  return bls_sets_in_flight() > min_sets;
 }
 
 // Shared Miller loops in k_mln (PipeBufs::ml_dom): on unless $BLS_ML_SHARED=0
@@ -767,7 +774,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // ... and under it the sum is one Pippenger MSM over the live sets (kernels/k_msm.hip)
   // instead of per-set [r] sig chains + k_gsum levels; the per-set RS are made (k_chain
   // role 2 alone) only when the merged check fails and the chunks' own sums are needed
-  const bool use_msm = use_total && msm_on();
+  const bool use_msm = use_total && (msm_on() || (ctx->debug_flags & BLS_DEBUG_MSM));
   GsumPlan total_gsum;
   if (use_total) {
     std::vector<uint32_t> goff(n_chunks + 1, (uint32_t)chunk_gsum.gsets.size());
@@ -1093,7 +1100,10 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     HIPC(ctx, hipStreamSynchronize(s));
     memcpy(chunk_ok.data(), res_host(ctx, b.chunk_ok), sizeof(int32_t) * n_chunks);
   }
-  if (stats) stats->merged_check = merged ? (merged_pass ? 1 : 2) : 0;
+  if (stats) {
+    stats->merged_check = merged ? (merged_pass ? 1 : 2) : 0;
+    stats->pass_shape = sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? mlf_per_lane() << 8 : 0u)) : 0u;
+  }
   if (stats) {
     stats->n_flagged = flagged;
     stats->n_unique_msgs = n_uniq;
@@ -1282,6 +1292,7 @@ int bls_gpu_verify_many(bls_gpu_ctx* ctx, const bls_batch* batches, uint32_t n_b
         stats->n_flagged += st.n_flagged;
         stats->n_unique_msgs += st.n_unique_msgs;
         stats->n_ml_units += st.n_ml_units;
+        stats->pass_shape |= st.pass_shape;
         stats->device_ms += st.device_ms;
       }
     }

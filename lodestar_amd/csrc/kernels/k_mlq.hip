@@ -201,6 +201,14 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   // process's sets in flight (every context's verify call, bls_sets_in_flight) pick:
   // 2 above $BLS_MLF_PL2_MIN (default 98,304) sets, else 1.  $BLS_MLF_PER_LANE = 1, 2 or 4
   // fixes it.
+  const uint32_t per_lane = mlf_per_lane();
+  const uint32_t lanes = (count + per_lane - 1) / per_lane;
+  if (wf == 2) k_mlf<2><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
+  else k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
+  return hipGetLastError();
+}
+
+uint32_t mlf_per_lane() {
   static const uint32_t fixed = [] {
     const char* e = getenv("BLS_MLF_PER_LANE");
     const int v = e ? atoi(e) : 0;
@@ -210,9 +218,5 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
     const char* e = getenv("BLS_MLF_PL2_MIN");
     return e ? (uint64_t)strtoull(e, nullptr, 10) : 98304ull;
   }();
-  const uint32_t per_lane = fixed ? fixed : (bls_sets_in_flight() > pl2_min ? 2u : 1u);
-  const uint32_t lanes = (count + per_lane - 1) / per_lane;
-  if (wf == 2) k_mlf<2><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
-  else k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
-  return hipGetLastError();
+  return fixed ? fixed : (bls_sets_in_flight() > pl2_min ? 2u : 1u);
 }

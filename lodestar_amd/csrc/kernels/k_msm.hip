@@ -8,13 +8,13 @@
 // 2 n affine points with 32-bit scalars, four 8-bit windows, 255 buckets per window.
 //
 //   k_msm_bin      one lane per set: its 8 (window, digit) entries, bucket slot by atomic count
-//   k_msm_scan     one workgroup: bucket offsets and level-0 segment offsets (prefix sums)
+//   k_msm_scan     one wavefront: bucket offsets and level-0 segment offsets (prefix sums)
 //   k_msm_scatter  one lane per set: point references into bucket order
 //   k_msm_seg      one lane per segment of <= seg points of one bucket: mixed additions
 //   k_msm_bucket   one lane per bucket: the sum of its segments
-//   k_msm_window   one workgroup of 256 lanes per window: T_w = sum_d d B_{w,d} as the sum
-//                  of the suffix sums of the buckets (Hillis-Steele scan + tree in LDS,
-//                  16 dependent additions), then [2^(8w)] T_w
+//   k_msm_window   one wavefront per window: T_w = sum_d d B_{w,d} from per-lane running
+//                  sums of 4 buckets, a suffix scan and a tree over the lanes in LDS,
+//                  then [2^(8w)] T_w
 //   k_msm_final    S = sum_w [2^(8w)] T_w into the pass's signature-sum slot (group 0;
 //                  the other chunk groups are infinity, so k_vset gives them f = 1)
 //
@@ -74,30 +74,40 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bin(PipeBufs b, MsmBufs m) {
   }
 }
 
-// one workgroup of 1024 lanes: off[k] = sum_{j<k} cnt[j]; seg_off likewise over
-// ceil(cnt / seg) segments per bucket
-__global__ __launch_bounds__(1024) void k_msm_scan(MsmBufs m, uint32_t seg) {
+// one wavefront (any SIMD with a free slot can take it under load; a 1024-lane workgroup
+// waited for a whole free CU): lane t owns buckets [16 t, 16 t + 16); off[k] = sum_{j<k}
+// cnt[j]; seg_off likewise over ceil(cnt / seg) segments per bucket
+__global__ __launch_bounds__(64) void k_msm_scan(MsmBufs m, uint32_t seg) {
   BLS_TAIL_PRIO();
-  __shared__ uint32_t a[1024], c[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t cnt = t < MSM_NB ? m.cnt[t] : 0u;
-  a[t] = cnt;
-  c[t] = (cnt + seg - 1) / seg;
+  __shared__ uint32_t a[64], c[64];
+  const uint32_t t = threadIdx.x, k0 = 16u * t;
+  uint32_t sa = 0, sc = 0;
+  for (uint32_t k = k0; k < k0 + 16u && k < MSM_NB; ++k) {
+    const uint32_t n = m.cnt[k];
+    sa += n;
+    sc += (n + seg - 1) / seg;
+  }
+  a[t] = sa;
+  c[t] = sc;
   __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+  for (uint32_t off = 1; off < 64; off <<= 1) {  // inclusive Hillis-Steele scan
     const uint32_t x = t >= off ? a[t - off] : 0u, y = t >= off ? c[t - off] : 0u;
     __syncthreads();
     a[t] += x;
     c[t] += y;
     __syncthreads();
   }
-  if (t < MSM_NB) {
-    m.off[t + 1] = a[t];
-    m.seg_off[t + 1] = c[t];
+  uint32_t pa = a[t] - sa, pc = c[t] - sc;  // exclusive prefixes of this lane's buckets
+  for (uint32_t k = k0; k < k0 + 16u && k < MSM_NB; ++k) {
+    m.off[k] = pa;
+    m.seg_off[k] = pc;
+    const uint32_t n = m.cnt[k];
+    pa += n;
+    pc += (n + seg - 1) / seg;
   }
-  if (t == 0) {
-    m.off[0] = 0;
-    m.seg_off[0] = 0;
+  if (t == 63) {
+    m.off[MSM_NB] = a[63];
+    m.seg_off[MSM_NB] = c[63];
   }
 }
 
@@ -147,34 +157,49 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bucket(MsmBufs m) {
   m.bucket[k] = acc;
 }
 
-// workgroup w, lane d: v_d = B_{w,d} (v_0 = O); suffix sums S_d = sum_{k >= d} v_k, then
-// T_w = sum_{d >= 1} S_d = sum_d d B_{w,d}; lane 0 scales by 2^(8 w)
-__global__ __launch_bounds__(256) void k_msm_window(MsmBufs m) {
+// one wavefront per window w (a 256-lane workgroup waited for a whole free CU under
+// load): T_w = sum_{d=1..255} d B_{w,d}.  Lane l owns digits d = 4 l + j (j = 0..3, B_0 = O):
+//   S_l = sum_j B_{4l+j},  W_l = sum_j j B_{4l+j}  (running sums, 5 additions)
+//   T_w = sum_l (4 l S_l + W_l) = sum_l ([4] U_l + W_l),  U_l = sum_{k >= l, k >= 1} S_k
+// U by a suffix scan over the lanes in LDS, then one tree; lane 0 scales by 2^(8 w)
+__global__ __launch_bounds__(64) void k_msm_window(MsmBufs m) {
   BLS_TAIL_PRIO();
-  __shared__ G2J L[256];
-  const uint32_t w = blockIdx.x, d = threadIdx.x;
-  G2J x = d ? m.bucket[w * MSM_D + d - 1] : jac_infinity<Fp2>();
-  L[d] = x;
+  __shared__ G2J L[64];
+  const uint32_t w = blockIdx.x, l = threadIdx.x;
+  auto bucket = [&](uint32_t d) { return d ? m.bucket[w * MSM_D + d - 1] : jac_infinity<Fp2>(); };
+  G2J s = bucket(4 * l + 3);  // suffix sums within the lane: s = B3, B3 + B2, ...
+  G2J wl = s;                 // W = B3 + (B3 + B2) + (B3 + B2 + B1)
+  for (int j = 2; j >= 0; --j) {
+    const G2J bj = bucket(4 * l + (uint32_t)j);
+    msm_add(&s, &bj);
+    if (j > 0) msm_add(&wl, &s);
+  }
+  L[l] = s;  // S_l
   __syncthreads();
-  for (uint32_t off = 1; off < 256; off <<= 1) {
-    G2J y = d + off < 256 ? L[d + off] : jac_infinity<Fp2>();
+  G2J u = s;
+  for (uint32_t off = 1; off < 64; off <<= 1) {  // suffix scan: U_l = sum_{k >= l} S_k
+    G2J y = l + off < 64 ? L[l + off] : jac_infinity<Fp2>();
     __syncthreads();
-    msm_add(&x, &y);
-    L[d] = x;
+    msm_add(&u, &y);
+    L[l] = u;
     __syncthreads();
   }
-  if (d == 0) L[0] = jac_infinity<Fp2>();
+  if (l == 0) u = jac_infinity<Fp2>();  // sum over l >= 1 only
+  msm_dbl(&u);
+  msm_dbl(&u);
+  msm_add(&u, &wl);
+  L[l] = u;
   __syncthreads();
-  for (uint32_t off = 128; off >= 1; off >>= 1) {
-    if (d < off) {
-      G2J y = L[d + off];
-      G2J z = L[d];
+  for (uint32_t off = 32; off >= 1; off >>= 1) {
+    if (l < off) {
+      G2J y = L[l + off];
+      G2J z = L[l];
       msm_add(&z, &y);
-      L[d] = z;
+      L[l] = z;
     }
     __syncthreads();
   }
-  if (d == 0) {
+  if (l == 0) {
     G2J t = L[0];
     for (uint32_t k = 0; k < 8 * w; ++k) msm_dbl(&t);
     m.win[w] = t;
@@ -214,11 +239,11 @@ hipError_t launch_k_msm(const PipeBufs& b, const MsmBufs& m, G2J* out, uint32_t 
   hipError_t e = hipMemsetAsync(m.cnt, 0, sizeof(uint32_t) * MSM_NB, s);
   if (e != hipSuccess) return e;
   k_msm_bin<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);
-  k_msm_scan<<<1, 1024, 0, s>>>(m, seg);
+  k_msm_scan<<<1, 64, 0, s>>>(m, seg);
   k_msm_scatter<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);
   k_msm_seg<<<bls_grid_for((uint32_t)msm_seg_cap(n)), BLS_BLOCK, 0, s>>>(b, m, seg);
   k_msm_bucket<<<bls_grid_for(MSM_NB), BLS_BLOCK, 0, s>>>(m);
-  k_msm_window<<<MSM_W, 256, 0, s>>>(m);
+  k_msm_window<<<MSM_W, 64, 0, s>>>(m);
   k_msm_final<<<bls_grid_for(groups), BLS_BLOCK, 0, s>>>(m, out, groups);
   return hipGetLastError();
 }

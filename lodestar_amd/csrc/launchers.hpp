@@ -92,5 +92,7 @@ hipError_t launch_k_mls(const bls::PipeBufs& b, uint32_t first, uint32_t count, 
 size_t mlq_line_words(uint32_t count);
 // sets in the verify calls currently running in this process (every context)
 uint64_t bls_sets_in_flight();
+// items per lane of k_mlf (1, 2 or 4) for a launch now (kernels/k_mlq.hip)
+uint32_t mlf_per_lane();
 hipError_t launch_k_mlqf(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, uint32_t* lines,
                          hipStream_t s, const uint32_t* items = nullptr);

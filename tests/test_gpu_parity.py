@@ -844,3 +844,40 @@ def test_failed_chunk_requests_verified_alone(gpu, oracle, table, n, bad):
     assert list(v) == expect
     retries, ok = _expected_stats(oracle, expect)
     assert (st.batch_retries, st.batch_sigs_success, st.merged_check) == (retries, ok, 2)
+
+
+def test_msm_signature_sum_matches_chains(gpu, oracle, table, verify_path):
+    """The Pippenger merged signature sum (BLS_DEBUG_MSM, kernels/k_msm.hip) gives the
+    verdicts and worker stats of the per-set [r] sig chains: 2,048 batchable sets (buckets
+    of several segments), all valid (the merged check passes on the MSM sum), then with
+    wrong signatures and an undecodable one (the MSM sum fails the merged check, the
+    chunks' own sums are rebuilt from k_chain role 2)."""
+    from lodestar_amd._abi import DEBUG_MSM
+
+    if verify_path != "sigagg":
+        pytest.skip("the MSM replaces the aggregated path's signature sum")
+    n = 2048
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"msm%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    for bad in ((), (5, 700, 2047)):
+        reqs, expect = [], []
+        for i in range(n):
+            sig, code = sigs[i].tobytes(), 1
+            if i in bad:
+                sig, code = sigs[(i + 1) % n].tobytes(), 0
+            if bad and i == 100:
+                sig, code = bytes(96), -CODE_BAD_ENCODING
+            reqs.append((True, [([i % 16], msgs[i], sig)]))
+            expect.append(code)
+        pb = pack_requests(reqs)
+        ref_v, ref_st = gpu.verify_packed(pb)
+        try:
+            gpu.set_debug_flags(DEBUG_MSM)
+            v, st = gpu.verify_packed(pb)
+        finally:
+            gpu.set_debug_flags(0)
+        assert list(v) == expect == list(ref_v)
+        assert st.merged_check == ref_st.merged_check == (2 if bad else 1)
+        retries, ok = _expected_stats(oracle, expect)
+        assert (st.batch_retries, st.batch_sigs_success) == (ref_st.batch_retries, ref_st.batch_sigs_success) == (retries, ok)
