@@ -114,6 +114,14 @@ def sigagg_of(n_sets: int) -> bool:
     return (e != "0") if e not in (None, "") else n_sets >= SIGAGG_MIN_SETS
 
 
+def mlf_products(wm: dict, shape: int | None) -> float:
+    """Fp products per item of k_mlf for a pass shape (items per lane in bits 8-15 of
+    bls_stats.pass_shape: 1, 2 or 4 pairs share f's squarings; None = 2)."""
+    per_lane = (shape >> 8) & 0xFF if shape is not None else 2
+    key = {1: "ml_f_one", 4: "ml_f_quad"}.get(per_lane, "ml_f_pair")
+    return wm.get(key, wm["ml_f_pair"])
+
+
 def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None) -> tuple[float, str]:
     """Fp products the GPU executes per set for a cfg2 call of n_sets single-set
     batchable requests, every kernel of the call (k_pre, the per-set path, the chunks'
@@ -139,8 +147,7 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None
         ml = (m["ml1s_8"] / 8 if sh8 else m["ml1s_4"] / 4) if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
         simt = int(os.environ.get("BLS_ML_SIMT", "2") or 2)
         if simt == 2:    # k_mlq lines + k_mlf (two pairs per f, or one): kernels/k_mlq.hip
-            one = shape is not None and (shape >> 8) & 0xFF == 1 and "ml_f_one" in wm
-            ml = wm["ml_lines"] + (wm["ml_f_one"] if one else wm["ml_f_pair"])
+            ml = wm["ml_lines"] + mlf_products(wm, shape)
         elif simt == 1:  # fused one-lane loop: kernels/k_mls.hip
             ml = wm["ml_simt"]
             ml1 = ml
@@ -859,10 +866,9 @@ def main() -> None:
 
                 def per_kernel(sh):  # Fp products per set of k_chain and the Miller loops
                     msm = bool(sh & 1) if sh is not None else os.environ.get("BLS_MSM", "0") == "1"
-                    one = sh is not None and (sh >> 8) & 0xFF == 1 and "ml_f_one" in wm
                     return {"k_chain": wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_pk"]
                             + (0.0 if msm else wm["chain_r_sig"]),
-                            "miller_loops": (wm["ml_lines"] + (wm["ml_f_one"] if one else wm["ml_f_pair"]))
+                            "miller_loops": (wm["ml_lines"] + mlf_products(wm, sh))
                             if simt == 2 else (wm["ml_simt"] if simt == 1 else None)}
 
                 pk_timed, pk_solo = per_kernel(shape), per_kernel(solo_shape)

@@ -266,6 +266,10 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
 /* Test / bench hook: the merged signature sum as a Pippenger multi-scalar
  * multiplication (kernels/k_msm.hip) whatever $BLS_MSM says. */
 #define BLS_DEBUG_MSM 64u
+/* Test / bench hook: items per lane of the Miller loops' f side (1, 2 or 4; 0 = by the
+ * process's sets in flight). */
+#define BLS_DEBUG_MLF_PL(n) ((uint32_t)(n) << 12)
+#define BLS_DEBUG_MLF_PL_MASK 0x7000u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

@@ -84,6 +84,11 @@ DEBUG_NO_UNITS = 32
 DEBUG_MSM = 64
 
 
+def DEBUG_MLF_PL(n: int) -> int:
+    """items per lane of the Miller loops' f side (BLS_DEBUG_MLF_PL in lodestar_bls.h)"""
+    return n << 12
+
+
 def DEBUG_PACK(n: int) -> int:
     """sets per wavefront of the per-set kernel (BLS_DEBUG_PACK in lodestar_bls.h)"""
     return n << 8

@@ -61,6 +61,7 @@ struct PipeBufs {
   uint32_t n_uniq;
   uint32_t scalar_base;        // set i draws r from index scalar_base + i (shards of one call, bls_gpu_partial)
   uint32_t pack;               // sets per wavefront of k_pset (0: by call size; BLS_DEBUG_PACK)
+  uint32_t mlf_pl;             // items per k_mlf lane (0: by the sets in flight; BLS_DEBUG_MLF_PL)
   uint32_t multi_set_rules;    // a shard of a larger call (bls_gpu_partial): no 1-set rules
   uint8_t* pk_inf;             // n_sets (nullable): 1 = the set's (aggregate) pubkey is infinity
   const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs

@@ -935,6 +935,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   b.pk_table_n = ctx->table_n;
   b.scalar_base = scalar_base;
   b.pack = (ctx->debug_flags & BLS_DEBUG_PACK_MASK) >> 8;
+  b.mlf_pl = (ctx->debug_flags & BLS_DEBUG_MLF_PL_MASK) >> 12;
   b.multi_set_rules = partial ? 1u : 0u;
   b.sigagg = sigagg ? 1u : 0u;
   b.unit_base = unit_base;
@@ -1102,7 +1103,8 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   }
   if (stats) {
     stats->merged_check = merged ? (merged_pass ? 1 : 2) : 0;
-    stats->pass_shape = sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? mlf_per_lane() << 8 : 0u)) : 0u;
+    stats->pass_shape =
+        sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? (b.mlf_pl ? b.mlf_pl : mlf_per_lane()) << 8 : 0u)) : 0u;
   }
   if (stats) {
     stats->n_flagged = flagged;

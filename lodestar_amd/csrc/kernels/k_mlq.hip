@@ -199,9 +199,9 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   // are in flight and the pass latency sets it): 2.22M vs 2.00M sets/s with 64k sets in
   // flight, 2.76M vs 2.90M with 128k (profiles/r03_ab_mlq_mlf.json).  By default the
   // process's sets in flight (every context's verify call, bls_sets_in_flight) pick:
-  // 2 above $BLS_MLF_PL2_MIN (default 98,304) sets, else 1.  $BLS_MLF_PER_LANE = 1, 2 or 4
-  // fixes it.
-  const uint32_t per_lane = mlf_per_lane();
+  // 2 above $BLS_MLF_PL2_MIN (default 98,304) sets, 4 above $BLS_MLF_PL4_MIN (200,000:
+  // 3.55M vs 3.41M sets/s at 12 x 22), else 1.  $BLS_MLF_PER_LANE = 1, 2 or 4 fixes it.
+  const uint32_t per_lane = b.mlf_pl ? b.mlf_pl : mlf_per_lane();
   const uint32_t lanes = (count + per_lane - 1) / per_lane;
   if (wf == 2) k_mlf<2><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
   else k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
@@ -218,5 +218,11 @@ uint32_t mlf_per_lane() {
     const char* e = getenv("BLS_MLF_PL2_MIN");
     return e ? (uint64_t)strtoull(e, nullptr, 10) : 98304ull;
   }();
-  return fixed ? fixed : (bls_sets_in_flight() > pl2_min ? 2u : 1u);
+  static const uint64_t pl4_min = [] {
+    const char* e = getenv("BLS_MLF_PL4_MIN");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 200000ull;
+  }();
+  if (fixed) return fixed;
+  const uint64_t k = bls_sets_in_flight();
+  return k > pl4_min ? 4u : (k > pl2_min ? 2u : 1u);
 }

@@ -50,6 +50,14 @@ __device__ G2A msm_point(const PipeBufs& b, uint32_t ref) {
 
 }  // namespace
 
+// the bucket counters to zero (one wavefront-sized workgroup per 64 counters; the runtime's
+// fill kernel for the same 4 KB averaged 5 ms per pass under load, profiles/r03_kernel_stats_default.csv)
+__global__ __launch_bounds__(BLS_BLOCK) void k_msm_zero(MsmBufs m) {
+  BLS_TAIL_PRIO();
+  const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (k < MSM_NB) m.cnt[k] = 0u;
+}
+
 __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bin(PipeBufs b, MsmBufs m) {
   BLS_TAIL_PRIO();
   const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
@@ -236,8 +244,7 @@ size_t msm_seg_cap(uint32_t n_sets) { return (8ull * n_sets) / msm_seg_len(n_set
 
 hipError_t launch_k_msm(const PipeBufs& b, const MsmBufs& m, G2J* out, uint32_t groups, hipStream_t s) {
   const uint32_t n = b.n_sets, seg = msm_seg_len(n);
-  hipError_t e = hipMemsetAsync(m.cnt, 0, sizeof(uint32_t) * MSM_NB, s);
-  if (e != hipSuccess) return e;
+  k_msm_zero<<<bls_grid_for(MSM_NB), BLS_BLOCK, 0, s>>>(m);
   k_msm_bin<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);
   k_msm_scan<<<1, 64, 0, s>>>(m, seg);
   k_msm_scatter<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);

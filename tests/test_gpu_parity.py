@@ -881,3 +881,44 @@ def test_msm_signature_sum_matches_chains(gpu, oracle, table, verify_path):
         assert st.merged_check == ref_st.merged_check == (2 if bad else 1)
         retries, ok = _expected_stats(oracle, expect)
         assert (st.batch_retries, st.batch_sigs_success) == (ref_st.batch_retries, ref_st.batch_sigs_success) == (retries, ok)
+
+
+@pytest.mark.parametrize("per_lane", [1, 2, 4])
+def test_mlf_items_per_lane(gpu, oracle, table, verify_path, per_lane):
+    """The f side of the split Miller loops with 1, 2 or 4 items per lane (the library
+    picks by the sets in flight; BLS_DEBUG_MLF_PL forces it), with and without the
+    Pippenger signature sum: invalid sets at a chunk's first, middle and last position and
+    in the last chunk, and an undecodable signature, so lanes whose items do not all share
+    a product domain or are not all live run them one by one; the merged check fails,
+    each chunk is checked, the failed chunks' requests are verified alone."""
+    from lodestar_amd._abi import DEBUG_MLF_PL, DEBUG_MSM
+
+    if verify_path != "sigagg":
+        pytest.skip("the split SIMT Miller loops run on the aggregated path")
+    n = 1030  # not a multiple of 4: the last lane holds fewer items
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"mlfpl%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    bad = {3, 15, 16, 517, 1029}
+    for with_bad in (False, True):
+        reqs, expect = [], []
+        for i in range(n):
+            sig, code = sigs[i].tobytes(), 1
+            if with_bad and i in bad:
+                sig, code = sigs[(i + 1) % n].tobytes(), 0
+            if with_bad and i == 600:
+                sig, code = bytes(96), -CODE_BAD_ENCODING
+            reqs.append((True, [([i % 16], msgs[i], sig)]))
+            expect.append(code)
+        pb = pack_requests(reqs)
+        retries, ok = _expected_stats(oracle, expect)
+        for extra in (0, DEBUG_MSM):
+            try:
+                gpu.set_debug_flags(DEBUG_MLF_PL(per_lane) | extra)
+                v, st = gpu.verify_packed(pb)
+            finally:
+                gpu.set_debug_flags(0)
+            assert list(v) == expect, (per_lane, extra)
+            assert st.merged_check == (2 if with_bad else 1)
+            assert (st.batch_retries, st.batch_sigs_success) == (retries, ok)
+            assert (st.pass_shape >> 8) & 0xFF == per_lane and (st.pass_shape & 1) == (1 if extra else 0)
