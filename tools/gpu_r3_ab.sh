@@ -34,13 +34,16 @@ if [ -n "$PMC" ]; then
   P3="GRBM_GUI_ACTIVE GRBM_COUNT"
   P4="FETCH_SIZE"
   P5="WRITE_SIZE"
+  # the probe pass runs the timed region's shape (one pass alone would pick the low-in-flight
+  # one): $PMC_ENV, default the Pippenger sum and four items per k_mlf lane
+  export ${PMC_ENV:-BLS_MSM=1 BLS_MLF_PER_LANE=4}
   PB="python3 $R/bench.py --probe-only --inflight 1 --calls-per-pass 32 --steps 1 --warmup 0"
   k=0
   for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
     k=$((k+1))
     timeout -s KILL 150 rocprofv3 --pmc $P -d $R/$O/pmc$k -o run --output-format csv -- $PB > $R/$O/pmc$k.log 2>&1 || { tail -20 $R/$O/pmc$k.log; exit 1; }
   done
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o run -- $PB > $R/$O/trace.log 2>&1 || { tail -20 $R/$O/trace.log; exit 1; }
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o run --output-format csv -- $PB > $R/$O/trace.log 2>&1 || { tail -20 $R/$O/trace.log; exit 1; }
   cd $R
   python3 tools/pmc_summary.py $O/pmc_summary.json "exactly one pass of 32 cfg2 calls (32768 sets; bench.py --probe-only --inflight 1 --calls-per-pass 32 --steps 1 --warmup 0); setup kernels (k_sign, k_sk_to_pk, k_load_pubkeys, k_aggregate) are input synthesis" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5 > $O/pmc_summary.txt
 fi

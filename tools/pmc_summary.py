@@ -54,7 +54,7 @@ def main() -> None:
     json.dump({"source": "rocprofv3 --pmc, one pass per counter group: " + " ".join(dirs), "kernels": kernels},
               open(out_path, "w"), indent=1)
     for name, k in kernels.items():
-        if any(t in name for t in ("pset", "k_mln", "k_chain", "k_pre")):
+        if any(t in name for t in ("pset", "k_mln", "k_chain", "k_pre", "k_mlq", "k_mlf", "k_msm", "k_fprod")):
             ipw = round(k["SQ_INSTS_VALU"] / k["SQ_WAVES"]) if k.get("SQ_WAVES") and "SQ_INSTS_VALU" in k else None
             print(name, {x: k.get(x) for x in ("waves_per_simd", "valu_busy", "hbm_bytes_per_launch", "SQ_WAVES")},
                   "valu_insts_per_wave", ipw)
