@@ -163,6 +163,22 @@ BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
   asm_add12_masked(r.l, d.l, pl, 0u - borrow);  // a < b: add p back
   return r;
 }
+
+// Unreduced forms for a product's operands only (the column product takes inputs < 3p,
+// test_hostsim.py::test_fp_mul_fips): a + b < 2p and a + p - b in (0, 2p] for a, b < p
+BLS_HD Fp fp_add_nr(const Fp& a, const Fp& b) {
+  Fp s;
+  asm_add12(s.l, a.l, b.l);
+  return s;
+}
+
+BLS_HD Fp fp_sub_nr(const Fp& a, const Fp& b) {
+  const uint32_t pl[12] = {BLS_P_LIMBS};
+  Fp t, r;
+  (void)asm_sub12(t.l, pl, b.l);  // p - b >= 1
+  asm_add12(r.l, a.l, t.l);
+  return r;
+}
 #else
 // Host build (CPU test harness and the CPU baseline under oracle/): the 12 x 32-bit
 // little-endian limbs are the bytes of 6 x 64-bit little-endian words, so the CPU
@@ -229,6 +245,37 @@ BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
       x[i] = (uint64_t)c;
       c >>= 64;
     }
+  }
+  return fp_w_store(x);
+}
+
+BLS_HD Fp fp_add_nr(const Fp& a, const Fp& b) {
+  uint64_t x[6], y[6];
+  fp_w_load(a, x);
+  fp_w_load(b, y);
+  unsigned __int128 c = 0;
+  for (int i = 0; i < 6; ++i) {
+    c += (unsigned __int128)x[i] + y[i];
+    x[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  return fp_w_store(x);
+}
+
+BLS_HD Fp fp_sub_nr(const Fp& a, const Fp& b) {
+  uint64_t x[6], y[6];
+  fp_w_load(a, x);
+  fp_w_load(b, y);
+  unsigned __int128 br = 0, c = 0;
+  for (int i = 0; i < 6; ++i) {  // y = p - b
+    const unsigned __int128 t = (unsigned __int128)BLS_P64[i] - y[i] - (uint64_t)br;
+    y[i] = (uint64_t)t;
+    br = (t >> 64) & 1;
+  }
+  for (int i = 0; i < 6; ++i) {
+    c += (unsigned __int128)x[i] + y[i];
+    x[i] = (uint64_t)c;
+    c >>= 64;
   }
   return fp_w_store(x);
 }
@@ -824,7 +871,8 @@ BLS_FP_MUL_ATTR Fp2 fp2_sqr_w(BLS_W12(a), BLS_W12(c)) { return fp2_sqr_d28(BLS_F
 #else
 // Host build: Montgomery product a*b/R mod p (R = 2^384) over 6 x 64-bit words,
 // separated operand scanning (the 36 partial products of a*b first, then the word-by-
-// word reduction), unsigned __int128 products.  Inputs < p, output < p.
+// word reduction), unsigned __int128 products.  Inputs < 2p (fp2_mul / fp2_sqr pass
+// unreduced sums, fp_add_nr), output < p.
 BLS_HD Fp fp_mul(const Fp& a, const Fp& b) {
   BLS_COUNT_FPM();
   typedef unsigned __int128 u128;
@@ -1170,7 +1218,11 @@ BLS_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
 #endif
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
+#ifdef BLS_FP2_EAGER  // build variant fp2eager: reduced pre-additions (A/B)
   Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+#else
+  Fp t2 = fp_mul(fp_add_nr(a.c0, a.c1), fp_add_nr(b.c0, b.c1));  // operands < 2p
+#endif
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
@@ -1178,9 +1230,15 @@ BLS_HD Fp2 fp2_sqr(const Fp2& a) {
 #ifdef BLS_FP2_MUL_FUSED
   return fp2_sqr_w(BLS_L12(a.c0), BLS_L12(a.c1));
 #endif
+#ifdef BLS_FP2_EAGER
   Fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
   Fp t1 = fp_mul(a.c0, a.c1);
   return Fp2{t0, fp_dbl(t1)};
+#else
+  Fp t0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub_nr(a.c0, a.c1));  // operands < 2p
+  Fp t1 = fp_mul(fp_add_nr(a.c0, a.c0), a.c1);                   // 2 a0 a1
+  return Fp2{t0, t1};
+#endif
 }
 
 // a * (1 + u)
