@@ -170,3 +170,28 @@ def test_bench_job_modes_gloo_world2(case):
         assert job0["calls"] == 4 and job0["sets"] == 32
         if case == "sharded_cfg4":
             assert job0["failing_calls"] >= 1
+
+
+def test_work_pricing_follows_pass_shape():
+    """bench.py prices the roofline's algorithmic work by the pass shape the library
+    reports (bls_stats.pass_shape): the Pippenger signature sum replaces the per-set
+    [r] sig chains, and 1 / 2 / 4 items per k_mlf lane share f's squarings, so the
+    products per set fall in that order; None keeps the environment's fixed choices."""
+    import json
+    from pathlib import Path
+
+    import bench
+
+    wm_path = Path(bench.ROOT) / "lodestar_amd" / "_native" / "work_model.json"
+    if not wm_path.exists():
+        pytest.skip("work model not built (build() writes it)")
+    wm = json.loads(wm_path.read_text())
+    assert bench.mlf_products(wm, 1 << 8) > bench.mlf_products(wm, 2 << 8) > bench.mlf_products(wm, 4 << 8)
+    assert bench.mlf_products(wm, None) == wm["ml_f_pair"]
+    n = 22 * 1024
+    chains, _ = bench.work_per_set(n, shape=2 << 8)
+    msm, note = bench.work_per_set(n, shape=1 | (2 << 8))
+    quad, _ = bench.work_per_set(n, shape=1 | (4 << 8))
+    assert "Pippenger" in note
+    assert chains - msm > 0.8 * wm["chain_r_sig"]  # the [r] sig chains leave, the MSM costs little
+    assert msm - quad == pytest.approx(wm["ml_f_pair"] - wm["ml_f_quad"])
