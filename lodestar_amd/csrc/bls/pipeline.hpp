@@ -247,6 +247,33 @@ BLS_HD void stage_pair_set(const PipeBufs& b, uint32_t i) {
 //   t < 2u:  SSWU point q_{t%2} of the set msg_uniq[t/2] (map_to_curve_sswu_fast;
 //            on its rare false return the set is flagged for the exact path)
 //   t >= 2u: decode signature t - 2u (on-curve, no subgroup test: k_pset does it)
+// A group's signature sum s becomes its virtual set v for the Miller loops: HQ =
+// affine(s) (one inversion), RP = -g1, so that f_v = ML(-g1, s); a sum at infinity (every
+// set errored, or the sum cancels) leaves nothing to pair: f_v = 1 (k_vset, k_msm_window)
+BLS_HD void vset_write(const PipeBufs& b, const G2J& s, uint32_t v) {
+  if (jac_is_inf(s)) {
+    b.chain_live[v] = 0u;
+    Fp* d = reinterpret_cast<Fp*>(&b.f[v]);
+    d[0] = c_one();
+    for (int k = 1; k < 12; ++k) d[k] = fp_zero();
+    return;
+  }
+  const Fp ni = fp_inv_gcd(fp_add(fp_sqr(s.z.c0), fp_sqr(s.z.c1)));
+  const Fp2 zi = Fp2{fp_mul(s.z.c0, ni), fp_neg(fp_mul(s.z.c1, ni))};
+  const Fp2 zi2 = fp2_sqr(zi);
+  const Fp2 x = fp2_mul(s.x, zi2);
+  const Fp2 y = fp2_mul(s.y, fp2_mul(zi2, zi));
+  Fp* o = b.chain + (size_t)CHAIN_WORDS * v;
+  o[CH_HQ + 0] = x.c0;
+  o[CH_HQ + 1] = x.c1;
+  o[CH_HQ + 2] = y.c0;
+  o[CH_HQ + 3] = y.c1;
+  o[CH_RP + 0] = c_g1_x();
+  o[CH_RP + 1] = c_g1_negy();
+  o[CH_RP + 2] = c_one();
+  b.chain_live[v] = 1u;
+}
+
 BLS_HD uint32_t pre_roots(const PipeBufs& b) { return b.msg_uniq ? b.n_uniq : b.n_sets; }
 BLS_HD uint32_t pre_lanes(const PipeBufs& b) { return 2 * pre_roots(b) + b.n_sets; }
 

@@ -47,6 +47,7 @@ struct bls_gpu_ctx {
   uint32_t table_n, table_cap;
   uint32_t debug_flags;  // bls_gpu_set_debug_flags
   // grow-only device workspace and pinned staging
+  uint32_t* msm_state;  // MSM bucket counters + tickets (MSM_STATE_WORDS), zero between passes
   uint8_t* dev_ws;
   size_t dev_ws_cap;
   uint8_t* host_stage;      // verify inputs, pinned + device-mapped: kernels read them in place
@@ -366,6 +367,7 @@ void bls_gpu_close(bls_gpu_ctx* ctx) {
   if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
   if (ctx->host_res) (void)hipHostFree(ctx->host_res);
   if (ctx->first_bad) (void)hipFree(ctx->first_bad);
+  if (ctx->msm_state) (void)hipFree(ctx->msm_state);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
   for (int i = 0; i < 9; ++i) (void)hipEventDestroy(ctx->ev[i]);
@@ -886,7 +888,6 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.f = c.take<Fp12>(n_total);
     b.ml_lines = sigagg ? c.take<uint32_t>(mlq_line_words(n_total)) : nullptr;
     if (use_msm) {
-      msm.cnt = c.take<uint32_t>(MSM_BUCKETS);
       msm.off = c.take<uint32_t>(MSM_BUCKETS + 1);
       msm.seg_off = c.take<uint32_t>(MSM_BUCKETS + 1);
       msm.ent = c.take<uint32_t>(8ull * n);
@@ -1002,8 +1003,13 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       HIPC(ctx, launch_k_chain(b, s, use_msm ? 0xBu : 0xFu)); dbg_sync(s, "k_chain");
       HIPC(ctx, hipEventRecord(ctx->ev[3], s));
       if (use_msm) {
-        HIPC(ctx, launch_k_msm(b, msm, gtmp[0], n_chunks, s)); dbg_sync(s, "k_msm");
-        HIPC(ctx, launch_k_vset(b, gtmp[0], n_chunks, n, s)); dbg_sync(s, "k_vset");
+        if (!ctx->msm_state) {
+          HIPC(ctx, hipMalloc(&ctx->msm_state, sizeof(uint32_t) * MSM_STATE_WORDS));
+          HIPC(ctx, hipMemsetAsync(ctx->msm_state, 0, sizeof(uint32_t) * MSM_STATE_WORDS, s));
+        }
+        msm.cnt = ctx->msm_state;
+        msm.ticket = ctx->msm_state + MSM_BUCKETS;
+        HIPC(ctx, launch_k_msm(b, msm, n_chunks, n, s)); dbg_sync(s, "k_msm");
       } else if (launch_gsum(ctx, b, use_total ? total_gsum : chunk_gsum, use_total ? tseg_dev : gseg_dev, gsets_dev,
                              gtmp, n, s)) {
         return -1;

@@ -56,30 +56,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_vset(PipeBufs b, const G2J* sums,
   BLS_TAIL_PRIO();
   const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (g >= n_groups) return;
-  const uint32_t v = vbase + g;
-  const G2J s = sums[g];
-  if (jac_is_inf(s)) {  // nothing to pair (every set errored, or the sum cancels): f = 1
-    b.chain_live[v] = 0u;
-    Fp* d = reinterpret_cast<Fp*>(&b.f[v]);
-    d[0] = c_one();
-#pragma unroll
-    for (int k = 1; k < 12; ++k) d[k] = fp_zero();
-    return;
-  }
-  const Fp ni = fp_inv_gcd(fp_add(fp_sqr(s.z.c0), fp_sqr(s.z.c1)));
-  const Fp2 zi = Fp2{fp_mul(s.z.c0, ni), fp_neg(fp_mul(s.z.c1, ni))};
-  const Fp2 zi2 = fp2_sqr(zi);
-  const Fp2 x = fp2_mul(s.x, zi2);
-  const Fp2 y = fp2_mul(s.y, fp2_mul(zi2, zi));
-  Fp* o = b.chain + (size_t)CHAIN_WORDS * v;
-  o[CH_HQ + 0] = x.c0;
-  o[CH_HQ + 1] = x.c1;
-  o[CH_HQ + 2] = y.c0;
-  o[CH_HQ + 3] = y.c1;
-  o[CH_RP + 0] = c_g1_x();
-  o[CH_RP + 1] = c_g1_negy();
-  o[CH_RP + 2] = c_one();
-  b.chain_live[v] = 1u;
+  vset_write(b, sums[g], vbase + g);
 }
 
 // Miller-loop units: segmented sums of RP_i = [r_i] pk_i (G1 Jacobian) over each unit's

@@ -7,16 +7,20 @@
 //   S = sum_i [a_i] sig_i + [b_i] mu(sig_i):
 // 2 n affine points with 32-bit scalars, four 8-bit windows, 255 buckets per window.
 //
-//   k_msm_bin      one lane per set: its 8 (window, digit) entries, bucket slot by atomic count
-//   k_msm_scan     one wavefront: bucket offsets and level-0 segment offsets (prefix sums)
+//   k_msm_bin      one lane per set: its 8 (window, digit) entries, bucket slot by atomic
+//                  count; the last workgroup to finish (ticket) turns the counts into
+//                  bucket and level-0 segment offsets and zeroes them for the next pass
 //   k_msm_scatter  one lane per set: point references into bucket order
 //   k_msm_seg      one lane per segment of <= seg points of one bucket: mixed additions
 //   k_msm_bucket   one lane per bucket: the sum of its segments
 //   k_msm_window   one wavefront per window: T_w = sum_d d B_{w,d} from per-lane running
 //                  sums of 4 buckets, a suffix scan and a tree over the lanes in LDS,
-//                  then [2^(8w)] T_w
-//   k_msm_final    S = sum_w [2^(8w)] T_w into the pass's signature-sum slot (group 0;
-//                  the other chunk groups are infinity, so k_vset gives them f = 1)
+//                  then [2^(8w)] T_w; the last window to finish (ticket) sums the four
+//                  into the pass's signature sum and writes the chunk groups' virtual
+//                  sets (group 0 the sum, the others infinity: f = 1; vset_write)
+// Each fused step saves a dispatch: under load a one-wave kernel waits milliseconds for
+// a free slot among the other passes' long waves (profiles/r03_ab_streams.json).
+// The counters and tickets live in a per-context buffer zeroed once (MsmBufs::cnt).
 //
 // Work per pass of n sets: ~8 n mixed additions (29 Fp products each) + n/seg * ... + a
 // fixed ~4k additions for the windows -- ~300 Fp products per set against ~1.6k for the
@@ -50,48 +54,52 @@ __device__ G2A msm_point(const PipeBufs& b, uint32_t ref) {
 
 }  // namespace
 
-// the bucket counters to zero (one wavefront-sized workgroup per 64 counters; the runtime's
-// fill kernel for the same 4 KB averaged 5 ms per pass under load, profiles/r03_kernel_stats_default.csv)
-__global__ __launch_bounds__(BLS_BLOCK) void k_msm_zero(MsmBufs m) {
-  BLS_TAIL_PRIO();
-  const uint32_t k = blockIdx.x * BLS_BLOCK + threadIdx.x;
-  if (k < MSM_NB) m.cnt[k] = 0u;
+// last workgroup of a launch: true in every lane of the workgroup that finished last;
+// the launch's writes are visible to it (device-scope release / acquire fences around a
+// device-scope ticket, reset for the next launch)
+__device__ bool msm_last_block(uint32_t* ticket) {
+  __shared__ uint32_t last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!last) return false;
+  __threadfence();
+  if (threadIdx.x == 0) (void)atomicExch(ticket, 0u);
+  return true;
 }
 
-__global__ __launch_bounds__(BLS_BLOCK) void k_msm_bin(PipeBufs b, MsmBufs m) {
+__global__ __launch_bounds__(BLS_BLOCK) void k_msm_bin(PipeBufs b, MsmBufs m, uint32_t seg) {
   BLS_TAIL_PRIO();
   const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
-  if (i >= b.n_sets) return;
-  uint32_t* ent = m.ent + 8ull * i;
-  if (!b.chain_live[i]) {
+  if (i < b.n_sets) {
+    uint32_t* ent = m.ent + 8ull * i;
+    if (!b.chain_live[i]) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ent[j] = ENT_NONE;
-    return;
-  }
-  uint32_t sc[2];
-  glv_split(set_scalar(b.seed, b.scalar_base + i), sc[0], sc[1]);
+      for (int j = 0; j < 8; ++j) ent[j] = ENT_NONE;
+    } else {
+      uint32_t sc[2];
+      glv_split(set_scalar(b.seed, b.scalar_base + i), sc[0], sc[1]);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t w = (uint32_t)j >> 1, d = (sc[j & 1] >> (8 * w)) & 255u;
-    if (d == 0) {
-      ent[j] = ENT_NONE;
-      continue;
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t w = (uint32_t)j >> 1, d = (sc[j & 1] >> (8 * w)) & 255u;
+        if (d == 0) {
+          ent[j] = ENT_NONE;
+          continue;
+        }
+        const uint32_t key = w * MSM_D + d - 1;
+        ent[j] = (key << 22) | atomicAdd(&m.cnt[key], 1u);
+      }
     }
-    const uint32_t key = w * MSM_D + d - 1;
-    ent[j] = (key << 22) | atomicAdd(&m.cnt[key], 1u);
   }
-}
-
-// one wavefront (any SIMD with a free slot can take it under load; a 1024-lane workgroup
-// waited for a whole free CU): lane t owns buckets [16 t, 16 t + 16); off[k] = sum_{j<k}
-// cnt[j]; seg_off likewise over ceil(cnt / seg) segments per bucket
-__global__ __launch_bounds__(64) void k_msm_scan(MsmBufs m, uint32_t seg) {
-  BLS_TAIL_PRIO();
+  if (!msm_last_block(m.ticket)) return;
+  // the scan, one wavefront: lane t owns buckets [16 t, 16 t + 16); off[k] = sum_{j<k}
+  // cnt[j], seg_off likewise over ceil(cnt / seg) segments per bucket
   __shared__ uint32_t a[64], c[64];
   const uint32_t t = threadIdx.x, k0 = 16u * t;
   uint32_t sa = 0, sc = 0;
   for (uint32_t k = k0; k < k0 + 16u && k < MSM_NB; ++k) {
-    const uint32_t n = m.cnt[k];
+    const uint32_t n = __hip_atomic_load(&m.cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sa += n;
     sc += (n + seg - 1) / seg;
   }
@@ -107,11 +115,12 @@ __global__ __launch_bounds__(64) void k_msm_scan(MsmBufs m, uint32_t seg) {
   }
   uint32_t pa = a[t] - sa, pc = c[t] - sc;  // exclusive prefixes of this lane's buckets
   for (uint32_t k = k0; k < k0 + 16u && k < MSM_NB; ++k) {
+    const uint32_t n = __hip_atomic_load(&m.cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     m.off[k] = pa;
     m.seg_off[k] = pc;
-    const uint32_t n = m.cnt[k];
     pa += n;
     pc += (n + seg - 1) / seg;
+    __hip_atomic_store(&m.cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // zero for the next pass
   }
   if (t == 63) {
     m.off[MSM_NB] = a[63];
@@ -170,7 +179,7 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_bucket(MsmBufs m) {
 //   S_l = sum_j B_{4l+j},  W_l = sum_j j B_{4l+j}  (running sums, 5 additions)
 //   T_w = sum_l (4 l S_l + W_l) = sum_l ([4] U_l + W_l),  U_l = sum_{k >= l, k >= 1} S_k
 // U by a suffix scan over the lanes in LDS, then one tree; lane 0 scales by 2^(8 w)
-__global__ __launch_bounds__(64) void k_msm_window(MsmBufs m) {
+__global__ __launch_bounds__(64) void k_msm_window(PipeBufs b, MsmBufs m, uint32_t groups, uint32_t vbase) {
   BLS_TAIL_PRIO();
   __shared__ G2J L[64];
   const uint32_t w = blockIdx.x, l = threadIdx.x;
@@ -212,23 +221,17 @@ __global__ __launch_bounds__(64) void k_msm_window(MsmBufs m) {
     for (uint32_t k = 0; k < 8 * w; ++k) msm_dbl(&t);
     m.win[w] = t;
   }
-}
-
-// out[0] = sum_w win[w]; out[1 .. groups) = O
-__global__ __launch_bounds__(BLS_BLOCK) void k_msm_final(MsmBufs m, G2J* out, uint32_t groups) {
-  BLS_TAIL_PRIO();
-  const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
-  if (g >= groups) return;
-  if (g) {
-    out[g] = jac_infinity<Fp2>();
-    return;
+  if (!msm_last_block(m.ticket + 1)) return;
+  // S = sum_w [2^(8w)] T_w: the chunk group 0's virtual set; the other groups are empty
+  if (l == 0) {
+    G2J acc = m.win[0];
+    for (uint32_t k = 1; k < MSM_W; ++k) {
+      const G2J p = m.win[k];
+      msm_add(&acc, &p);
+    }
+    vset_write(b, acc, vbase);
   }
-  G2J acc = m.win[0];
-  for (uint32_t w = 1; w < MSM_W; ++w) {
-    const G2J p = m.win[w];
-    msm_add(&acc, &p);
-  }
-  out[0] = acc;
+  for (uint32_t g = 1 + l; g < groups; g += 64) vset_write(b, jac_infinity<Fp2>(), vbase + g);
 }
 
 uint32_t msm_seg_len(uint32_t n_sets) {
@@ -242,15 +245,13 @@ uint32_t msm_seg_len(uint32_t n_sets) {
 
 size_t msm_seg_cap(uint32_t n_sets) { return (8ull * n_sets) / msm_seg_len(n_sets) + MSM_NB + 1; }
 
-hipError_t launch_k_msm(const PipeBufs& b, const MsmBufs& m, G2J* out, uint32_t groups, hipStream_t s) {
+hipError_t launch_k_msm(const PipeBufs& b, const MsmBufs& m, uint32_t groups, uint32_t vbase, hipStream_t s) {
   const uint32_t n = b.n_sets, seg = msm_seg_len(n);
-  k_msm_zero<<<bls_grid_for(MSM_NB), BLS_BLOCK, 0, s>>>(m);
-  k_msm_bin<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);
-  k_msm_scan<<<1, 64, 0, s>>>(m, seg);
+  if (n == 0) return hipErrorInvalidValue;
+  k_msm_bin<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m, seg);
   k_msm_scatter<<<bls_grid_for(n), BLS_BLOCK, 0, s>>>(b, m);
   k_msm_seg<<<bls_grid_for((uint32_t)msm_seg_cap(n)), BLS_BLOCK, 0, s>>>(b, m, seg);
   k_msm_bucket<<<bls_grid_for(MSM_NB), BLS_BLOCK, 0, s>>>(m);
-  k_msm_window<<<MSM_W, 64, 0, s>>>(m);
-  k_msm_final<<<bls_grid_for(groups), BLS_BLOCK, 0, s>>>(m, out, groups);
+  k_msm_window<<<MSM_W, 64, 0, s>>>(b, m, groups, vbase);
   return hipGetLastError();
 }

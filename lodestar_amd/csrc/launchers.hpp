@@ -35,7 +35,8 @@ hipError_t launch_k_exact(const bls::PipeBufs& b, hipStream_t s);
 hipError_t launch_k_chain(const bls::PipeBufs& b, hipStream_t s, uint32_t roles = 0xFu);
 // Pippenger sum of [r_i] sig_i over the live sets (kernels/k_msm.hip)
 struct MsmBufs {
-  uint32_t* cnt;      // 1020 bucket counts
+  uint32_t* cnt;      // 1020 bucket counts + 2 tickets: per context, zero between passes
+  uint32_t* ticket;   // cnt + 1020
   uint32_t* off;      // 1021 bucket offsets into sorted
   uint32_t* seg_off;  // 1021 segment offsets
   uint32_t* ent;      // 8 n_sets (bucket << 22 | slot) entries
@@ -46,7 +47,9 @@ struct MsmBufs {
 };
 #define MSM_BUCKETS 1020u
 size_t msm_seg_cap(uint32_t n_sets);
-hipError_t launch_k_msm(const bls::PipeBufs& b, const MsmBufs& m, bls::G2J* out, uint32_t groups, hipStream_t s);
+#define MSM_STATE_WORDS (MSM_BUCKETS + 2u)
+// the merged signature sum into the chunk groups' virtual sets vbase .. vbase + groups
+hipError_t launch_k_msm(const bls::PipeBufs& b, const MsmBufs& m, uint32_t groups, uint32_t vbase, hipStream_t s);
 hipError_t launch_k_gsum(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const bls::G2J* in,
                          bls::G2J* out, hipStream_t s);
 hipError_t launch_k_vset(const bls::PipeBufs& b, const bls::G2J* sums, uint32_t n_groups, uint32_t vbase,
