@@ -633,9 +633,9 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--inflight", type=int, default=12, help="verifier contexts (HIP streams) per GPU")
     # default 12 contexts x 22 calls (profiles/r03_knee.json): the rate follows the sets in
-    # flight (4 x 16 2.29M at 29 ms per pass, 12 x 16 3.09M at 64 ms, 12 x 22 3.34M at 81 ms,
-    # 16 x 16 3.30-3.38M at 78-79 ms: past 200k sets in flight the library switches to the
-    # Pippenger signature sum); a call's verdicts arrive when its pass ends, inside the
+    # flight (4 x 16 2.29M at 29 ms per pass, 12 x 16 3.09M at 64 ms, 12 x 22 3.52-3.60M at
+    # 75-77 ms: past 200k sets in flight the library switches to the Pippenger signature sum
+    # and four items per k_mlf lane); a call's verdicts arrive when its pass ends, inside the
     # reference's 100 ms job buffering (multithread/index.ts:57 MAX_BUFFER_WAIT_MS).  12
     # contexts keep the scratch the runtime reserves per hardware queue (k_chain: 464 MiB)
     # well under the ~8 GiB at which it aborts queues (20 contexts did,
