@@ -43,7 +43,8 @@ VARIANTS = {"mul32": ["-DBLS_FP_MUL32", "-DBLS_CHAIN_INL32"], "chain_inl32": ["-
             "chain_occ1": ["-DBLS_CHAIN_OCC1"], "chain_occ3": ["-DBLS_CHAIN_OCC3"],
             "chain_binr": ["-DBLS_CHAIN_BINARY_R"], "chain_w4": ["-DBLS_CHAIN_W4"],
             "chain_inl28": ["-DBLS_CHAIN_INL28"], "fp2fused": ["-DBLS_FP2_FUSED"], "fips": ["-DBLS_FP_FIPS"], "cios": ["-DBLS_FP_CIOS"],
-            "noprio": ["-DBLS_NO_TAIL_PRIO"], "fp2eager": ["-DBLS_FP2_EAGER"]}
+            "noprio": ["-DBLS_NO_TAIL_PRIO"], "fp2eager": ["-DBLS_FP2_EAGER"],
+            "mlf_single": ["-DBLS_MLF_SINGLE_LINES"]}
 
 
 # Scratch budget (the guard against the round-2 "kernel never finished"): the HIP runtime

@@ -91,8 +91,19 @@ __device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, uint32_
     if (bit != 62) f = sqr12(f);
     const int adds = (int)((X >> bit) & 1ull);
     for (int a = 0; a <= adds; ++a) {
+      uint32_t g = 0;
+#ifndef BLS_MLF_SINGLE_LINES
+      // two items' lines at once (fp12_mul_line2: 23 Fp2 products instead of 26)
 #pragma unroll 1
-      for (uint32_t g = 0; g < n; ++g) {
+      for (; g + 1 < n; g += 2) {
+        Fp2 l0, l2, l3, m0, m2, m3;
+        load_line(L, stride, k0 + g, e, l0, l2, l3);
+        load_line(L, stride, k0 + g + 1, e, m0, m2, m3);
+        f = fp12_mul_line2(f, l0, l2, l3, m0, m2, m3);
+      }
+#endif
+#pragma unroll 1
+      for (; g < n; ++g) {
         Fp2 l0, l2, l3;
         load_line(L, stride, k0 + g, e, l0, l2, l3);
         f = mul_line12(f, l0, l2, l3);

@@ -195,6 +195,11 @@ void hs_fp12_frob2(const uint8_t* a, uint8_t* out) { wr_fp12(fp12_frob2(rd_fp12(
 void hs_fp12_mul_line(const uint8_t* f, const uint8_t* l0, const uint8_t* l2, const uint8_t* l3, uint8_t* out) {
   wr_fp12(fp12_mul_line(rd_fp12(f), rd_fp2(l0), rd_fp2(l2), rd_fp2(l3)), out);
 }
+void hs_fp12_mul_line2(const uint8_t* f, const uint8_t* l, const uint8_t* m, uint8_t* out) {
+  wr_fp12(fp12_mul_line2(rd_fp12(f), rd_fp2(l), rd_fp2(l + 96), rd_fp2(l + 192), rd_fp2(m), rd_fp2(m + 96),
+                         rd_fp2(m + 192)),
+          out);
+}
 void hs_final_exp(const uint8_t* a, uint8_t* out) { wr_fp12(final_exponentiation(rd_fp12(a)), out); }
 
 void hs_miller_loop(const uint8_t* g1, const uint8_t* g2, uint8_t* out) {

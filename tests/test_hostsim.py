@@ -193,6 +193,20 @@ def test_fp12_tower(hostsim, oracle):
     assert bf12(o.raw) == oracle.f12_mul(t, t)
 
 
+def test_fp12_mul_line2(hostsim):
+    """Two sparse line products at once (field.hpp fp12_mul_line2: the lines' product
+    first, 23 Fp2 products instead of 26) equal the two products one after the other."""
+    rng = random.Random(12)
+    o1, o2 = _buf(576), _buf(576)
+    for _ in range(20):
+        f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+        ls = [[(rng.randrange(P), rng.randrange(P)) for _ in range(3)] for _ in range(2)]
+        hostsim.hs_fp12_mul_line(f12b(f), f2b(ls[0][0]), f2b(ls[0][1]), f2b(ls[0][2]), o1)
+        hostsim.hs_fp12_mul_line(o1.raw, f2b(ls[1][0]), f2b(ls[1][1]), f2b(ls[1][2]), o1)
+        hostsim.hs_fp12_mul_line2(f12b(f), b"".join(f2b(x) for x in ls[0]), b"".join(f2b(x) for x in ls[1]), o2)
+        assert o1.raw == o2.raw
+
+
 def test_hash_to_g2_golden(hostsim, golden):
     o = _buf(192)
     for v in golden["hash_to_g2"]:
