@@ -87,11 +87,12 @@ int main() {
         }
       }
       mlq += tick();
-      // k_mlf: two pairs per f -- 62 squarings and 2 x 68 sparse line products, per pair
+      // k_mlf: two pairs per f -- 62 squarings and 68 paired line products (fp12_mul_line2)
       Fp12 g = fp12_one();
       for (int bit = 62; bit >= 0; --bit) {
         if (bit != 62) g = fp12_sqr(g);
-        for (int rep = 0; rep < (((BLS_X_ABS >> bit) & 1ull) ? 4 : 2); ++rep) g = fp12_mul_line(g, c0, c1, c2);
+        for (int rep = 0; rep < (((BLS_X_ABS >> bit) & 1ull) ? 2 : 1); ++rep)
+          g = fp12_mul_line2(g, c0, c1, c2, c0, c1, c2);
       }
       mlf += tick() / 2.0;
       // k_mlf with one pair per f (few sets in flight): 62 squarings and 68 line products
@@ -101,11 +102,12 @@ int main() {
         for (int rep = 0; rep < (((BLS_X_ABS >> bit) & 1ull) ? 2 : 1); ++rep) g1 = fp12_mul_line(g1, c0, c1, c2);
       }
       mlf1 += tick();
-      // four pairs per f (many sets in flight): 62 squarings and 4 x 68 line products
+      // four pairs per f (many sets in flight): 62 squarings and 2 x 68 paired line products
       Fp12 g4 = fp12_one();
       for (int bit = 62; bit >= 0; --bit) {
         if (bit != 62) g4 = fp12_sqr(g4);
-        for (int rep = 0; rep < (((BLS_X_ABS >> bit) & 1ull) ? 8 : 4); ++rep) g4 = fp12_mul_line(g4, c0, c1, c2);
+        for (int rep = 0; rep < (((BLS_X_ABS >> bit) & 1ull) ? 4 : 2); ++rep)
+          g4 = fp12_mul_line2(g4, c0, c1, c2, c0, c1, c2);
       }
       mlf4 += tick() / 4.0;
     }
