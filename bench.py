@@ -137,20 +137,11 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None
     chunks = max(1, n_sets // reqs_per_chunk)
     merged = (n_sets + chunks - 1) * m["fin_fmul"] + m["fin_fe1"] + m["fin_fe2"]
     if sigagg_of(n_sets):
-        # a set's Miller-loop share: eight sets of a chunk share one loop (ml1s_8, k_mlns<8>;
-        # four with $BLS_ML_SHARE=4 or without the small frame; none with
-        # $BLS_ML_SHARED=0) -- blst's multi-pairing likewise shares f's squarings; a
-        # chunk's signature-sum pair runs a single-pair loop (ml1_4 / 4)
-        ml1 = m["ml1_4"] / 4
-        sh8 = (os.environ.get("BLS_ML_SHARE") != "4" and os.environ.get("BLS_ML_SMALL_FRAME", "1") != "0"
-               and "ml1s_8" in m)
-        ml = (m["ml1s_8"] / 8 if sh8 else m["ml1s_4"] / 4) if os.environ.get("BLS_ML_SHARED", "1") != "0" else ml1
-        simt = int(os.environ.get("BLS_ML_SIMT", "2") or 2)
-        if simt == 2:    # k_mlq lines + k_mlf (two pairs per f, or one): kernels/k_mlq.hip
-            ml = wm["ml_lines"] + mlf_products(wm, shape)
-        elif simt == 1:  # fused one-lane loop: kernels/k_mls.hip
-            ml = wm["ml_simt"]
-            ml1 = ml
+        # a set's Miller loop: k_mlq lines + k_mlf f side (1, 2 or 4 pairs sharing f's
+        # squarings, as blst's multi-pairing does; kernels/k_mlq.hip); a chunk's
+        # signature-sum pair runs the same loop
+        ml = wm["ml_lines"] + mlf_products(wm, shape)
+        ml1 = ml
         # the signature sums: one group sum over the pass and ONE signature Miller loop
         # (merged signature sum, $BLS_SIG_TOTAL), or one per chunk
         total = os.environ.get("BLS_SIG_TOTAL", "1") != "0" and chunks > 1
@@ -168,9 +159,9 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None
             fixed = (4 * (256 * 8 + 255) + 3) * wm["gsum_add"] + 36 * wm["g2_dbl"]
             r_sig = 0.0
             sums = (8 * 255 / 256 * wm["msm_madd"] + 4 * wm["msm_mu"] + 8 / seg * wm["gsum_add"] + fixed / n_sets
-                    + (m["ml1_1"] + wm["vset"]) / n_sets)
+                    + (ml1 + wm["vset"]) / n_sets)
         elif total:
-            sums = (m["ml1_1"] + wm["vset"]) / n_sets + (n_sets - 1) / n_sets * wm["gsum_add"]
+            sums = (ml1 + wm["vset"]) / n_sets + (n_sets - 1) / n_sets * wm["gsum_add"]
         else:
             sums = chunks / n_sets * (ml1 + wm["vset"]) + (n_sets - chunks) / n_sets * wm["gsum_add"]
         per = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + r_sig + wm["chain_r_pk"] + ml
@@ -316,9 +307,10 @@ def cpu_baseline(sets, raw96, threads: int | None = None, seconds: float = 10.0,
             "cpu": _cpu_model(), "nproc": os.cpu_count(),
             "cgroup_cpu_quota": quota,
             "per_core_sets_per_s": round(one.value, 1),
-            "whole_host_sets_per_s": round(one.value * (os.cpu_count() or 1), 1),
-            "whole_host_note": "one worker's rate x nproc: the reference pool on every core of this host with no "
-                               "quota (an upper bound: no memory-bandwidth or SMT contention counted)",
+            "whole_host_sets_per_s_extrapolated": round(one.value * (os.cpu_count() or 1), 1),
+            "whole_host_note": "EXTRAPOLATED, not measured: one worker's measured rate x nproc, the reference pool "
+                               "on every core of this host with no quota (an upper bound: no memory-bandwidth or SMT "
+                               "contention counted); `value` is what the pool measured under this job's quota",
             "sample": f"cfg2: {threads} worker threads (one per core, poolSize.ts:3-11) x messages of 128 batchable "
                       f"single-set requests for {seconds:.0f} s ({msgs.value} messages); one worker alone for "
                       f"{min(seconds, 5.0):.0f} s ({one_msgs.value} messages); cfg1: one 128-set non-batchable request "
@@ -406,7 +398,8 @@ def run_calls(ctxs, packed, calls_per_pass: int):
 
 
 def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, reps: int = 3,
-                latency_runs: int = 10) -> dict:
+                latency_runs: int = 10, cfg4_ctx: int = 4, cfg4_cpp: int = 32, cfg5_sets: int = 131_072,
+                cfg5_roots: int = 256) -> dict:
     """BASELINE configs 3 and 4 at N = 1: cfg3, one block-import call
     (latency, sets/s, pubkeys aggregated/s); cfg4 this GPU's slice of the 1M-set range-sync
     job (1/8: shard by call), once with range sync's own non-batchable 128-set calls and
@@ -440,9 +433,9 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
                        "p99_ms": round(float(np.percentile(np.array(lat) * 1e3, 99)), 3),
                        "sets_per_s": round(n3 / p50, 1), "pubkeys_aggregated_per_s": round(keys3 / p50, 1),
                        "stage_ms": {k: round(float(x) / latency_runs, 3) for k, x in zip(STAGE_NAMES, stage)}}
-        # cfg4: this GPU's slice, both call shapes
-        # cfg4 calls are 128 sets: 32 of them per device pass (4096 sets) on 4 contexts
-        c4, cpp4 = ctxs[:4], 32
+        # cfg4: this GPU's slice, both call shapes; calls of 128 sets, cfg4_cpp of them per
+        # device pass on cfg4_ctx contexts (sets in flight = the product, stated)
+        c4, cpp4 = ctxs[:cfg4_ctx], cfg4_cpp
         for key, batchable in (("cfg4_slice", False), ("cfg4_slice_batchable", True)):
             w4 = W.cfg4_slice(ctxs[0], n_keys, cfg4_sets, batchable_calls=batchable)
             pbs = W.packed_calls(w4)
@@ -457,10 +450,33 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
             res[key] = {"workload": w4.note, "sets": w4.n_sets, "calls": len(pbs), "invalid_sets": n_inv,
                         "false_requests": sum(int((o == 0).sum()) for o in out),
                         "elapsed_s": round(best, 4), "sets_per_s": round(w4.n_sets / best, 1),
-                        "contexts": len(c4), "calls_per_pass": cpp4, "runs": reps,
+                        "contexts": len(c4), "calls_per_pass": cpp4, "sets_in_flight": len(c4) * cpp4 * 128,
+                        "runs": reps,
                         "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
                         "passes_merged_check_failed": tot["merged_fail"],
                         "verdicts": "every call matches the sets' validity by construction"}
+        # cfg5: this GPU's slice of the mainnet epoch (1/8 of ~1M attestations over 2048
+        # committee roots), calls of 1024 batchable single-set requests on the headline's
+        # contexts, invalid sets included (their passes fail the merged check and run the
+        # chunk and per-request fallback inside the timed region)
+        w5 = W.cfg5_slice(ctxs[0], n_keys, cfg5_sets, cfg5_roots, invalid=max(1, cfg5_sets // 2048))
+        pbs = W.packed_calls(w5)
+        cpp5 = (len(pbs) + n_ctx - 1) // n_ctx
+        run_calls(ctxs, pbs[: n_ctx], 1)  # warm-up
+        best, out, tot = None, None, None
+        for _ in range(reps):
+            el, out, tot = run_calls(ctxs, pbs, cpp5)
+            best = el if best is None else min(best, el)
+        bad = [k for k in range(len(pbs)) if not W.verdicts_ok(w5, k, out[k])]
+        assert not bad, f"cfg5_slice: {len(bad)} calls with wrong verdicts (first {bad[0]})"
+        res["cfg5_slice"] = {"workload": w5.note, "sets": w5.n_sets, "calls": len(pbs),
+                             "invalid_sets": sum(not x for v in w5.valid for x in v),
+                             "false_requests": sum(int((o == 0).sum()) for o in out),
+                             "elapsed_s": round(best, 4), "sets_per_s": round(w5.n_sets / best, 1),
+                             "contexts": n_ctx, "calls_per_pass": cpp5, "runs": reps,
+                             "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
+                             "passes_merged_check_failed": tot["merged_fail"],
+                             "verdicts": "every call matches the sets' validity by construction"}
     finally:
         for c in ctxs:
             c.close()
@@ -622,9 +638,65 @@ def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int, per_call: 
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` with no launcher around it (WORLD_SIZE unset): start N rank
+    processes of this script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    rendezvous on 127.0.0.1), before anything in this process touches a GPU -- the
+    reference's pool splits the work across its workers the same way, one message per
+    worker (multithread/index.ts:153-166).  Rank 0 prints the JSON line; a rank that
+    fails stops the others; returns the worst exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    worst = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                worst = bad[0]
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                break
+            time.sleep(0.2)
+        for p in procs:
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return worst or next((p.returncode for p in procs if p.returncode), 0)
+
+
+def _stand_in(spec: str):
+    """--stand-in MODULE:FACTORY: a CPU object answering the GpuContext calls the job
+    modes make (tests/test_bench_jobs.py supplies one), so the rank launch and the
+    job modes run without a device.  Test infrastructure only; never the measurement."""
+    import importlib
+
+    mod, _, name = spec.partition(":")
+    return getattr(importlib.import_module(mod), name)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node, one rank each: launched here when no launcher set WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=1024)
@@ -665,21 +737,35 @@ def main() -> None:
     ap.add_argument("--table-keys", type=int, default=1 << 20, help="device pubkey table of the cfg3 / cfg4 records")
     ap.add_argument("--cfg4-sets", type=int, default=125_000,
                     help="sets of this GPU's cfg4 slice (1M sets over 8 GPUs by call)")
+    ap.add_argument("--cfg4-contexts", type=int, default=4, help="contexts of the cfg4 sub-record")
+    ap.add_argument("--cfg4-calls-per-pass", type=int, default=32, help="128-set calls per pass of the cfg4 sub-record")
     ap.add_argument("--no-merged-check", action="store_true",
                     help="one final exponentiation per chunk only (BLS_DEBUG_NO_MERGED_CHECK)")
+    ap.add_argument("--stand-in", default=None, metavar="MODULE:FACTORY",
+                    help="dry run of --mode cfg4 / cfg5 without a device: ranks on gloo, contexts from this CPU "
+                         "stand-in (tests only)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one rank per GPU, launched before this process touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != max(1, args.gpus):
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
     dist, device = None, None
     if world > 1:
-        import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        device = f"cuda:{local_rank}"
-        dist.init_process_group("nccl")
+        if args.stand_in:
+            dist.init_process_group("gloo")
+        else:
+            import torch
+
+            torch.cuda.set_device(local_rank)
+            device = f"cuda:{local_rank}"
+            dist.init_process_group("nccl")
 
     def barrier_sync():
         if dist is not None:
@@ -687,6 +773,18 @@ def main() -> None:
 
             dist.barrier()
             torch.cuda.synchronize()
+
+    if args.stand_in:
+        if args.mode not in ("cfg4", "cfg5"):
+            raise SystemExit("--stand-in runs the sharded-by-call job modes (cfg4, cfg5)")
+        factory = _stand_in(args.stand_in)
+        out = bench_job(args, [factory() for _ in range(args.inflight)], rank, world, dist, device, None)
+        out["data"] += "; DRY RUN: CPU stand-in contexts (--stand-in), not a measurement"
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK, DEBUG_NO_MSG_DEDUP, DEBUG_NO_UNITS
     from lodestar_amd.native import GpuContext
@@ -862,14 +960,11 @@ def main() -> None:
             pass_sets = args.sets * K
             kern = {}
             if agg:
-                simt = int(os.environ.get("BLS_ML_SIMT", "2") or 2)
-
                 def per_kernel(sh):  # Fp products per set of k_chain and the Miller loops
                     msm = bool(sh & 1) if sh is not None else os.environ.get("BLS_MSM", "0") == "1"
                     return {"k_chain": wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_pk"]
                             + (0.0 if msm else wm["chain_r_sig"]),
-                            "miller_loops": (wm["ml_lines"] + mlf_products(wm, sh))
-                            if simt == 2 else (wm["ml_simt"] if simt == 1 else None)}
+                            "miller_loops": wm["ml_lines"] + mlf_products(wm, sh)}
 
                 pk_timed, pk_solo = per_kernel(shape), per_kernel(solo_shape)
                 for name, fpm in pk_timed.items():
@@ -914,13 +1009,16 @@ def main() -> None:
             if world == 1 and not args.no_cpu_baseline and args.mode == "cfg2":
                 out["cpu_baseline"] = cpu_baseline(sets, raw96, seconds=args.cpu_seconds,
                                                    latency_runs=args.latency_runs)
-                out["cpu_baseline"]["gpu_over_whole_host"] = round(
-                    value / max(1e-9, out["cpu_baseline"]["whole_host_sets_per_s"]), 2)
+                out["cpu_baseline"]["gpu_over_measured_pool"] = round(value / max(1e-9, out["cpu_baseline"]["value"]), 2)
+                out["cpu_baseline"]["gpu_over_whole_host_extrapolated"] = round(
+                    value / max(1e-9, out["cpu_baseline"]["whole_host_sets_per_s_extrapolated"]), 2)
     for c in ctxs:
         c.close()
     ctxs = []
     if world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records:
-        out.update(sub_records(args.table_keys, inflight, K, args.cfg4_sets))
+        out.update(sub_records(args.table_keys, inflight, K, args.cfg4_sets, cfg4_ctx=args.cfg4_contexts,
+                               cfg4_cpp=args.cfg4_calls_per_pass, cfg5_sets=args.cfg5_sets,
+                               cfg5_roots=args.cfg5_roots))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

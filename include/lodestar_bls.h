@@ -89,10 +89,51 @@ int bls_gpu_init(int device, bls_gpu_ctx** out);
 /* The same with a stream priority: BLS_PRIORITY_HIGH puts the context's kernels ahead
  * of normal-priority contexts' queued work on the device -- the latency lane of
  * verifyOnMainThread calls (multithread/index.ts:138-151: the reference runs them on the
- * main thread, outside the worker queue).  BLS_PRIORITY_NORMAL = bls_gpu_init. */
+ * main thread, outside the worker queue).  BLS_PRIORITY_NORMAL = bls_gpu_init.
+ *
+ * Both admit a context only while the scratch the HIP runtime reserves for the
+ * process's contexts fits a budget (see bls_admission below); otherwise they return
+ * BLS_ERR_ADMISSION without creating anything, and bls_gpu_init_error() says why.  Any
+ * other failure returns -1 (-2 for bad arguments) with its message there too.  The
+ * reference's pool likewise records a worker that fails to start and keeps the others
+ * (multithread/index.ts:221-229). */
 #define BLS_PRIORITY_NORMAL 0
 #define BLS_PRIORITY_HIGH 1
+#define BLS_ERR_ADMISSION (-4)
 int bls_gpu_init_priority(int device, int priority, bls_gpu_ctx** out);
+
+/* Message of the last failed bls_gpu_init / bls_gpu_init_priority on the calling thread
+ * ("" after a successful one). */
+const char* bls_gpu_init_error(void);
+
+/* Scratch admission.  The HIP runtime backs each hardware queue with private-segment
+ * memory for a full device of the deepest kernel dispatched on it and aborts the queues
+ * (HSA_STATUS_ERROR_OUT_OF_RESOURCES, every call of the process failing) past ~8 GiB.
+ * A process's streams of one priority map onto at most GPU_MAX_HW_QUEUES hardware
+ * queues (HIP's default 4), per priority level, so
+ *   queues_in_use    = min(contexts_normal, hw_queues) + min(contexts_high, hw_queues)
+ *   scratch_reserved = queues_in_use x scratch_per_queue
+ * where scratch_per_queue is the deepest verify-path kernel's reservation (scratch
+ * bytes per lane x 64 x resident waves per SIMD x 1024 SIMDs, from the kernels' resource
+ * usage at build time; bls_scratch_worst_kernel names it).  A context is admitted while
+ * scratch_reserved <= scratch_budget (default 6 GiB; $BLS_SCRATCH_BUDGET_MIB or
+ * bls_gpu_set_scratch_budget). */
+typedef struct bls_admission {
+  uint32_t contexts_normal, contexts_high; /* open contexts on the device */
+  uint32_t hw_queues;                      /* GPU_MAX_HW_QUEUES (4 when unset) */
+  uint32_t queues_in_use;
+  uint64_t scratch_per_queue, scratch_reserved, scratch_budget; /* bytes */
+} bls_admission;
+
+/* The accounting alone (no device needed): 0 if n_normal + n_high contexts are
+ * admissible with hw_queues hardware queues per priority (0 = $GPU_MAX_HW_QUEUES), else
+ * BLS_ERR_ADMISSION; *out (nullable) receives the figures. */
+int bls_scratch_plan(uint32_t n_normal, uint32_t n_high, uint32_t hw_queues, bls_admission* out);
+/* The figures for the contexts open on `device` now. */
+int bls_gpu_admission(int device, bls_admission* out);
+const char* bls_scratch_worst_kernel(void);
+/* Override the budget for this process (0 restores the default / environment). */
+void bls_gpu_set_scratch_budget(uint64_t bytes);
 
 /* Release device memory and streams (IBlsVerifier.close, index.ts:176-197). */
 void bls_gpu_close(bls_gpu_ctx* ctx);

@@ -94,6 +94,29 @@ async function main() {
   out.inflight_at_close = inflight;
   const q = await Promise.all(queued);
   out.closed = q.find((x) => x !== "resolved" && x !== true) || "none";
+  // libuv pool warning against a stand-in pool of 4 threads (3 contexts + 2 > 4)
+  const warnings = [];
+  const w = new GpuBlsVerifier({contexts: 3, addon: fake, uvThreadpoolSize: 4, warn: (m) => warnings.push(m)});
+  await w.close();
+  out.pool_warning = warnings[0] || null;
+  // scratch admission: the library refuses pool contexts past its budget (BLS_ERR_ADMISSION)
+  const refusing = (admit) => Object.assign({}, fake, {
+    init: (dev, high) => {
+      if (!high && admit-- <= 0) {
+        const e = Error("BLS_ERR_ADMISSION: stand-in refusal");
+        e.code = "BLS_ERR_ADMISSION";
+        throw e;
+      }
+      return fake.init(dev, high);
+    },
+  });
+  const part = new GpuBlsVerifier({contexts: 3, addon: refusing(1), uvThreadpoolSize: 64});
+  out.admitted_partial = {ctxs: part.ctxs.length, errors: part.initErrors.length,
+                          verdict: await part.verifySignatureSets([sets[1]], {batchable: false})};
+  await part.close();
+  const none = new GpuBlsVerifier({contexts: 2, addon: refusing(0), uvThreadpoolSize: 64});
+  out.admitted_none = await none.verifySignatureSets([sets[1]], {batchable: true}).then(() => "resolved", (e) => e.message);
+  await none.close();
   console.log(JSON.stringify(out));
 }
 

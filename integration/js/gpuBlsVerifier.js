@@ -16,9 +16,18 @@
  * the main thread outside the worker queue (index.ts:138-151), so they never wait
  * behind a pool call here either.  Each context runs its calls on a libuv worker
  * (napi_async_work): the process needs UV_THREADPOOL_SIZE >= contexts + 2 (pool
- * contexts, the main-thread lane, one spare), set in the environment before Node
- * starts; this module sets 18 when it is unset (enough for 16 contexts), which takes
- * effect only if nothing used the libuv pool yet.
+ * contexts, the main-thread lane, one spare), set in the environment BEFORE Node starts
+ * (libuv sizes its pool once, when anything first uses it -- any fs call of a beacon
+ * node does, long before this module loads -- so setting it from JS is too late).  The
+ * constructor warns when the pool the process started with (UV_THREADPOOL_SIZE at
+ * module load, libuv's 4 when unset) is smaller than contexts + 2.
+ *
+ * Contexts: the library admits a context only while the HIP runtime's scratch for the
+ * process's contexts fits its budget (bls_gpu_init_priority, BLS_ERR_ADMISSION).  As the
+ * reference's pool keeps the workers that started and records the others
+ * (multithread/index.ts:221-229), a refused or failed pool context is recorded in
+ * `initErrors` and the pool runs on the rest; when none started, queued work rejects
+ * with the first error (index.ts:247-253).  The main-thread lane is opened first.
  *
  * A signature set is {pubkeyIndices: number[]} (indices into the device pubkey
  * table loaded with loadPubkeys, i.e. index2pubkey) or {pubkey: Uint8Array(96)}
@@ -31,8 +40,8 @@ const path = require("path");
 
 const ADDON_PATH = path.join(__dirname, "..", "..", "lodestar_amd", "_native", "lodestar_bls.node");
 let defaultAddon = null;
-// libuv reads this when its pool first starts (see the header comment)
-if (!process.env.UV_THREADPOOL_SIZE) process.env.UV_THREADPOOL_SIZE = "18";
+// the libuv pool this process started with (see the header comment): read, never written
+const UV_POOL_AT_LOAD = Number(process.env.UV_THREADPOOL_SIZE || 4);
 let warnedPoolSize = false;
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:39
@@ -145,16 +154,24 @@ class GpuBlsVerifier {
     // the N-API addon (opts.addon: a stand-in with the same four functions, for host-side tests)
     this.addon = opts.addon || (defaultAddon = defaultAddon || require(ADDON_PATH));
     const addon = this.addon;
-    this.ctxs = [];
-    // `inflight`: calls queued or running on the context (at most one pool call each)
-    for (let i = 0; i < contexts; i++) this.ctxs.push({handle: addon.init(device, false), inflight: 0, id: i});
-    // the main-thread lane: its own high-priority context, never used by the pool
+    // the main-thread lane first: its own high-priority context, never used by the pool
     this.mainCtx = {handle: addon.init(device, true), inflight: 0, id: "main"};
-    const uvSize = Number(process.env.UV_THREADPOOL_SIZE || 4);
-    if (!opts.addon && contexts + 2 > uvSize && !warnedPoolSize) {
+    this.ctxs = [];
+    this.initErrors = [];
+    // `inflight`: calls queued or running on the context (at most one pool call each)
+    for (let i = 0; i < contexts; i++) {
+      try {
+        this.ctxs.push({handle: addon.init(device, false), inflight: 0, id: this.ctxs.length});
+      } catch (e) {
+        this.initErrors.push(e); // a worker that failed to start (index.ts:221-229)
+      }
+    }
+    const uvSize = opts.uvThreadpoolSize || UV_POOL_AT_LOAD;
+    const warn = opts.warn || ((m) => console.warn(m));
+    if (this.ctxs.length + 2 > uvSize && (opts.warn || !warnedPoolSize)) {
       warnedPoolSize = true;
-      console.warn(`GpuBlsVerifier: UV_THREADPOOL_SIZE=${uvSize} < contexts + 2 = ${contexts + 2}; ` +
-        "GPU calls will queue for libuv threads (set it in the environment before starting node)");
+      warn(`GpuBlsVerifier: the libuv pool has ${uvSize} threads < contexts + 2 = ${this.ctxs.length + 2}; ` +
+        "GPU calls will queue for libuv threads (set UV_THREADPOOL_SIZE in the environment before starting node)");
     }
     this.jobs = []; // queue: jobs[jobsHead..] are pending
     this.jobsHead = 0;
@@ -228,16 +245,17 @@ class GpuBlsVerifier {
   }
 
   /** verifySignatureSet over many sets in one GPU call (e.g. every inline check of a
-   * block when batch verification is off): per set a boolean, or the Error its own
-   * verifySignatureSet would throw (a signature that does not decode) -- one bad set
-   * does not hide the other sets' verdicts (lodestar_amd/stf.py returns the same). */
+   * block when batch verification is off): per set {valid: boolean, error?: Error} --
+   * valid is false with the Error its own verifySignatureSet would throw when the
+   * signature does not decode, so a truthiness check of `valid` can never pass it; one
+   * bad set does not hide the other sets' verdicts (lodestar_amd/stf.py likewise). */
   verifySignatureSetsEachSync(sets) {
     const v = this.addon.verifySync(this.mainCtx.handle, packRequests(sets.map((s) => ({batchable: false, sets: [s]}))));
     return sets.map((_, i) => {
       try {
-        return this._settle(v, i);
+        return {valid: this._settle(v, i)};
       } catch (e) {
-        return e;
+        return {valid: false, error: e};
       }
     });
   }
@@ -289,6 +307,8 @@ class GpuBlsVerifier {
   /** queueBlsWork (index.ts:238-285) */
   _queue(workReq) {
     if (this.closed) return Promise.reject(Error("QUEUE_ABORTED"));
+    // every pool context failed to start: the first error (index.ts:247-253)
+    if (this.ctxs.length === 0 && this.initErrors.length > 0) return Promise.reject(this.initErrors[0]);
     return new Promise((resolve, reject) => {
       // the job is its own BlsWorkReq ({batchable, sets}) plus the promise handlers
       const job = {resolve, reject, batchable: workReq.batchable, sets: workReq.sets,

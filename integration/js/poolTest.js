@@ -58,7 +58,10 @@ async function main() {
       return e.message;
     }
   });
-  out.stfEach = pool.verifySignatureSetsEachSync([sets[0], wrong, sets[2]]);
+  const each = pool.verifySignatureSetsEachSync([sets[0], wrong, sets[2], invalid]);
+  out.stfEach = each.map((r) => r.valid);
+  // an undecodable set is never truthy (ADVICE r3: a mixed boolean / Error array was)
+  out.stfEachInvalid = [Boolean(each[3].valid), each[3].error ? each[3].error.message : null];
   await pool.close();
   assert.ok(true);
   console.log(JSON.stringify(out));

@@ -3,7 +3,8 @@
  * `GpuBlsVerifier` (integration/js/gpuBlsVerifier.js) loads in place of the
  * @chainsafe/blst worker pool (beacon-node/src/chain/bls/multithread/index.ts).
  *
- *   init(device, highPriority?) -> handle   (highPriority: bls_gpu_init_priority HIGH)
+ *   init(device, highPriority?) -> handle   (highPriority: bls_gpu_init_priority HIGH; throws an
+ *          Error with code "BLS_ERR_ADMISSION" when the scratch admission refuses the context)
  *   loadPubkeys(handle, Uint8Array pks, pkLen) -> Int32Array codes
  *   verify(handle, {reqSetOffsets, reqBatchable, messages, signatures,
  *                   setPkOffsets?, pkIndices?, pubkeys?, signatureLens?, seed?})
@@ -83,8 +84,15 @@ static napi_value js_init(napi_env env, napi_callback_info info) {
     if (t == napi_boolean) CHECK(env, napi_get_value_bool(env, argv[1], &high));
   }
   bls_gpu_ctx* ctx = NULL;
-  if (bls_gpu_init_priority(dev, high ? BLS_PRIORITY_HIGH : BLS_PRIORITY_NORMAL, &ctx) != 0 || !ctx) {
-    napi_throw_error(env, NULL, "bls_gpu_init failed (no HIP device?)");
+  const int rc = bls_gpu_init_priority(dev, high ? BLS_PRIORITY_HIGH : BLS_PRIORITY_NORMAL, &ctx);
+  if (rc != 0 || !ctx) {
+    /* the library's reason; error.code "BLS_ERR_ADMISSION" when the scratch admission
+     * refused the context (the adapter then runs on the contexts it has, as the reference
+     * pool keeps the workers that started, multithread/index.ts:221-229) */
+    const char* why = bls_gpu_init_error();
+    char msg[600];
+    snprintf(msg, sizeof(msg), "%s", why && *why ? why : "bls_gpu_init failed (no HIP device?)");
+    napi_throw_error(env, rc == BLS_ERR_ADMISSION ? "BLS_ERR_ADMISSION" : "BLS_ERR_INIT", msg);
     return NULL;
   }
   bls_handle* h = (bls_handle*)calloc(1, sizeof(bls_handle));

@@ -64,7 +64,13 @@ SYMBOLS = (
     "bls_gpu_coop_probe",
     "bls_gpu_kernel_probe",
     "bls_gpu_set_debug_flags",
+    "bls_gpu_init_error",
+    "bls_scratch_plan",
+    "bls_gpu_admission",
+    "bls_scratch_worst_kernel",
+    "bls_gpu_set_scratch_budget",
 )
+ERR_ADMISSION = -4  # BLS_ERR_ADMISSION: the context would push the runtime's scratch past the budget
 # SSZ kinds of bls_gpu_ssz_roots (low 8 bits: serialized size)
 SSZ_ROOT = 0x000 | 32
 SSZ_UINT64 = 0x100 | 8
@@ -107,6 +113,18 @@ class BlsBatch(ctypes.Structure):
         ("signatures", ctypes.c_void_p),
         ("signature_lens", ctypes.c_void_p),
         ("seed", ctypes.c_void_p),
+    ]
+
+
+class BlsAdmission(ctypes.Structure):
+    _fields_ = [
+        ("contexts_normal", ctypes.c_uint32),
+        ("contexts_high", ctypes.c_uint32),
+        ("hw_queues", ctypes.c_uint32),
+        ("queues_in_use", ctypes.c_uint32),
+        ("scratch_per_queue", ctypes.c_uint64),
+        ("scratch_reserved", ctypes.c_uint64),
+        ("scratch_budget", ctypes.c_uint64),
     ]
 
 
@@ -178,6 +196,16 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_gpu_kernel_probe.restype = i32
         lib.bls_gpu_set_debug_flags.argtypes = [vp, u32]
         lib.bls_gpu_set_debug_flags.restype = i32
+        lib.bls_gpu_init_error.argtypes = []
+        lib.bls_gpu_init_error.restype = ctypes.c_char_p
+        lib.bls_scratch_plan.argtypes = [u32, u32, u32, ctypes.POINTER(BlsAdmission)]
+        lib.bls_scratch_plan.restype = i32
+        lib.bls_gpu_admission.argtypes = [i32, ctypes.POINTER(BlsAdmission)]
+        lib.bls_gpu_admission.restype = i32
+        lib.bls_scratch_worst_kernel.argtypes = []
+        lib.bls_scratch_worst_kernel.restype = ctypes.c_char_p
+        lib.bls_gpu_set_scratch_budget.argtypes = [ctypes.c_uint64]
+        lib.bls_gpu_set_scratch_budget.restype = None
     return lib
 
 

@@ -11,6 +11,7 @@ import concurrent.futures as cf
 import hashlib
 import json
 import os
+import re
 import subprocess
 import sys
 from pathlib import Path
@@ -39,24 +40,22 @@ def sources() -> list[Path]:
 
 
 # A/B build variants: extra defines -> lodestar_amd/_native/liblodestar_bls_<name>.so
-VARIANTS = {"mul32": ["-DBLS_FP_MUL32", "-DBLS_CHAIN_INL32"], "chain_inl32": ["-DBLS_CHAIN_INL32"],
-            "chain_occ1": ["-DBLS_CHAIN_OCC1"], "chain_occ3": ["-DBLS_CHAIN_OCC3"],
-            "chain_binr": ["-DBLS_CHAIN_BINARY_R"], "chain_w4": ["-DBLS_CHAIN_W4"],
-            "chain_inl28": ["-DBLS_CHAIN_INL28"], "fp2fused": ["-DBLS_FP2_FUSED"], "fips": ["-DBLS_FP_FIPS"], "cios": ["-DBLS_FP_CIOS"],
-            "noprio": ["-DBLS_NO_TAIL_PRIO"], "fp2eager": ["-DBLS_FP2_EAGER"],
-            "mlf_single": ["-DBLS_MLF_SINGLE_LINES"]}
+# (the round-3 variants that lost were removed from the sources; their A/B records stay
+# under profiles/r03_ab_*.json)
+VARIANTS: dict[str, list[str]] = {}
 
 
-# Scratch budget (the guard against the round-2 "kernel never finished"): the HIP runtime
-# backs each hardware queue with scratch for a full device of the kernel's wavefronts,
-# scratch bytes/lane x 64 x resident waves (occupancy x 1024 SIMDs), and past ~8 GiB over
-# the queues in use it aborts the queue with HSA_STATUS_ERROR_OUT_OF_RESOURCES
-# (profiles/r03_scratch_out_of_resources.txt: 4,160 B/lane at 2 waves/SIMD, 16 contexts).
-# The verify path runs up to 16 contexts (queues), so a kernel it launches may reserve at
-# most 8 GiB / 16 = 512 MiB; the build refuses one that needs more.
-SCRATCH_BUDGET = 512 << 20
+# Scratch: the HIP runtime backs each hardware queue with scratch for a full device of the
+# deepest kernel dispatched on it, scratch bytes/lane x 64 x resident waves (occupancy x
+# 1024 SIMDs), and past ~8 GiB over the queues in use it aborts them with
+# HSA_STATUS_ERROR_OUT_OF_RESOURCES (profiles/r03_scratch_out_of_resources.txt).  The
+# library admits contexts at run time against that (bls_gpu_init_priority, the
+# per-queue figure baked in as BLS_SCRATCH_PER_QUEUE from the kernels compiled here:
+# scratch_per_queue()).  The build refuses a kernel whose reservation alone would leave
+# room for fewer than MIN_QUEUES queues within the default 6 GiB admission budget.
+ADMISSION_BUDGET = 6 << 30
+MIN_QUEUES = 4
 SIMDS = 1024
-FIXTURE_KERNELS = ("k_sign", "k_sk_to_pk", "k_probe_")  # input synthesis / probes, one context
 
 
 def _resources(remarks: str) -> list[dict]:
@@ -84,12 +83,22 @@ def _resources(remarks: str) -> list[dict]:
 
 
 def _check_scratch(src: Path, kernels: list[dict]) -> None:
+    cap = ADMISSION_BUDGET // MIN_QUEUES
     for k in kernels:
-        if k["device_scratch_bytes"] > SCRATCH_BUDGET and not any(f in k["name"] for f in FIXTURE_KERNELS):
+        if k["device_scratch_bytes"] > cap:
             raise SystemExit(f"{src.name}: kernel {k['name']} reserves {k['device_scratch_bytes'] >> 20} MiB of "
                              f"scratch per queue ({k.get('scratch')} B/lane x 64 x {k.get('occupancy')} waves/SIMD "
-                             f"x {SIMDS} SIMDs) > {SCRATCH_BUDGET >> 20} MiB: the runtime aborts queues past ~8 GiB "
-                             "over 16 contexts (lodestar_amd/build.py SCRATCH_BUDGET)")
+                             f"x {SIMDS} SIMDs) > {cap >> 20} MiB: fewer than {MIN_QUEUES} contexts would fit the "
+                             "runtime's ~8 GiB (lodestar_amd/build.py ADMISSION_BUDGET)")
+
+
+def scratch_per_queue(table: list[dict]) -> tuple[int, str]:
+    """The deepest kernel's per-queue reservation (bytes) and its name: what a context's
+    queue may have to hold (any kernel of the library can run on a context's stream)."""
+    worst = max(table, key=lambda k: k["device_scratch_bytes"])
+    m = re.match(r"_Z(\d+)", worst["name"])  # the kernel's plain name from its mangled one
+    name = worst["name"][m.end(): m.end() + int(m.group(1))] if m else worst["name"]
+    return worst["device_scratch_bytes"], name
 
 
 def _compile(src: Path, hdr: str, verbose: bool, extra: list[str] | None = None) -> Path:
@@ -163,11 +172,17 @@ def build(jobs: int | None = None, verbose: bool = True, variant: str | None = N
     extra = VARIANTS[variant] if variant else None
     lib = OUT_DIR / f"liblodestar_bls_{variant}.so" if variant else LIB
     jobs = jobs or min(len(srcs), os.cpu_count() or 4)
+    # the kernels first: their resource usage sets the host TU's admission figure
+    kern_srcs, host_src = srcs[1:], srcs[0]
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdr, verbose, extra), srcs))
+        kobjs = list(ex.map(lambda s: _compile(s, hdr, verbose, extra), kern_srcs))
+    table = [dict(k, tu=o.stem.split(".")[0]) for o in kobjs for k in json.loads(o.with_suffix(".res.json").read_text())]
+    per_queue, worst = scratch_per_queue(table)
+    host_extra = (extra or []) + [f"-DBLS_SCRATCH_PER_QUEUE={per_queue}ull", f'-DBLS_SCRATCH_WORST_KERNEL="{worst}"']
+    objs = [_compile(host_src, hdr, verbose, host_extra)] + kobjs
     if not variant:  # every kernel's registers, occupancy and scratch reservation, for the record
-        table = [dict(k, tu=o.stem.split(".")[0]) for o in objs for k in json.loads(o.with_suffix(".res.json").read_text())]
-        (OUT_DIR / "kernel_resources.json").write_text(json.dumps(table, indent=1))
+        (OUT_DIR / "kernel_resources.json").write_text(json.dumps(
+            {"scratch_per_queue": per_queue, "scratch_worst_kernel": worst, "kernels": table}, indent=1))
     stamp = hashlib.sha256("".join(str(o) for o in objs).encode()).hexdigest()
     stamp_file = OUT_DIR / (f".lib_stamp_{variant}" if variant else ".lib_stamp")
     if lib.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:

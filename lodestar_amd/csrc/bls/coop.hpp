@@ -61,9 +61,6 @@ struct CoopLdsN {
 #define COOP_FRAME2 380  // the 2-set packed programs (tools/gen_coop.py FRAME2): with the
                          // 40-constant bank 20.2 KB of LDS, 8 blocks = 2 wavefronts per SIMD
 #define COOP_FRAME3 640  // the 3-set packed programs (tools/gen_coop.py FRAME3)
-#define COOP_FRAME4S 288  // the shared 4-pair Miller loop ml1s_4 (tools/gen_coop.py FRAME4S):
-                          // 15.7 KB with the bank, 10 wavefronts per CU (k_mlns<4>)
-#define COOP_FRAME8S 512  // the shared 8-pair loop ml1s_8 (FRAME8S): 26.5 KB, 6 per CU
 
 // Programs of S sets packed in one wavefront (tools/gen_pset.py build_pset(S)):
 // add[(xb << S) | rmask], bit s of rmask = r bit of packed set s; add[0] unused
@@ -81,11 +78,9 @@ struct CoopEnv {
   CoopProg pset_prep, pset_dbl_r, pset_dbl_all, pset_add_x, pset_add_r, pset_add_xr, pset_phase2, pset_norm2,
       pset_affine2, pset_ml2;
   CoopPsetN packed[2];  // [0]: 2 sets per wavefront, [1]: 3 sets
-  // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln):
-  // 1 or 2 sets per wavefront (COOP_FRAME), 4 sets (COOP_FRAME2)
-  CoopProg ml1_1, ml1_2, ml1_4;
-  CoopProg ml1s_4;  // four pairs of one product domain sharing f (build_ml1_shared)
-  CoopProg ml1s_8;  // eight pairs sharing f (kernels/k_pset.hip k_mlns<8>)
+  // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln, the
+  // cooperative packings tests force): 1 or 2 sets per wavefront (COOP_FRAME)
+  CoopProg ml1_1, ml1_2;
 };
 
 // fin frame registers
@@ -392,12 +387,6 @@ __device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* fra
 __device__ __forceinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
                                          uint32_t* flag) {
   coop_run_t<false>(env, pg, frame, cbank, flag, nullptr);
-}
-
-// Inlined into the kernel, so the kernel's own occupancy attribute
-// (amdgpu_waves_per_eu) bounds the interpreter's registers (kernels/k_pset.hip k_mlns)
-__device__ __forceinline__ void coop_run_inline(const CoopEnv& env, CoopProg pg, Fp* frame, uint32_t* flag) {
-  coop_run_body<false>(env, pg, frame, flag, nullptr);
 }
 
 // copy the constant bank into LDS (once per block)

@@ -164,8 +164,9 @@ BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
   return r;
 }
 
-// Unreduced forms for a product's operands only (the column product takes inputs < 3p,
-// test_hostsim.py::test_fp_mul_fips): a + b < 2p and a + p - b in (0, 2p] for a, b < p
+// Unreduced forms for a product's operands only (the 28-bit-digit product takes inputs
+// < 3p, test_hostsim.py::test_fp_mul_d28_lazy): a + b < 2p and a + p - b in (0, 2p]
+// for a, b < p
 BLS_HD Fp fp_add_nr(const Fp& a, const Fp& b) {
   Fp s;
   asm_add12(s.l, a.l, b.l);
@@ -434,112 +435,6 @@ BLS_HD Fp fp_mul_d28_lazy(const Fp& a, const Fp& b) {
 #pragma unroll
     for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)x[i] * y[j];
   return fp_redc_d28(t);
-}
-
-// The same product in product-scanning (FIPS) order with the reduction interleaved:
-// column k takes its a b and m p terms, and the column's m_k (k < 14) from its low
-// digit, so only the digits of a, b, m and one 64-bit column are live (~50 VGPRs
-// instead of ~130 for 27 columns at once).  Out of line, the product's register
-// footprint is what its callers must keep clear around every call (the compiler's
-// interprocedural register allocation): k_chain's G2 chains spill around the calls.
-// Result: (t + m p) / 2^384 with R = 2^(13*28 + 20): column 13's carry starts at result
-// bit 0 (after its low 20 bits), column k >= 14 at bit 8 + 28 (k - 14).  Inputs < 3p,
-// output < 2p.  tests: test_hostsim.py::test_fp_mul_fips.
-template <bool SQR>
-BLS_HD Fp fp_mul_fips(const Fp& a, const Fp& b) {
-  uint32_t x[14], y[14], m[14];
-  fp_to_d28(a, x);
-  if (SQR) {
-#pragma unroll
-    for (int k = 0; k < 14; ++k) y[k] = x[k];
-  } else {
-    fp_to_d28(b, y);
-  }
-  // per column: the a b terms and the m p terms of digits already known are summed
-  // off the critical path (two independent chains), then the carry in, m_{k-1} p_1 and
-  // m_k p_0 -- only those three are serial between columns
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 14; ++k) {
-    uint64_t s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i <= k; ++i) {
-      if (i & 1) s1 += (uint64_t)x[i] * y[k - i];
-      else s0 += (uint64_t)x[i] * y[k - i];
-    }
-#pragma unroll
-    for (int i = 0; i + 1 < k; ++i) {
-      if (i & 1) s1 += (uint64_t)m[i] * p28_digit(k - i);
-      else s0 += (uint64_t)m[i] * p28_digit(k - i);
-    }
-    acc += s0 + s1;
-    if (k > 0) acc += (uint64_t)m[k - 1] * p28_digit(1);
-    const uint32_t mask = k < 13 ? BLS_D28_MASK : 0xFFFFFu;
-    m[k] = ((uint32_t)acc * BLS_NP28) & mask;
-    acc += (uint64_t)m[k] * p28_digit(0);
-    if (k < 13) acc >>= 28;  // column k is 0 mod 2^28
-  }
-  // column 13 is 0 mod 2^20: the result starts at its bit 20
-  acc >>= 20;
-  const uint32_t low8 = (uint32_t)acc & 0xFFu;
-  acc >>= 8;  // now in units of 2^8, the weight of column 14
-  uint32_t e[14];
-#pragma unroll
-  for (int k = 14; k < 27; ++k) {
-    uint64_t s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = k - 13; i < 14; ++i) {
-      s0 += (uint64_t)x[i] * y[k - i];
-      s1 += (uint64_t)m[i] * p28_digit(k - i);
-    }
-    acc += s0 + s1;
-    e[k - 14] = (uint32_t)acc & BLS_D28_MASK;
-    acc >>= 28;
-  }
-  e[13] = (uint32_t)acc;  // < 2^(383 - 8 - 364) bits
-  // pack low8 + sum e_j 2^(8 + 28 j) into 12 x 32-bit limbs
-  Fp r;
-  uint64_t w = low8;
-  int nb = 8, li = 0;
-#pragma unroll
-  for (int j = 0; j < 14; ++j) {
-    w |= (uint64_t)e[j] << nb;
-    nb += 28;
-    while (nb >= 32 && li < 12) {
-      r.l[li++] = (uint32_t)w;
-      w >>= 32;
-      nb -= 32;
-    }
-  }
-  while (li < 12) {
-    r.l[li++] = (uint32_t)w;
-    w >>= 32;
-  }
-  return r;
-}
-
-// The same product with the reduction interleaved row by row (CIOS): row i adds x_i y
-// into columns i..i+13, then m_i p, and carries column i into i+1 -- only ~15 columns
-// are live at once (~70 VGPRs instead of ~130), and each row's 14 multiply-adds are
-// independent (the column product's ILP).  Same output as fp_mul_d28_lazy.
-// tests: test_hostsim.py::test_fp_mul_fips.
-BLS_HD Fp fp_mul_cios(const Fp& a, const Fp& b) {
-  uint32_t x[14], y[14];
-  fp_to_d28(a, x);
-  fp_to_d28(b, y);
-  uint64_t t[27];
-#pragma unroll
-  for (int k = 0; k < 27; ++k) t[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-#pragma unroll
-    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)x[i] * y[j];
-    const uint32_t m = ((uint32_t)t[i] * BLS_NP28) & (i < 13 ? BLS_D28_MASK : 0xFFFFFu);
-#pragma unroll
-    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)m * p28_digit(j);
-    if (i < 13) t[i + 1] += t[i] >> 28;  // column i is now 0 mod 2^28
-  }
-  return fp_d28_tail(t);
 }
 
 // squaring: 14 squares + 91 cross products against doubled digits (< 2^29)
@@ -823,23 +718,15 @@ __device__ __forceinline__ Fp fp_sqr_cols(const Fp& a) {
 #endif
 // BLS_FP_D28 (a kernel TU that defines it before the includes): the 28-bit-digit
 // product (fp_mul_d28_lazy: ~580 VALU instructions instead of ~740 plus wait states,
-// ~20 % lower latency per product on gfx950).  Opted into by k_pre, the cooperative
-// interpreter kernels and k_chain (out of line there: inlined into its 512-VGPR chains
-// it compiled to a kernel that never finished on gfx950, ROCm 7.2, BLS_DEBUG_SYNC);
-// the other point-chain kernels keep the 32-bit-digit product.
-// BLS_FP_MUL32 (build variant mul32) forces the 32-bit-digit product everywhere.
-#if !defined(BLS_FP_D28) || defined(BLS_FP_MUL32)
+// ~20 % lower latency per product on gfx950), out of line.  Opted into by k_pre, the
+// cooperative interpreter kernels, k_chain, the Miller loops and the MSM; the other
+// point-chain kernels keep the 32-bit-digit column product.  (Product-scanning and
+// row-interleaved orders of the 28-bit product measured 3-8 % slower,
+// profiles/r03_ab_product_order.json.)
+#if !defined(BLS_FP_D28)
 BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_sqr_cols(a); }
 __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul_cols<false>(a, b); }
 __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cols<true>(a, b); }
-#elif defined(BLS_FP_FIPS)
-BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_mul_fips<true>(a, a)); }
-__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_fips<false>(a, b)); }
-__device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_fips<false>(a, b); }
-#elif defined(BLS_FP_CIOS)
-BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_mul_cios(a, a)); }
-__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_cios(a, b)); }
-__device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_mul_cios(a, b); }
 #else
 BLS_FP_MUL_ATTR Fp fp_sqr_dev(Fp a) { return fp_reduce_once(fp_sqr_d28_lazy(a)); }
 __device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_mul_d28_lazy(a, b)); }
@@ -858,16 +745,6 @@ __device__ __forceinline__ Fp fp_mul_lazy(const Fp& a, const Fp& b) { return fp_
 BLS_FP_MUL_ATTR Fp fp_mul_w(BLS_W12(a), BLS_W12(b)) { return fp_mul_inl(BLS_FP_OF(a), BLS_FP_OF(b)); }
 BLS_FP_MUL_ATTR Fp fp_sqr_w(BLS_W12(a)) { return fp_sqr_dev(BLS_FP_OF(a)); }
 __device__ __forceinline__ Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_w(BLS_L12(a), BLS_L12(b)); }
-#if defined(BLS_FP_D28) && !defined(BLS_FP_MUL32) && defined(BLS_FP2_FUSED)
-// the lazy Fp2 product and square out of line (build variant fp2fused: 48 words, 32 in
-// v0-v31 and 16 on the stack; the callee spans ~210 VGPRs, which its callers then spill
-// around every call: 2.62M vs 3.12M sets/s at 12 x 16, profiles/r03_ab_fp2_lazy.json)
-BLS_FP_MUL_ATTR Fp2 fp2_mul_w(BLS_W12(a), BLS_W12(c), BLS_W12(b), BLS_W12(d)) {
-  return fp2_mul_d28(BLS_FP_OF(a), BLS_FP_OF(c), BLS_FP_OF(b), BLS_FP_OF(d));
-}
-#define BLS_FP2_MUL_FUSED 1
-BLS_FP_MUL_ATTR Fp2 fp2_sqr_w(BLS_W12(a), BLS_W12(c)) { return fp2_sqr_d28(BLS_FP_OF(a), BLS_FP_OF(c)); }
-#endif
 #else
 // Host build: Montgomery product a*b/R mod p (R = 2^384) over 6 x 64-bit words,
 // separated operand scanning (the 36 partial products of a*b first, then the word-by-
@@ -1212,33 +1089,19 @@ BLS_HD Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
 BLS_HD Fp2 fp2_half(const Fp2& a) { return Fp2{fp_half(a.c0), fp_half(a.c1)}; }
 BLS_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& b) { return Fp2{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 
+// Karatsuba with unreduced pre-additions (operands < 2p; reduced ones measured 3 % slower
+// at the plateau, profiles/r03_ab_fp2_preadd.json)
 BLS_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
-#ifdef BLS_FP2_MUL_FUSED
-  return fp2_mul_w(BLS_L12(a.c0), BLS_L12(a.c1), BLS_L12(b.c0), BLS_L12(b.c1));
-#endif
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
-#ifdef BLS_FP2_EAGER  // build variant fp2eager: reduced pre-additions (A/B)
-  Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-#else
   Fp t2 = fp_mul(fp_add_nr(a.c0, a.c1), fp_add_nr(b.c0, b.c1));  // operands < 2p
-#endif
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
 BLS_HD Fp2 fp2_sqr(const Fp2& a) {
-#ifdef BLS_FP2_MUL_FUSED
-  return fp2_sqr_w(BLS_L12(a.c0), BLS_L12(a.c1));
-#endif
-#ifdef BLS_FP2_EAGER
-  Fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  Fp t1 = fp_mul(a.c0, a.c1);
-  return Fp2{t0, fp_dbl(t1)};
-#else
   Fp t0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub_nr(a.c0, a.c1));  // operands < 2p
   Fp t1 = fp_mul(fp_add_nr(a.c0, a.c0), a.c1);                   // 2 a0 a1
   return Fp2{t0, t1};
-#endif
 }
 
 // a * (1 + u)

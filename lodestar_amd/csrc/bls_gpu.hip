@@ -18,6 +18,7 @@
 // All kernels of a call run on the context's stream; the host waits twice
 // (chunk verdicts, final verdicts).
 #include <hip/hip_runtime.h>
+#include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/random.h>
@@ -65,6 +66,7 @@ struct bls_gpu_ctx {
   // one call at a time per context: every entry point that touches the stream,
   // workspace or table holds this (callers may share a context across threads)
   std::mutex* mu;
+  int admitted;  // counted by the scratch admission (bls_scratch_plan): 0 no, 1 normal, 2 high priority
 };
 
 #define CTX_LOCK(ctx) std::lock_guard<std::mutex> ctx_guard_(*(ctx)->mu)
@@ -237,8 +239,7 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
               {"pset_add_xr", &ctx->coop.pset_add_xr},   {"pset_phase2", &ctx->coop.pset_phase2},
               {"pset_norm2", &ctx->coop.pset_norm2},     {"pset_affine2", &ctx->coop.pset_affine2},
               {"pset_ml2", &ctx->coop.pset_ml2},         {"ml1_1", &ctx->coop.ml1_1},
-              {"ml1_2", &ctx->coop.ml1_2},               {"ml1_4", &ctx->coop.ml1_4},
-              {"ml1s_4", &ctx->coop.ml1s_4},             {"ml1s_8", &ctx->coop.ml1s_8}};
+              {"ml1_2", &ctx->coop.ml1_2}};
   ctx->coop_progs = new std::vector<std::pair<std::string, CoopProg>>();
   for (uint32_t k = 0; k < h.n_progs; ++k) {
     CoopProgEntry e;
@@ -305,7 +306,86 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
 static std::atomic<uint64_t> g_sets_in_flight{0};
 uint64_t bls_sets_in_flight() { return g_sets_in_flight.load(std::memory_order_relaxed); }
 
+// ---------------------------------------------------------------------------
+// Scratch admission.  The HIP runtime backs every hardware queue with private-segment
+// (scratch) memory for a full device of the deepest kernel dispatched on it, and past
+// ~8 GiB over the queues in use it aborts them with HSA_STATUS_ERROR_OUT_OF_RESOURCES:
+// every call in flight in the process fails and later calls too
+// (profiles/r03_scratch_out_of_resources.txt; 16 queues at 464 MiB ran, 16 at 520 MiB
+// and 20 at 456 MiB aborted).  So a context is admitted only while the queues its
+// contexts map onto, times the deepest verify-path kernel's reservation (baked at build
+// time from the kernels' resource usage, lodestar_amd/build.py), fit a budget; otherwise
+// bls_gpu_init_priority returns BLS_ERR_ADMISSION with a message, as the reference's pool
+// records a worker that failed to start (multithread/index.ts:221-229) and fails queued
+// work only when every worker failed (:247-253).
+//   queues in use: HIP maps a process's streams of one priority onto at most
+//   GPU_MAX_HW_QUEUES hardware queues (default 4), per priority level.
+// ---------------------------------------------------------------------------
+#ifndef BLS_SCRATCH_PER_QUEUE
+#define BLS_SCRATCH_PER_QUEUE 0ull  // set by lodestar_amd/build.py (-D); 0 = unknown (no limit)
+#endif
+#ifndef BLS_SCRATCH_WORST_KERNEL
+#define BLS_SCRATCH_WORST_KERNEL "unknown"
+#endif
+#define BLS_SCRATCH_BUDGET_DEFAULT (6ull << 30)  // 75 % of the ~8 GiB abort point
+
+namespace {
+std::mutex g_adm_mu;
+constexpr int ADM_MAX_DEV = 64;
+uint32_t g_adm_normal[ADM_MAX_DEV], g_adm_high[ADM_MAX_DEV];
+std::atomic<uint64_t> g_adm_budget_override{0};
+thread_local char g_init_err[512];
+
+uint32_t hw_queues_env() {
+  const char* e = getenv("GPU_MAX_HW_QUEUES");
+  const long v = e && *e ? strtol(e, nullptr, 10) : 0;
+  return v > 0 ? (uint32_t)v : 4u;
+}
+
+uint64_t scratch_budget() {
+  const uint64_t o = g_adm_budget_override.load();
+  if (o) return o;
+  const char* e = getenv("BLS_SCRATCH_BUDGET_MIB");
+  const unsigned long long v = e && *e ? strtoull(e, nullptr, 10) : 0ull;
+  return v ? (uint64_t)v << 20 : BLS_SCRATCH_BUDGET_DEFAULT;
+}
+
+void init_fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void init_fail(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_init_err, sizeof(g_init_err), fmt, ap);
+  va_end(ap);
+}
+}  // namespace
+
 extern "C" {
+
+int bls_scratch_plan(uint32_t n_normal, uint32_t n_high, uint32_t hw_queues, bls_admission* out) {
+  bls_admission a;
+  memset(&a, 0, sizeof(a));
+  a.contexts_normal = n_normal;
+  a.contexts_high = n_high;
+  a.hw_queues = hw_queues ? hw_queues : hw_queues_env();
+  a.queues_in_use = (n_normal < a.hw_queues ? n_normal : a.hw_queues) + (n_high < a.hw_queues ? n_high : a.hw_queues);
+  a.scratch_per_queue = BLS_SCRATCH_PER_QUEUE;
+  a.scratch_reserved = (uint64_t)a.queues_in_use * a.scratch_per_queue;
+  a.scratch_budget = scratch_budget();
+  if (out) *out = a;
+  return a.scratch_reserved <= a.scratch_budget ? 0 : BLS_ERR_ADMISSION;
+}
+
+const char* bls_scratch_worst_kernel(void) { return BLS_SCRATCH_WORST_KERNEL; }
+
+int bls_gpu_admission(int device, bls_admission* out) {
+  if (device < 0 || device >= ADM_MAX_DEV) return -2;
+  std::lock_guard<std::mutex> g(g_adm_mu);
+  return bls_scratch_plan(g_adm_normal[device], g_adm_high[device], 0, out);
+}
+
+void bls_gpu_set_scratch_budget(uint64_t bytes) { g_adm_budget_override.store(bytes); }
+
+const char* bls_gpu_init_error(void) { return g_init_err; }
 
 int bls_gpu_device_count(void) {
   int n = 0;
@@ -316,42 +396,67 @@ int bls_gpu_device_count(void) {
 int bls_gpu_init(int device, bls_gpu_ctx** out) { return bls_gpu_init_priority(device, BLS_PRIORITY_NORMAL, out); }
 
 int bls_gpu_init_priority(int device, int priority, bls_gpu_ctx** out) {
+  if (!out) return -2;
   *out = nullptr;
+  g_init_err[0] = 0;
+  if (device < 0 || device >= ADM_MAX_DEV) {
+    init_fail("bls_gpu_init: device %d out of range", device);
+    return -2;
+  }
+  const bool high = priority == BLS_PRIORITY_HIGH;
+  {
+    // admit first: a refused context never creates its stream (no queue, no reservation)
+    std::lock_guard<std::mutex> g(g_adm_mu);
+    bls_admission a;
+    const uint32_t nn = g_adm_normal[device] + (high ? 0u : 1u), nh = g_adm_high[device] + (high ? 1u : 0u);
+    if (bls_scratch_plan(nn, nh, 0, &a) != 0) {
+      init_fail("BLS_ERR_ADMISSION: a %s-priority context on device %d would map %u normal + %u high-priority "
+                "contexts onto %u hardware queues (GPU_MAX_HW_QUEUES=%u), reserving %llu MiB of scratch "
+                "(%llu MiB per queue for %s) > the %llu MiB budget ($BLS_SCRATCH_BUDGET_MIB); close a context or "
+                "lower the context count",
+                high ? "high" : "normal", device, nn, nh, a.queues_in_use, a.hw_queues,
+                (unsigned long long)(a.scratch_reserved >> 20), (unsigned long long)(a.scratch_per_queue >> 20),
+                BLS_SCRATCH_WORST_KERNEL, (unsigned long long)(a.scratch_budget >> 20));
+      return BLS_ERR_ADMISSION;
+    }
+    if (high) ++g_adm_high[device];
+    else ++g_adm_normal[device];
+  }
   bls_gpu_ctx* ctx = new bls_gpu_ctx();
   memset(ctx, 0, sizeof(*ctx));
   ctx->mu = new std::mutex();
   ctx->device = device;
-  hipError_t e = hipSetDevice(device);
-  if (e != hipSuccess) {
-    fprintf(stderr, "bls_gpu_init: hipSetDevice(%d): %s\n", device, hipGetErrorString(e));
-    delete ctx->mu;
-    delete ctx;
+  ctx->admitted = high ? 2 : 1;
+  // every failure below releases what was made through bls_gpu_close (it tolerates
+  // members that were never created) and leaves its message for bls_gpu_init_error
+  auto fail = [&](const char* what, hipError_t e) {
+    init_fail("bls_gpu_init: %s: %s", what, hipGetErrorString(e));
+    bls_gpu_close(ctx);
     return -1;
-  }
+  };
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return fail("hipSetDevice", e);
   int prio_lo = 0, prio_hi = 0;  // HIP: numerically lower = higher priority
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking,
-                                  priority == BLS_PRIORITY_HIGH ? prio_hi : prio_lo) != hipSuccess ||
-      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
-    delete ctx;
-    return -1;
-  }
-  for (int i = 0; i < 9; ++i) {
-    if (hipEventCreate(&ctx->ev[i]) != hipSuccess) {
-      delete ctx;
-      return -1;
-    }
-  }
+  if ((e = hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, high ? prio_hi : prio_lo)) != hipSuccess)
+    return fail("hipStreamCreateWithPriority", e);
+  if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess)
+    return fail("hipEventCreate", e);
+  for (int i = 0; i < 9; ++i)
+    if ((e = hipEventCreate(&ctx->ev[i])) != hipSuccess) return fail("hipEventCreate", e);
   if (load_coop_tables(ctx) != 0) {
-    fprintf(stderr, "bls_gpu_init: %s\n", ctx->err);
+    init_fail("bls_gpu_init: %s", ctx->err);
     bls_gpu_close(ctx);
     return -1;
   }
-  if (hipMalloc(&ctx->first_bad, 2 * sizeof(uint32_t)) != hipSuccess ||
-      hipMemset(ctx->first_bad, 0xFF, 2 * sizeof(uint32_t)) != hipSuccess) {
-    bls_gpu_close(ctx);
-    return -1;
-  }
+  if ((e = hipMalloc(&ctx->first_bad, 2 * sizeof(uint32_t))) != hipSuccess ||
+      (e = hipMemset(ctx->first_bad, 0xFF, 2 * sizeof(uint32_t))) != hipSuccess)
+    return fail("first_bad", e);
+  // the MSM's bucket counters and tickets: zeroed here once, then reset by the kernels'
+  // last workgroups (and re-zeroed after a failed call, verify_impl)
+  if ((e = hipMalloc(&ctx->msm_state, sizeof(uint32_t) * MSM_STATE_WORDS)) != hipSuccess ||
+      (e = hipMemset(ctx->msm_state, 0, sizeof(uint32_t) * MSM_STATE_WORDS)) != hipSuccess)
+    return fail("msm_state", e);
   *out = ctx;
   return 0;
 }
@@ -360,20 +465,27 @@ void bls_gpu_close(bls_gpu_ctx* ctx) {
   if (!ctx) return;
   ctx->mu->lock();  // wait for a call in flight on another thread
   ctx->mu->unlock();
+  if (ctx->admitted) {
+    std::lock_guard<std::mutex> g(g_adm_mu);
+    if (ctx->admitted == 2) --g_adm_high[ctx->device];
+    else --g_adm_normal[ctx->device];
+    ctx->admitted = 0;
+  }
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->table) (void)hipFree(ctx->table);
   if (ctx->dev_ws) (void)hipFree(ctx->dev_ws);
   if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
   if (ctx->host_res) (void)hipHostFree(ctx->host_res);
   if (ctx->first_bad) (void)hipFree(ctx->first_bad);
   if (ctx->msm_state) (void)hipFree(ctx->msm_state);
-  (void)hipEventDestroy(ctx->ev0);
-  (void)hipEventDestroy(ctx->ev1);
-  for (int i = 0; i < 9; ++i) (void)hipEventDestroy(ctx->ev[i]);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  for (int i = 0; i < 9; ++i)
+    if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   if (ctx->coop_dev) (void)hipFree(ctx->coop_dev);
   delete ctx->coop_progs;
-  (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx->mu;
   delete ctx;
 }
@@ -722,10 +834,30 @@ struct InFlight {
   ~InFlight() { g_sets_in_flight.fetch_sub(n, std::memory_order_relaxed); }
 };
 
+static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats,
+                       uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status, uint32_t* partial_err,
+                       const std::vector<uint32_t>* req_bounds);
+
+// One call under the context's lock.  A call that fails part-way may leave the MSM's
+// bucket counters / tickets (reset only by the kernels' last workgroups) mid-pass: they
+// are zeroed again before the context takes another call.
 static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats,
                        uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status,
                        uint32_t* partial_err = nullptr, const std::vector<uint32_t>* req_bounds = nullptr) {
   CTX_LOCK(ctx);
+  const int rc = verify_body(ctx, in, verdicts, stats, scalar_base, partial_out, partial_status, partial_err,
+                             req_bounds);
+  if (rc < 0 && ctx->msm_state) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipMemsetAsync(ctx->msm_state, 0, sizeof(uint32_t) * MSM_STATE_WORDS, ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream);
+  }
+  return rc;
+}
+
+static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats,
+                       uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status, uint32_t* partial_err,
+                       const std::vector<uint32_t>* req_bounds) {
   const bool partial = partial_out != nullptr;
   HIPC(ctx, hipSetDevice(ctx->device));
   const uint32_t n = in->n_sets, R = in->n_reqs;
@@ -776,7 +908,9 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // ... and under it the sum is one Pippenger MSM over the live sets (kernels/k_msm.hip)
   // instead of per-set [r] sig chains + k_gsum levels; the per-set RS are made (k_chain
   // role 2 alone) only when the merged check fails and the chunks' own sums are needed
-  const bool use_msm = use_total && (msm_on() || (ctx->debug_flags & BLS_DEBUG_MSM));
+  // (an MSM entry packs its bucket slot in 22 bits and a bucket takes up to 2 entries per
+  // set: passes above MSM_MAX_SETS keep the group sums)
+  const bool use_msm = use_total && n <= MSM_MAX_SETS && (msm_on() || (ctx->debug_flags & BLS_DEBUG_MSM));
   GsumPlan total_gsum;
   if (use_total) {
     std::vector<uint32_t> goff(n_chunks + 1, (uint32_t)chunk_gsum.gsets.size());
@@ -1003,10 +1137,6 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       HIPC(ctx, launch_k_chain(b, s, use_msm ? 0xBu : 0xFu)); dbg_sync(s, "k_chain");
       HIPC(ctx, hipEventRecord(ctx->ev[3], s));
       if (use_msm) {
-        if (!ctx->msm_state) {
-          HIPC(ctx, hipMalloc(&ctx->msm_state, sizeof(uint32_t) * MSM_STATE_WORDS));
-          HIPC(ctx, hipMemsetAsync(ctx->msm_state, 0, sizeof(uint32_t) * MSM_STATE_WORDS, s));
-        }
         msm.cnt = ctx->msm_state;
         msm.ticket = ctx->msm_state + MSM_BUCKETS;
         HIPC(ctx, launch_k_msm(b, msm, n_chunks, n, s)); dbg_sync(s, "k_msm");

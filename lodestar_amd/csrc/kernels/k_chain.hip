@@ -9,9 +9,10 @@
 //                                           verifyMultipleSignatures, [ext] blst)
 //
 // The batch equation prod e(r_i pk_i, H_i) * e(-g1, sum r_i sig_i) == 1 is then
-// evaluated as the reference's blst does it: one Miller loop per set for
-// (RP, H) (k_mln, cooperative) and ONE per group for (-g1, sum RS) (k_gsum sums
-// the RS of a chunk / request, k_vset turns the sum into a virtual set for k_mln).
+// evaluated as the reference's blst does it: one Miller loop per set for (RP, H)
+// (k_mlq / k_mlf, kernels/k_mlq.hip) and ONE per pass for (-g1, sum RS) (the merged
+// signature sum: k_msm's Pippenger sum, or k_gsum's group sums of the RS with k_vset
+// turning a sum into a virtual set).
 //
 // These are narrow, strictly sequential double-and-add chains (about 6k Fp products
 // per set: 3 G2 chains over |x|, one over r, one G1 chain over r): one lane per set
@@ -24,21 +25,11 @@
 // Output per live set (b.chain, CH_* layout); b.chain_live[i] = 1 (k_chain_done).  A
 // set whose request errors (decode status, infinity pubkey) or whose signature is
 // outside G2 gets f_i = 1 and is not live (not summed, no Miller loop).
-// The 28-bit-digit product (bls/field.hpp), called out of line: inlined into these
-// chains (512 VGPRs) it compiled to a kernel that never finished on gfx950 (ROCm 7.2,
-// BLS_DEBUG_SYNC); out of line it finishes, 394 VGPRs, and cfg2 runs 1-2 % faster than
-// with the inlined 32-bit-digit product (profiles/r02b_ab_chain_d28.json).  Build
-// variant chain_inl32 restores that one.
-#ifdef BLS_CHAIN_INL32
-#define BLS_FP_INLINE 1
-#elif defined(BLS_CHAIN_INL28)
-// build variant chain_inl28: the round-2 configuration that never finished (d28 product
-// inlined into the chains); the build's scratch guard rejects it
-#define BLS_FP_INLINE 1
+// The 28-bit-digit product (bls/field.hpp) is called out of line; inlined into these
+// chains the kernel needs 4,544 B of scratch per lane, a reservation of 568 MiB per
+// queue that took the runtime past its scratch grant with the bench's queues (DESIGN.md
+// §3, profiles/r03_chain_inl28_resources.txt) -- the round-2 "never finished".
 #define BLS_FP_D28 1
-#else
-#define BLS_FP_D28 1
-#endif
 #include "../launchers.hpp"
 
 using namespace bls;
@@ -60,17 +51,13 @@ __device__ G2J iso_jac(const Fp* q) {
 __device__ __noinline__ void g2_mul_u64(G2J* out, const G2J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
 // affine base (the signature): mixed additions
 __device__ __noinline__ void g2_mul_aff(G2J* out, const G2A* in, uint64_t k) { *out = aff_mul_u64(*in, k); }
-// [r] sig and [r] pk for the per-set batch scalar r: a fixed 4-bit window
-// (curve.hpp jac_mul_u64_w4) with the per-set table of [1..15]P in the call's
-// workspace (PipeBufs::rtab2 / rtab1: a private-memory table raised the scratch size
-// past what the runtime grants 64 calls in flight).  With one lane per set the scalars
-// differ across the wavefront, so double-and-add executes an addition at every bit
-// (some lane has a 1 there): 63 doublings + 63 additions per chain; the window
-// executes 63 doublings + 28 additions (profiles/r02c_ab_chain_window.json).
-// Default: GLV/GLS (curve.hpp jac_mul_glv): the set's scalar is a + b mu with a, b its
-// two 32-bit halves and mu = -x^2, applied as [a]P + [b]endo(P) through a joint 2-bit
-// window -- 33 doublings instead of 63 (G1: sigma(x, y) = (beta x, y); G2: -psi^2).
-#if !defined(BLS_CHAIN_BINARY_R) && !defined(BLS_CHAIN_W4)
+// [r] sig and [r] pk for the per-set batch scalar r: GLV/GLS (curve.hpp jac_mul_glv):
+// the set's scalar is a + b mu with a, b its two 32-bit halves and mu = -x^2, applied as
+// [a]P + [b]endo(P) through a joint 2-bit window -- 33 doublings instead of 63 (G1:
+// sigma(x, y) = (beta x, y); G2: -psi^2).  The window's table of points lives in the
+// call's workspace (PipeBufs::rtab2 / rtab1), not in private memory.  (Double-and-add
+// and a fixed 4-bit window over the 64-bit scalar measured slower,
+// profiles/r02c_ab_chain_window.json.)
 __device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J* T) {
   uint32_t a, b;
   glv_split(k, a, b);
@@ -81,17 +68,6 @@ __device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J* 
   glv_split(k, a, b);
   *out = jac_mul_glv<Fp>(*in, a, b, T);
 }
-#elif !defined(BLS_CHAIN_BINARY_R)  // build variant chain_w4: 64-bit scalars, 4-bit windows
-__device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J* T) {
-  *out = in->inf ? jac_infinity<Fp2>() : jac_mul_u64_w4<Fp2>(jac_from_aff(*in), in, k, T);
-}
-__device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J* T) {
-  *out = jac_mul_u64_w4<Fp>(*in, nullptr, k, T);
-}
-#else  // build variant chain_binr: double-and-add
-__device__ __noinline__ void g2_mul_r(G2J* out, const G2A* in, uint64_t k, G2J*) { *out = aff_mul_u64(*in, k); }
-__device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J*) { *out = jac_mul_u64(*in, k); }
-#endif
 // out-of-line general addition for the handful of additions outside the chains
 __device__ __noinline__ void g2_add(G2J* out, const G2J* a, const G2J* b) { *out = jac_add(*a, *b); }
 
@@ -202,17 +178,10 @@ __device__ __noinline__ void chain_role_rp(const PipeBufs& b, uint32_t i) {
 //   role 3  RP = [r] pk                                             ~1.0k
 // Results that decide the set's fate go to b.chain_st[4 i + role] (k_chain_done
 // reads them; every role that runs writes its byte, so no clearing is needed).
-// At most 256 VGPRs (93 spilled), so two wavefronts share a SIMD: cfg2 +1.2 % over one
-// 394-VGPR wavefront per SIMD (profiles/r02b_ab_chain_occ2.json); build variant
-// chain_occ1 lifts the cap, chain_occ3 lowers it to 3 per SIMD: both slower at the
-// bench default (1.69M and 1.82-1.84M vs 1.82-1.87M, profiles/r02c_ab_chain_occ.json).
-#ifdef BLS_CHAIN_OCC1
-#define BLS_CHAIN_ATTR
-#elif defined(BLS_CHAIN_OCC3)
-#define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(3)))
-#else
+// At most 256 VGPRs, so two wavefronts share a SIMD: cfg2 +1.2 % over one 394-VGPR
+// wavefront per SIMD (profiles/r02b_ab_chain_occ2.json); one or three per SIMD were
+// slower (profiles/r02c_ab_chain_occ.json).
 #define BLS_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(2)))
-#endif
 __global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, uint32_t blocks_per_role,
                                                                    uint32_t roles) {
   // the (blockIdx / blocks_per_role)-th role present in the mask

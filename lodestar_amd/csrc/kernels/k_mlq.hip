@@ -13,8 +13,8 @@
 //          of different domains, or the individually verified pass (units_paired = 0),
 //          run one f per item.
 //
-// Against the fused one-lane loop (k_mls: 6,803 Fp products per pair, f + T + lines
-// live together in one lane, 512 registers and spills): the line side takes ~1,920
+// Against a fused one-lane loop (6,803 Fp products per pair, f + T + lines live together
+// in one lane, 512 registers and spills; removed in round 4): the line side takes ~1,920
 // products per pair with T, P and Q only; the f side 62 squarings (36) per two pairs
 // plus 68 sparse line products (39) per pair -> ~5,700 products per pair, each kernel
 // with half the live state.
@@ -92,8 +92,8 @@ __device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, uint32_
     const int adds = (int)((X >> bit) & 1ull);
     for (int a = 0; a <= adds; ++a) {
       uint32_t g = 0;
-#ifndef BLS_MLF_SINGLE_LINES
-      // two items' lines at once (fp12_mul_line2: 23 Fp2 products instead of 26)
+      // two items' lines at once (fp12_mul_line2: 23 Fp2 products instead of 26; +4 % at
+      // the plateau, profiles/r03_ab_mlq_mlf.json)
 #pragma unroll 1
       for (; g + 1 < n; g += 2) {
         Fp2 l0, l2, l3, m0, m2, m3;
@@ -101,7 +101,6 @@ __device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, uint32_
         load_line(L, stride, k0 + g + 1, e, m0, m2, m3);
         f = fp12_mul_line2(f, l0, l2, l3, m0, m2, m3);
       }
-#endif
 #pragma unroll 1
       for (; g < n; ++g) {
         Fp2 l0, l2, l3;

@@ -213,30 +213,13 @@ __global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
 // A part of the wave with no live set borrows the first live set's inputs.
 enum : int { ML1_SLOTS = 19, ML1_RP = 0, ML1_HQ = 3, ML1_F = 7 };
 
-// Whether the SH items at i0 (first pass: units paired) are live items of one
-// product domain, so they can share one Miller loop (ml1s_4 / ml1s_8)
-template <int SH>
-__device__ __forceinline__ bool mln_shared(const PipeBufs& b, const CoopEnv& env, uint32_t i0, uint32_t end) {
-  const CoopProg& pg = SH == 8 ? env.ml1s_8 : env.ml1s_4;
-  if (!b.ml_dom || pg.n == 0 || i0 + (uint32_t)SH > end || i0 + (uint32_t)SH > b.indiv_vbase) return false;
-  bool shared = true;
-#pragma unroll
-  for (int s = 0; s < SH; ++s) {
-    const uint32_t i = i0 + s;
-    shared = shared && b.chain_live[i] && !(b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE) &&
-             b.ml_dom[i] == b.ml_dom[i0];
-  }
-  return shared;
-}
-
 // S items starting at i0 on an LDS frame: the single-pair loops (ml1_S, constants
-// staged at slot cb, the frame size that program was scheduled for) or, for four live
-// items of one product domain, one shared 4-pair loop (ml1s_4, constants at slot
-// COOP_FRAME4S).  The body of k_mln<S>.
+// staged at slot cb, the frame size that program was scheduled for).  The body of
+// k_mln<S>.
 template <int S>
 __device__ __forceinline__ void mln_items(const PipeBufs& b, const CoopEnv& env, Fp* frame, uint32_t* flag,
                                           int cb, uint32_t i0, uint32_t end, uint32_t units_paired) {
-  const CoopProg& ml = S == 1 ? env.ml1_1 : (S == 2 ? env.ml1_2 : env.ml1_4);
+  const CoopProg& ml = S == 1 ? env.ml1_1 : env.ml1_2;
   const int lane = threadIdx.x;
   bool live[S];
   int first_live = -1;
@@ -250,9 +233,7 @@ __device__ __forceinline__ void mln_items(const PipeBufs& b, const CoopEnv& env,
     if (live[s] && first_live < 0) first_live = s;
   }
   if (first_live < 0) return;
-  // shared mode: four live items of one product domain -> one loop, f in the first item
-  const bool shared = S == 4 && units_paired && mln_shared<4>(b, env, i0, end);
-  coop_stage_consts(env, frame + (shared ? COOP_FRAME4S : cb));
+  coop_stage_consts(env, frame + cb);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint32_t i = i0 + (live[s] ? s : first_live), o = ML1_SLOTS * s;
@@ -262,12 +243,7 @@ __device__ __forceinline__ void mln_items(const PipeBufs& b, const CoopEnv& env,
   }
   if (lane == 0) *flag = 0;
   __syncthreads();
-  coop_run(env, shared ? env.ml1s_4 : ml, frame, frame + (shared ? COOP_FRAME4S : cb), flag);
-  if (shared) {
-    if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(frame, ML1_F + lane);
-    else if (lane < 48) reinterpret_cast<Fp*>(&b.f[i0 + 1 + (lane - 12) / 12])[lane % 12] = lane % 12 ? fp_zero() : c_one();
-    return;
-  }
+  coop_run(env, ml, frame, frame + cb, flag);
 #pragma unroll
   for (int s = 0; s < S; ++s)
     if (live[s] && lane < 12) reinterpret_cast<Fp*>(&b.f[i0 + s])[lane] = coop_get(frame, ML1_SLOTS * s + ML1_F + lane);
@@ -279,86 +255,6 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uin
   __shared__ Lds sh;
   mln_items<S>(b, env, sh.frame, &sh.flag, (int)(sizeof(sh.frame) / sizeof(Fp)), first + (uint32_t)S * blockIdx.x,
                first + count, units_paired);
-}
-
-// First-pass Miller loops, one launch: blocks [0, G) take the real sets [first, mid)
-// SH at a time -- SH live sets of one chunk run one shared SH-pair loop (ml1s_SH),
-// otherwise each pair runs ml1_2 -- and the blocks after them the virtual items of
-// [mid, mid + V) (chunk signature sums, units), vp per wavefront.  SH = 8 (default):
-// 512 slots (26.5 KB, 6 wavefronts per CU), 24 % fewer interpreter steps per set than
-// 4-pair loops; with no Miller-loop units its virtual items (the chunk signature sums)
-// go four per wavefront (vp = 4: ml1_4 in the same frame, 916 steps, inside the 1,133
-// of the shared loops); with units (cfg5) the units carry most of the Miller loops
-// and go one per wavefront (vp = 1: ml1_1, 408 steps) to keep the launch short.  SH = 4: the 288-slot frame (COOP_FRAME4S, 15.7 KB, 10 per CU), one
-// virtual item per wavefront (ml1_1, 408 steps: ml1_4 does not fit the frame).  The
-// interpreter is inlined once, so the occupancy attribute bounds its registers (163
-// VGPRs, 3 wavefronts per SIMD; the out-of-line copy takes 256 and 2).
-#ifndef BLS_MLN4S_WAVES
-#define BLS_MLN4S_WAVES 3
-#endif
-// (SH = 8: the LDS caps it at 1.5 per SIMD, so the register budget is 2)
-template <int SH>
-__global__ __launch_bounds__(COOP_LANES)
-__attribute__((amdgpu_waves_per_eu(SH == 8 ? 2 : BLS_MLN4S_WAVES, SH == 8 ? 2 : BLS_MLN4S_WAVES)))
-void k_mlns(PipeBufs b, CoopEnv env, uint32_t first, uint32_t mid, uint32_t n_virt, uint32_t vp) {
-  constexpr int VP = SH == 8 ? 4 : 1;  // the most virtual items per wavefront
-  __shared__ CoopLdsN<SH == 8 ? COOP_FRAME8S : COOP_FRAME4S> sh;
-  const int lane = threadIdx.x;
-  const uint32_t G = (mid - first + (uint32_t)SH - 1u) / (uint32_t)SH;
-  const bool virt = blockIdx.x >= G;
-  const uint32_t i0 = virt ? mid + vp * (blockIdx.x - G) : first + (uint32_t)SH * blockIdx.x;
-  const uint32_t end = virt ? mid + n_virt : mid;
-  const bool shd = !virt && mln_shared<SH>(b, env, i0, end);
-  const bool vsh = virt && VP == 4 && vp == 4u && mln_shared<4>(b, env, i0, end);
-  const int n = virt ? (int)vp : (shd ? SH : 2);
-  int cb = COOP_FRAME;
-  CoopProg pg = env.ml1_2;
-  if (shd) {
-    cb = SH == 8 ? COOP_FRAME8S : COOP_FRAME4S;
-    pg = SH == 8 ? env.ml1s_8 : env.ml1s_4;
-  } else if (vsh) {
-    cb = COOP_FRAME4S;
-    pg = env.ml1s_4;
-  } else if (virt) {
-    cb = (VP == 4 && vp == 4u) ? COOP_FRAME2 : COOP_FRAME;
-    pg = (VP == 4 && vp == 4u) ? env.ml1_4 : env.ml1_1;
-  }
-  for (uint32_t h = 0; h < ((virt || shd) ? 1u : (uint32_t)SH / 2u); ++h) {
-    const uint32_t j0 = i0 + 2u * h;
-    bool live[SH];
-    int first_live = -1;
-#pragma unroll
-    for (int s = 0; s < SH; ++s) {
-      const uint32_t i = j0 + s;
-      live[s] = s < n && i < end && b.chain_live[i] && !(b.set_unit && i < b.n_sets && b.set_unit[i] != UNIT_NONE);
-      if (live[s] && first_live < 0) first_live = s;
-    }
-    if (first_live < 0) continue;
-    __syncthreads();
-    coop_stage_consts(env, sh.frame + cb);
-#pragma unroll
-    for (int s = 0; s < SH; ++s) {
-      if (s >= n) break;
-      const uint32_t i = j0 + (live[s] ? s : first_live), o = ML1_SLOTS * s;
-      const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
-      if (lane < 3) lds_store_fp(sh.frame, o + ML1_RP + lane, ch[CH_RP + lane]);
-      else if (lane < 7) lds_store_fp(sh.frame, o + ML1_HQ + lane - 3, ch[CH_HQ + lane - 3]);
-    }
-    if (lane == 0) sh.flag = 0;
-    __syncthreads();
-    coop_run_inline(env, pg, sh.frame, &sh.flag);
-    if (shd || vsh) {
-      // f of item 0 = the product; items 1 .. n-1 = 1
-      if (lane < 12) reinterpret_cast<Fp*>(&b.f[i0])[lane] = coop_get(sh.frame, ML1_F + lane);
-      for (int w = lane - 12; w >= 0 && w < 12 * (n - 1); w += 52)
-        reinterpret_cast<Fp*>(&b.f[i0 + 1 + w / 12])[w % 12] = w % 12 ? fp_zero() : c_one();
-    } else {
-#pragma unroll
-      for (int s = 0; s < (VP > 2 ? VP : 2); ++s)
-        if (s < n && live[s] && lane < 12)
-          reinterpret_cast<Fp*>(&b.f[j0 + s])[lane] = coop_get(sh.frame, ML1_SLOTS * s + ML1_F + lane);
-    }
-  }
 }
 
 // Sets per wavefront for a batch: 1 for small batches (latency: one wave per set
@@ -380,31 +276,10 @@ static uint32_t pack_for(uint32_t n_sets) {
   return n_sets >= min_sets ? 2u : 1u;
 }
 
-// Sets per wavefront of k_mln: BLS_DEBUG_PACK(1 / 2) or $BLS_ML_PACK (1, 2, 4); default 4
-static uint32_t ml_pack(const PipeBufs& b) {
-  static const int env = [] {
-    const char* e = getenv("BLS_ML_PACK");
-    return e ? atoi(e) : 0;
-  }();
-  if (b.pack == 1 || b.pack == 2) return b.pack;
-  if (env == 1 || env == 2 || env == 4) return (uint32_t)env;
-  return 4u;
-}
-
-// own_only: sets run their own Miller loop even when they belong to a unit (requests
-// verified alone after their chunk failed)
-// SIMT Miller loops unless a test forces a cooperative packing (BLS_DEBUG_PACK):
-// $BLS_ML_SIMT = 2 (default): lines then f (kernels/k_mlq.hip); 1: the fused one-lane
-// loop (kernels/k_mls.hip); 0: the cooperative kernels below
-static int ml_simt() {
-  static const int simt = [] {
-    const char* e = getenv("BLS_ML_SIMT");
-    return e ? atoi(e) : 2;
-  }();
-  return simt;
-}
-
-bool k_mln_list_ok(const PipeBufs& b) { return ml_simt() == 2 && b.pack == 0 && b.ml_lines; }
+// The aggregated path's Miller loops are the SIMT pair k_mlq / k_mlf
+// (kernels/k_mlq.hip); a test that forces a cooperative packing (BLS_DEBUG_PACK(1 / 2))
+// runs them as the cooperative single-pair loops above instead, 1 or 2 per wavefront.
+bool k_mln_list_ok(const PipeBufs& b) { return b.pack == 0 && b.ml_lines; }
 
 hipError_t launch_k_mln_list(const PipeBufs& b, const uint32_t* items, uint32_t count, hipStream_t s) {
   if (count == 0) return hipSuccess;
@@ -412,37 +287,14 @@ hipError_t launch_k_mln_list(const PipeBufs& b, const uint32_t* items, uint32_t 
   return launch_k_mlqf(b, 0, count, true, b.ml_lines, s, items);
 }
 
+// own_only: sets run their own Miller loop even when they belong to a unit (requests
+// verified alone after their chunk failed)
 hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count, hipStream_t s,
                         bool own_only) {
   if (count == 0) return hipSuccess;
-  const int simt = ml_simt();
-  if (simt == 2 && b.pack == 0 && b.ml_lines) return launch_k_mlqf(b, first, count, own_only, b.ml_lines, s);
-  if (simt >= 1 && b.pack == 0) return launch_k_mls(b, first, count, own_only, s);
-  const uint32_t S = ml_pack(b), up = own_only ? 0u : 1u;
-  static const bool small_frame = [] {
-    const char* e = getenv("BLS_ML_SMALL_FRAME");
-    return !(e && e[0] == '0');
-  }();
-  if (S == 4 && up && small_frame && b.ml_dom && env.ml1s_4.n > 0 && env.ml1_2.n > 0) {
-    // first pass: the real sets four per wavefront, the virtual items (chunk signature
-    // sums, Miller-loop units) one per wavefront, in one launch
-    // eight pairs per shared loop by default (fewer interpreter steps per set: +6 % at
-    // the bench's 8 x 8 calls in flight, profiles/r02c_ab_share8.json); $BLS_ML_SHARE=4
-    static const uint32_t share = [] {
-      const char* e = getenv("BLS_ML_SHARE");
-      return (e && atoi(e) == 4) ? 4u : 8u;
-    }();
-    const uint32_t end = first + count, mid = b.n_sets <= first ? first : (b.n_sets < end ? b.n_sets : end);
-    if (share == 8 && env.ml1s_8.n > 0 && env.ml1_4.n > 0) {
-      const uint32_t vp = b.n_units ? 1u : 4u;
-      k_mlns<8><<<(mid - first + 7) / 8 + (end - mid + vp - 1) / vp, COOP_LANES, 0, s>>>(b, env, first, mid,
-                                                                                        end - mid, vp);
-    } else {
-      k_mlns<4><<<(mid - first + 3) / 4 + (end - mid), COOP_LANES, 0, s>>>(b, env, first, mid, end - mid, 1u);
-    }
-  } else if (S == 4 && env.ml1_4.n > 0) {
-    k_mln<4, CoopLdsN<COOP_FRAME2>><<<(count + 3) / 4, COOP_LANES, 0, s>>>(b, env, first, count, up);
-  } else if (S == 2 && env.ml1_2.n > 0) {
+  if (b.pack == 0 && b.ml_lines) return launch_k_mlqf(b, first, count, own_only, b.ml_lines, s);
+  const uint32_t up = own_only ? 0u : 1u;
+  if (b.pack == 2 && env.ml1_2.n > 0) {
     k_mln<2, CoopLds><<<(count + 1) / 2, COOP_LANES, 0, s>>>(b, env, first, count, up);
   } else {
     k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env, first, count, up);

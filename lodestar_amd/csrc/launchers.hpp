@@ -11,12 +11,8 @@
 // Serial tails of a pass (signature sums, their affine form, the product tree and the
 // final exponentiations, status) run few wavefronts whose chains set the pass latency;
 // with other passes' wide kernels on the same SIMDs they raise their wave priority so the
-// SIMD issues them first (s_setprio 3).  $-free A/B: build variant "noprio".
-#ifdef BLS_NO_TAIL_PRIO
-#define BLS_TAIL_PRIO() ((void)0)
-#else
+// SIMD issues them first (s_setprio 3; +3.6 % at 4 x 16, profiles/r03_ab_tail_prio.json).
 #define BLS_TAIL_PRIO() __builtin_amdgcn_s_setprio(3)
-#endif
 
 static inline unsigned bls_grid_for(uint32_t n) { return (n + BLS_BLOCK - 1) / BLS_BLOCK; }
 
@@ -48,6 +44,7 @@ struct MsmBufs {
 #define MSM_BUCKETS 1020u
 size_t msm_seg_cap(uint32_t n_sets);
 #define MSM_STATE_WORDS (MSM_BUCKETS + 2u)
+#define MSM_MAX_SETS (1u << 21)  // k_msm_bin: 22-bit bucket slots, <= 2 entries per set and bucket
 // the merged signature sum into the chunk groups' virtual sets vbase .. vbase + groups
 hipError_t launch_k_msm(const bls::PipeBufs& b, const MsmBufs& m, uint32_t groups, uint32_t vbase, hipStream_t s);
 hipError_t launch_k_gsum(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const bls::G2J* in,
@@ -91,7 +88,6 @@ hipError_t launch_k_mln(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_
 // the failed chunks at once
 bool k_mln_list_ok(const bls::PipeBufs& b);
 hipError_t launch_k_mln_list(const bls::PipeBufs& b, const uint32_t* items, uint32_t count, hipStream_t s);
-hipError_t launch_k_mls(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, hipStream_t s);
 size_t mlq_line_words(uint32_t count);
 // sets in the verify calls currently running in this process (every context)
 uint64_t bls_sets_in_flight();

@@ -11,7 +11,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._abi import BlsBatch, BlsStats, load_library
+from ._abi import ERR_ADMISSION, BlsAdmission, BlsBatch, BlsStats, load_library
 
 
 def _ptr(a: np.ndarray | None):
@@ -29,6 +29,26 @@ def _u8(b) -> np.ndarray:
 
 class NativeError(RuntimeError):
     pass
+
+
+class AdmissionError(NativeError):
+    """bls_gpu_init refused the context (BLS_ERR_ADMISSION): the HIP runtime's scratch for
+    the process's contexts would pass the budget (include/lodestar_bls.h bls_admission)."""
+
+
+def scratch_plan(n_normal: int, n_high: int, hw_queues: int = 0) -> tuple[bool, dict]:
+    """The library's admission accounting for n_normal + n_high contexts (no device
+    needed): (admissible, the bls_admission figures)."""
+    a = BlsAdmission()
+    rc = load_library().bls_scratch_plan(n_normal, n_high, hw_queues, ctypes.byref(a))
+    return rc == 0, {f: getattr(a, f) for f, _ in BlsAdmission._fields_}
+
+
+def admission(device: int = 0) -> dict:
+    """The figures for the contexts open on `device` in this process."""
+    a = BlsAdmission()
+    load_library().bls_gpu_admission(device, ctypes.byref(a))
+    return {f: getattr(a, f) for f, _ in BlsAdmission._fields_}
 
 
 @dataclass
@@ -117,8 +137,10 @@ class GpuContext:
         if ndev <= device:
             raise NativeError(f"no HIP device {device} (visible: {ndev}); the verifier has no CPU fallback")
         h = ctypes.c_void_p()
-        if self.lib.bls_gpu_init_priority(device, 1 if high_priority else 0, ctypes.byref(h)) != 0:
-            raise NativeError(f"bls_gpu_init_priority({device}) failed")
+        rc = self.lib.bls_gpu_init_priority(device, 1 if high_priority else 0, ctypes.byref(h))
+        if rc != 0:
+            msg = (self.lib.bls_gpu_init_error() or b"").decode() or f"bls_gpu_init_priority({device}) failed"
+            raise (AdmissionError if rc == ERR_ADMISSION else NativeError)(msg)
         self._h = h
         self.device = device
 

@@ -47,7 +47,7 @@ from typing import Sequence, Union
 
 from ._abi import ERROR_MESSAGES
 from .metrics import BlsMetrics, get_aggregated_pubkeys_count
-from .native import GpuContext, pack_requests
+from .native import GpuContext, NativeError, pack_requests
 
 MAX_SIGNATURE_SETS_PER_JOB = 128   # multithread/index.ts:39
 GPU_SETS_PER_CALL = 1024           # sets per bls_gpu_verify call (cfg2 shape)
@@ -108,8 +108,20 @@ class GpuBlsVerifier:
                  metrics: BlsMetrics | None = None):
         self.verify_all_multi_thread = verify_all_multi_thread
         self.max_sets_per_call = max_sets_per_call
-        self._ctxs = [GpuContext(device) for _ in range(n_contexts)]
-        self._main = GpuContext(device, high_priority=True)  # the main-thread lane, no pool call
+        # the main-thread lane first (its own high-priority context, never used by the
+        # pool), then the pool's contexts: a context the library refuses (scratch
+        # admission, BLS_ERR_ADMISSION) or that fails to start is recorded and the pool runs
+        # on the others, as the reference's pool keeps the workers that started
+        # (multithread/index.ts:221-229); with none at all, queued work raises the first
+        # error (index.ts:247-253)
+        self._main = GpuContext(device, high_priority=True)
+        self._ctxs: list[GpuContext] = []
+        self.init_errors: list[Exception] = []
+        for _ in range(n_contexts):
+            try:
+                self._ctxs.append(GpuContext(device))
+            except NativeError as e:
+                self.init_errors.append(e)
         self._main_lock = threading.Lock()
         if pubkeys48 is not None:
             self.load_pubkeys(pubkeys48)
@@ -261,6 +273,8 @@ class GpuBlsVerifier:
         return verdicts, stats
 
     def _queue(self, sets: list, batchable: bool) -> _Job:
+        if not self._ctxs and self.init_errors:
+            raise self.init_errors[0]  # every pool context failed to start (index.ts:247-253)
         job = _Job([_wire(s) for s in sets], batchable, Future(), time.monotonic())
         with self._cv:
             if self._closed:

@@ -130,20 +130,6 @@ void hs_fp_mul_d28_raw(const uint8_t* a, const uint8_t* b, uint8_t* out, int sqr
   Fp r = sqr ? fp_sqr_d28_lazy(x) : fp_mul_d28_lazy(x, y);
   memcpy(out, r.l, 48);
 }
-void hs_fp_mul_fips_raw(const uint8_t* a, const uint8_t* b, uint8_t* out, int sqr) {
-  Fp x, y;
-  memcpy(x.l, a, 48);
-  memcpy(y.l, b, 48);
-  const Fp r = sqr ? fp_mul_fips<true>(x, x) : fp_mul_fips<false>(x, y);
-  memcpy(out, r.l, 48);
-}
-void hs_fp_mul_cios_raw(const uint8_t* a, const uint8_t* b, uint8_t* out) {
-  Fp x, y;
-  memcpy(x.l, a, 48);
-  memcpy(y.l, b, 48);
-  const Fp r = fp_mul_cios(x, y);
-  memcpy(out, r.l, 48);
-}
 void hs_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_add(rd_fp(a), rd_fp(b)), out); }
 void hs_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp(fp_sub(rd_fp(a), rd_fp(b)), out); }
 void hs_fp_half(const uint8_t* a, uint8_t* out) { wr_fp(fp_half(rd_fp(a)), out); }

@@ -194,4 +194,34 @@ def test_work_pricing_follows_pass_shape():
     quad, _ = bench.work_per_set(n, shape=1 | (4 << 8))
     assert "Pippenger" in note
     assert chains - msm > 0.8 * wm["chain_r_sig"]  # the [r] sig chains leave, the MSM costs little
-    assert msm - quad == pytest.approx(wm["ml_f_pair"] - wm["ml_f_quad"])
+    # every set's loop and the pass's one signature loop (1 / n per set) follow the shape
+    assert msm - quad == pytest.approx((wm["ml_f_pair"] - wm["ml_f_quad"]) * (1 + 1 / n))
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts two rank processes itself (RANK /
+    WORLD_SIZE / LOCAL_RANK, rendezvous on 127.0.0.1) and rank 0 reports n_gpus 2 -- here
+    as a dry run: gloo ranks whose contexts are the oracle stand-in (--stand-in), the
+    cfg4 range-sync job sharded by call at reduced size."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = str(root)
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", "2", "--mode", "cfg4", "--steps", "1", "--warmup", "0",
+           "--inflight", "1", "--table-keys", "16", "--cfg4-sets", "16", "--cfg4-call-sets", "8", "--cfg4-agg-k", "4",
+           "--cfg4-invalid", "0.1", "--stand-in", "tests.test_bench_jobs:OracleCtx"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(root))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 alone prints
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["value"] > 0 and "DRY RUN" in r["data"]
+    assert r["job"]["sets"] == 16 and r["job"]["calls"] == 2  # this rank's half of the 32-set job
+    # a launcher's WORLD_SIZE must agree with --gpus
+    bad = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--mode", "cfg4"], capture_output=True,
+                         text=True, timeout=120, env=dict(env, WORLD_SIZE="1"), cwd=str(root))
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

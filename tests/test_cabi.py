@@ -13,7 +13,7 @@ ROOT = Path(__file__).resolve().parent.parent
 
 def test_header_symbols_exported():
     hdr = (ROOT / "include" / "lodestar_bls.h").read_text()
-    declared = set(re.findall(r"^\s*(?:int|void|int64_t|const char\*)\s+(bls_gpu_\w+)\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:int|void|int64_t|const char\*)\s+(bls_\w+)\(", hdr, re.M))
     assert declared == set(SYMBOLS)
     lib = ctypes.CDLL(str(LIB_PATH))
     for name in declared:
@@ -37,3 +37,37 @@ def test_device_count_without_gpu():
 
     lib = load_library()
     assert lib.bls_gpu_device_count() >= 0
+
+
+def test_scratch_admission_accounting():
+    """The admission arithmetic (bls_scratch_plan, no device): queues per priority level
+    are min(contexts, GPU_MAX_HW_QUEUES); the per-queue figure is the deepest kernel's
+    reservation from the build's resource table; a context is admitted while
+    queues x per-queue <= budget (include/lodestar_bls.h bls_admission)."""
+    import json
+
+    from lodestar_amd._abi import load_library
+    from lodestar_amd.native import scratch_plan
+
+    lib = load_library()
+    res = json.loads((ROOT / "lodestar_amd" / "_native" / "kernel_resources.json").read_text())
+    per_queue = max(k["device_scratch_bytes"] for k in res["kernels"])
+    assert res["scratch_per_queue"] == per_queue > 0
+    assert res["scratch_worst_kernel"].encode() == lib.bls_scratch_worst_kernel()
+    lib.bls_gpu_set_scratch_budget(0)
+    ok, a = scratch_plan(12, 1, 24)
+    assert ok and a["queues_in_use"] == 13 and a["scratch_per_queue"] == per_queue
+    assert a["scratch_reserved"] == 13 * per_queue and a["scratch_budget"] == 6 << 30
+    # at HIP's default 4 queues per priority every context count fits
+    ok, a = scratch_plan(64, 8, 4)
+    assert ok and a["queues_in_use"] == 8
+    # the largest admissible count with one queue per context, and one more refused
+    cap = (6 << 30) // per_queue
+    assert scratch_plan(cap - 1, 1, 64)[0] and not scratch_plan(cap, 1, 64)[0]
+    # an override budget (bls_gpu_set_scratch_budget) moves the cap; 0 restores it
+    lib.bls_gpu_set_scratch_budget(3 * per_queue)
+    try:
+        assert scratch_plan(2, 1, 64)[0] and not scratch_plan(3, 1, 64)[0]
+    finally:
+        lib.bls_gpu_set_scratch_budget(0)
+    assert scratch_plan(12, 1, 24)[1]["scratch_budget"] == 6 << 30

@@ -48,28 +48,6 @@ def test_fp_mul_d28_lazy(hostsim):
             assert r % P == (a * (a if sqr else b) * rinv) % P
 
 
-def test_fp_mul_fips(hostsim):
-    """The product-scanning and row-interleaved products (field.hpp fp_mul_fips,
-    fp_mul_cios): the same value as the column product for inputs < 3p, output < 2p,
-    squares included."""
-    rng = random.Random(33)
-    o, o2 = _buf(48), _buf(48)
-    rinv = pow(2, -384, P)
-    vals = [0, 1, P - 1, P, 2 * P - 1, 3 * P - 1, 2 ** 382, 3 * P - 2 ** 200] + [rng.randrange(3 * P) for _ in range(300)]
-    for k, a in enumerate(vals):
-        b = vals[(7 * k + 3) % len(vals)]
-        for sqr in (0, 1):
-            hostsim.hs_fp_mul_fips_raw(a.to_bytes(48, "little"), b.to_bytes(48, "little"), o, sqr)
-            r = int.from_bytes(o.raw, "little")
-            assert r < 2 * P
-            assert r % P == (a * (a if sqr else b) * rinv) % P
-            hostsim.hs_fp_mul_d28_raw(a.to_bytes(48, "little"), b.to_bytes(48, "little"), o2, sqr)
-            assert o.raw == o2.raw
-        hostsim.hs_fp_mul_cios_raw(a.to_bytes(48, "little"), b.to_bytes(48, "little"), o)
-        hostsim.hs_fp_mul_d28_raw(a.to_bytes(48, "little"), b.to_bytes(48, "little"), o2, 0)
-        assert o.raw == o2.raw
-
-
 def test_fp2_mul_lazy(hostsim):
     """The device Fp2 product with one reduction per coefficient (field.hpp fp2_mul_d28):
     canonical inputs -> canonical (a0 b0 - a1 b1) / R, (a0 b1 + a1 b0) / R, including the

@@ -48,7 +48,8 @@ def test_js_pool_matches_reference_tests(gpu, golden, oracle, tmp_path):
     assert r["empty"] == "Empty signature set"
     # state-transition verifySignatureSet through verifySync (signatureSets.ts:24-38)
     assert r["stfSync"] == [True, False, "BLST_ERROR: BLST_INVALID_SIZE"]
-    assert r["stfEach"] == [True, False, True]
+    assert r["stfEach"] == [True, False, True, False]
+    assert r["stfEachInvalid"] == [False, "BLST_ERROR: BLST_INVALID_SIZE"]
 
 
 def test_js_adapter_host_side():
@@ -71,6 +72,12 @@ def test_js_adapter_host_side():
     assert r["raw_max_call_sets"] == 128
     # verifyOnMainThread runs on the dedicated high-priority context
     assert r["main_handles"] == 1 and r["main_calls"] == [1] and r["pool_high"] == 2
+    # the libuv pool warning reads the pool the process started with (a stand-in of 4)
+    assert r["pool_warning"] and "4 threads < contexts + 2 = 5" in r["pool_warning"]
+    # admission: a refused pool context is recorded and the pool runs on the others; with
+    # none admitted, queued work rejects with the first error (multithread/index.ts:247-253)
+    assert r["admitted_partial"] == {"ctxs": 1, "errors": 2, "verdict": True}
+    assert r["admitted_none"] == "BLS_ERR_ADMISSION: stand-in refusal"
 
 
 @pytest.mark.gpu

@@ -103,65 +103,3 @@ def test_pset2_two_sets_per_wavefront(progs, oracle):
         o = PS.SET_SLOTS * s + PS.F
         f = [(frame[o + 6 * (w % 2) + 2 * (w // 2)], frame[o + 6 * (w % 2) + 2 * (w // 2) + 1]) for w in range(6)]
         assert oracle.f12_is_one(oracle.final_exponentiation(f, hard_multiple=3)) == expect_one[s]
-
-
-def test_ml1_shared_equals_product_of_single_loops(progs, oracle):
-    """ml1s_4 (four pairs of one chunk sharing f's squarings, k_mln's shared mode) gives
-    exactly the product of the four single-pair loops ml1_4 computes."""
-    pg, consts = progs
-    rng = random.Random(21)
-    frame = [0] * GC.FRAME2
-    assert pg["ml1s_4"].n_slots == GC.FRAME4S
-    for s in range(4):
-        o = PS.ML1_SLOTS * s
-        k1, k2 = rng.randrange(1, oracle.R), rng.randrange(1, oracle.R)
-        px, py = oracle.E1.mul(oracle.G1, k1)
-        z = rng.randrange(1, P)
-        frame[o + PS.ML1_RP:o + PS.ML1_RP + 3] = [px * z * z % P, py * z ** 3 % P, z]
-        (x0, x1), (y0, y1) = oracle.E2.mul(oracle.G2, k2)
-        frame[o + PS.ML1_HQ:o + PS.ML1_HQ + 4] = [x0, x1, y0, y1]
-    single, shared = list(frame), list(frame)
-    simulate(pg["ml1_4"], single, consts)
-    simulate(pg["ml1s_4"], shared, consts)
-
-    def f12(fr, o):
-        return [(fr[o + 6 * (w % 2) + 2 * (w // 2)] % P, fr[o + 6 * (w % 2) + 2 * (w // 2) + 1] % P) for w in range(6)]
-
-    prod = f12(single, PS.ML1_F)
-    for s in range(1, 4):
-        prod = oracle.f12_mul(prod, f12(single, PS.ML1_SLOTS * s + PS.ML1_F))
-    assert f12(shared, PS.ML1_F) == prod
-
-
-
-def test_ml1_shared8_equals_product_of_single_loops(progs, oracle):
-    """ml1s_8 (k_mlns<8>, $BLS_ML_SHARE=8: eight pairs of one chunk sharing f's
-    squarings) gives exactly the product of the eight single-pair loops ml1_4 computes
-    on the two halves."""
-    pg, consts = progs
-    rng = random.Random(23)
-    frame = [0] * GC.FRAME8S
-    for s in range(8):
-        o = PS.ML1_SLOTS * s
-        k1, k2 = rng.randrange(1, oracle.R), rng.randrange(1, oracle.R)
-        px, py = oracle.E1.mul(oracle.G1, k1)
-        z = rng.randrange(1, P)
-        frame[o + PS.ML1_RP:o + PS.ML1_RP + 3] = [px * z * z % P, py * z ** 3 % P, z]
-        (x0, x1), (y0, y1) = oracle.E2.mul(oracle.G2, k2)
-        frame[o + PS.ML1_HQ:o + PS.ML1_HQ + 4] = [x0, x1, y0, y1]
-    shared = list(frame)
-    simulate(pg["ml1s_8"], shared, consts)
-
-    def f12(fr, o):
-        return [(fr[o + 6 * (w % 2) + 2 * (w // 2)] % P, fr[o + 6 * (w % 2) + 2 * (w // 2) + 1] % P) for w in range(6)]
-
-    prod = None
-    for h in range(2):
-        half = [0] * GC.FRAME2
-        n = 4 * PS.ML1_SLOTS
-        half[:n] = frame[h * n:(h + 1) * n]
-        simulate(pg["ml1_4"], half, consts)
-        for s in range(4):
-            f = f12(half, PS.ML1_SLOTS * s + PS.ML1_F)
-            prod = f if prod is None else oracle.f12_mul(prod, f)
-    assert f12(shared, PS.ML1_F) == prod

@@ -31,8 +31,6 @@ X_ABS = 0xD201000000010000
 FRAME = 256
 FRAME2 = 380   # frame of the 2-set programs (kernels/k_pset.hip, CoopLdsN<COOP_FRAME2>; 2 waves/SIMD)
 FRAME3 = 640   # frame of the 3-set programs (CoopLdsN<COOP_FRAME3>)
-FRAME4S = 288  # frame of the shared 4-pair Miller loop (k_mlns<4>, CoopLdsN<COOP_FRAME4S>; 10 waves / CU)
-FRAME8S = 512  # frame of the shared 8-pair Miller loop (k_mlns<8>, CoopLdsN<COOP_FRAME8S>; 6 waves / CU)
 MONT_R = 1 << 384
 
 # "fin" frame registers
@@ -487,17 +485,11 @@ def build_all():
                                  S=2, prefix="pset2")
     progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME3, psi, iso, G1X, G1Y,
                                  S=3, prefix="pset3")
-    # single-pair Miller loops of the aggregated-signature path (k_mln): 1 or 2 sets
-    # per wavefront in the 256-slot frame, 4 sets in the 380-slot frame (2 waves / SIMD)
+    # single-pair Miller loops of the aggregated-signature path as cooperative programs
+    # (k_mln, the packings tests force; the default is the SIMT k_mlq / k_mlf): 1 or 2 sets
+    # per wavefront in the 256-slot frame
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=2))
-    progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, S=4))
-    # the shared 4-pair loop in the smallest frame it fits without extra steps (747
-    # steps at 288 slots as at 380): its LDS sets the occupancy of the k_mlns<4> launch
-    progs.append(gen_pset.build_ml1_shared(consts, T, miller_dbl, miller_add, X_ABS, FRAME4S, S=4))
-    # eight pairs sharing f: 1133 steps (141.6 per set against 186.8 for ml1s_4) in a
-    # 512-slot frame ($BLS_ML_SHARE=8)
-    progs.append(gen_pset.build_ml1_shared(consts, T, miller_dbl, miller_add, X_ABS, FRAME8S, S=8))
     return progs, consts
 
 

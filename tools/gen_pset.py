@@ -563,33 +563,6 @@ ML1_SLOTS = 19                 # per packed set: RP 0..2 (G1 Jacobian), HQ 3..6 
 ML1_RP, ML1_HQ, ML1_F = 0, 3, 7
 
 
-def build_ml1_shared(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=4, prefix="ml1s"):
-    """f = prod_s ML(RP_s, HQ_s) for S sets of one product domain (a chunk or a
-    request) packed in one wavefront: the S pairs share f's squarings and fold their
-    lines in a product tree (miller_loop_multi), as blst's multi-pairing does.  Same
-    frame as build_ml1's S-set program; the product lands in set 0's F slots."""
-    assert S % 2 == 0
-    c = Circuit(f"{prefix}_{S}", consts)
-    t = T(c)
-    pairs = []
-    for s in range(S):
-        o = ML1_SLOTS * s
-        X, Y, Z = (Circuit.inp(o + ML1_RP + k) for k in range(3))
-        pz3 = c.mat(c.mul(c.mat(c.mul(Z, Z)), Z))
-        pxz = c.mat(c.mul(X, Z))
-        pairs.append((t.f2(o + ML1_HQ), t.f2(o + ML1_HQ + 2), pxz, Y, pz3))
-    f = miller_loop_multi(t, pairs, miller_dbl, miller_add, X_ABS)
-    for k in range(2):
-        for j in range(3):
-            for i in range(2):
-                c.out(ML1_F + 6 * k + 2 * j + i, f[k][j][i])
-    live = set()
-    for s in range(S):
-        o = ML1_SLOTS * s
-        live |= set(range(o, o + ML1_F))
-    return schedule(c, FRAME, live)
-
-
 def build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1, prefix="ml1"):
     """f_s = ML(RP_s, HQ_s) for S sets packed in one wavefront (set s at slot offset
     ML1_SLOTS * s): one pair per set, the signature side of the batch equation is
