@@ -163,7 +163,7 @@ __device__ __forceinline__ uint32_t k20p_limb(int i) {  // 2^20 * p, 13 limbs
 }
 
 // (sum + extra) mod p of the accumulator as a value in [0, 3p) (the interpreter's
-// lazy representation); extra < 2^20 (the +1s of the negated terms, see coop_lin)
+// lazy representation); extra < 2^20 (the |c| of the negated terms, see coop_lin)
 __device__ __forceinline__ Fp acc_reduce(Acc13 a, uint32_t extra) {
   uint32_t k20p[13];
 #pragma unroll
@@ -210,59 +210,40 @@ __device__ __forceinline__ int coop_wave_max_terms(int n) {
 }
 
 // sum_k cf[k] * slot[refs[k]] mod p over n <= 8 terms.  refs index the block's LDS
-// slot array (frame, then the constant bank at COOP_FRAME).  Each term is added
-// branch-free (up to the wave's largest n):
-// x * |c| (only when some lane of the wave has |c| != 1), then the two's-complement
-// add a + (x ^ mask) (mask = ~0 for c < 0); the +1 of each negation is folded into
-// the reduction bias.  Loop bounds and the multiply test are wave-uniform.
+// slot array (frame, then the constant bank at COOP_FRAME).  Branch-free up to the
+// wave's largest n (loop bound wave-uniform; a lane's unused term has coefficient 0):
+// each term is 12 multiply-adds of its limbs, complemented for c < 0, by |c| into 64-bit
+// limb columns (8 x 2^32 x 2^15 < 2^50: no carries until the end), then one carry pass.
+// A negated term adds |c| (2^384 - 1 - x) = -|c| x + |c| (2^384 - 1): the 2^384 part
+// leaves limb 12, the -|c| goes to the reduction bias.  (Round 3 formed every product
+// x |c| as a 13-limb number and added it with a carry chain: ~62 instructions per term
+// against ~26 here.)
 __device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n, const LdsU4* slots) {
   if (__all(n == 1 && cf[0] == 1)) return lds_load_fp(slots, refs[0]);
   const int nmax = coop_wave_max_terms(n);
-  Acc13 acc;
+  uint64_t col[12];
 #pragma unroll
-  for (int i = 0; i < 13; ++i) acc.l[i] = 0;
-  uint32_t negs = 0;
+  for (int i = 0; i < 12; ++i) col[i] = 0;
+  uint32_t negs = 0;  // sum of |c| over the negated terms
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     if (k >= nmax) break;
-    if (k < n) {
-      const int c = cf[k];
-      const uint32_t mask = c < 0 ? 0xffffffffu : 0u;
-      const uint32_t m = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
-      negs += mask & 1u;
-      const Fp x = lds_load_fp(slots, refs[k]);
-      uint32_t t[13];
-      if (__any(m != 1u)) {
-        // 12 independent 32x32 products, then one carry chain
-        uint64_t pr[12];
+    const int c = k < n ? cf[k] : 0;
+    const uint32_t mask = c < 0 ? 0xffffffffu : 0u;
+    const uint32_t m = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
+    negs += mask & m;
+    const Fp x = lds_load_fp(slots, refs[k]);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) pr[i] = (uint64_t)x.l[i] * m;
-        uint32_t hs[12], ls[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          ls[i] = (uint32_t)pr[i];
-          hs[i] = (uint32_t)(pr[i] >> 32);
-        }
-        uint32_t mid[12];
-        mid[0] = ls[0];
-#pragma unroll
-        for (int i = 1; i < 12; ++i) mid[i] = ls[i];
-        uint32_t c12 = asm_add11_shift(mid, hs);  // mid[i] += hs[i-1], i = 1..11; returns hs[11] + carry
-#pragma unroll
-        for (int i = 0; i < 12; ++i) t[i] = mid[i] ^ mask;
-        t[12] = c12 ^ mask;
-      } else if (__any(mask != 0u)) {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) t[i] = x.l[i] ^ mask;
-        t[12] = mask;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) t[i] = x.l[i];
-        t[12] = 0u;
-      }
-      asm_acc_add13(acc.l, t);
-    }
+    for (int i = 0; i < 12; ++i) col[i] += (uint64_t)(x.l[i] ^ mask) * m;
   }
+  Acc13 acc;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    acc.l[i] = (uint32_t)col[i];
+    col[i + 1] += col[i] >> 32;
+  }
+  acc.l[11] = (uint32_t)col[11];
+  acc.l[12] = (uint32_t)(col[11] >> 32) - negs;  // two's complement: the -|c| 2^384 of the negated terms
   return acc_reduce(acc, negs);
 }
 

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
-"""Time the cooperative programs on cuda:0: us per step at 1 / 64 / 1024 tasks, and
-per-step s_memtime stamps of one run split by step kind (product steps vs
-linear-combination steps)."""
+"""Time the cooperative programs on cuda:0: us per step at 1 / 1024 tasks, and the
+per-step s_memtime stamps of one run (step start, compute done): how much of a step
+is the lanes' compute (operand gathers, product) and how much the write-back and the
+wave sync.  Program names as in lodestar_amd/_native/coop_programs.json.
+
+    python tools/coop_probe.py [name:reps ...]
+"""
 import json
 import sys
 from pathlib import Path
@@ -9,30 +13,25 @@ from pathlib import Path
 import numpy as np
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-sys.path.insert(0, str(Path(__file__).resolve().parent))
-import gen_coop  # noqa: E402
 from lodestar_amd.native import GpuContext  # noqa: E402
 
-progs, _ = gen_coop.build_all()
-kinds = {p.name: [any(op.kind == 1 for op in st) for st in p.steps] for p in progs}
+ROOT = Path(__file__).resolve().parent.parent
+progs = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
 with GpuContext(0) as g:
     out = {}
-    names = sys.argv[1:] or ["fin_fmul:200", "pset3_dbl_all:100", "pset3_add_1111:100", "pset3_phase2:3",
-                             "pset3_ml2:3", "fin_fe2:2"]
+    names = sys.argv[1:] or ["pset_dbl_all:100", "pset_ml2:3", "fin_fe2:2", "fin_fe1:2", "pset_prep:3"]
     for item in names:
         name, reps = item.split(":")[0], int(item.split(":")[1])
-        for blocks in (1, 1024, 3072):
+        n_steps = progs[name]["steps"]
+        for blocks in (1, 1024):
             us, ms = g.coop_probe(name, blocks, reps)
             out[f"{name}@{blocks}"] = {"us_per_step": round(us, 3), "ms_per_run": round(ms / reps, 3)}
-        k = np.array(kinds[name])
-        _, _, st = g.coop_probe(name, 1, 1, 2 * len(k) + 1)
-        st = st.astype(np.int64)  # s_memtime: shader-clock cycles; 2 stamps per step
+        _, _, st = g.coop_probe(name, 1, 1, 2 * n_steps + 1)
+        st = st.astype(np.int64)  # s_memtime (100 MHz constant clock on gfx9): 2 stamps per step
         start, comp = st[0:-1:2], st[1::2]
         total = np.diff(st[0::2])
         compute = comp - start
-        out[f"{name}:stamps"] = {
-            "mul_steps": int(k.sum()), "mul_total": float(total[k].mean()) if k.any() else 0,
-            "mul_compute": float(compute[k].mean()) if k.any() else 0,
-            "lin_steps": int((~k).sum()), "lin_total": float(total[~k].mean()) if (~k).any() else 0,
-            "lin_compute": float(compute[~k].mean()) if (~k).any() else 0}
+        out[f"{name}:stamps"] = {"steps": n_steps, "mul_steps": progs[name]["mul_steps"],
+                                 "total_ticks_mean": float(total.mean()), "compute_ticks_mean": float(compute.mean()),
+                                 "total_ticks_p10_p50_p90": [float(np.percentile(total, q)) for q in (10, 50, 90)]}
     print(json.dumps(out, indent=1))

@@ -42,6 +42,10 @@ if [ -n "$LAT" ]; then
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$O/lat -o run --output-format csv -- python3 $R/tools/lat_probe.py --runs 10 > $R/$O/lat.log 2>&1) || { tail -20 $O/lat.log; exit 1; }
   grep p50_ms $O/lat.log | tail -1
 fi
+if [ -n "$COOP" ]; then
+  timeout -k 10 240 python -u tools/coop_probe.py > $O/coop_probe.json 2> $O/coop_probe.err || { echo "coop probe failed"; tail -5 $O/coop_probe.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/coop_probe.json'));[print(k,v) for k,v in d.items()]"
+fi
 if [ -n "$PMC" ]; then
   cd /tmp && export TMPDIR=/tmp
   R=$GRAFT_REPO_ROOT
