@@ -116,9 +116,10 @@ def sigagg_of(n_sets: int) -> bool:
 
 def mlf_products(wm: dict, shape: int | None) -> float:
     """Fp products per item of k_mlf for a pass shape (items per lane in bits 8-15 of
-    bls_stats.pass_shape: 1, 2 or 4 pairs share f's squarings; None = 2)."""
+    bls_stats.pass_shape: 1, 2 or 4 pairs share f's squarings, 3 one pair over two lanes --
+    the products of one pair per f, the duplicated f.c1 l3 term not counted; None = 2)."""
     per_lane = (shape >> 8) & 0xFF if shape is not None else 2
-    key = {1: "ml_f_one", 4: "ml_f_quad"}.get(per_lane, "ml_f_pair")
+    key = {1: "ml_f_one", 3: "ml_f_one", 4: "ml_f_quad"}.get(per_lane, "ml_f_pair")
     return wm.get(key, wm["ml_f_pair"])
 
 
@@ -175,7 +176,7 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None
         wm["k_pre"], ps, merged / n_sets)
 
 
-PMC_FILE = "r03_pmc_pass32.json"   # the committed counter summary the bench line cites
+PMC_FILE = "r04_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
 VERIFY_KERNELS = ("k_pk", "k_pre", "k_chain", "k_gsum", "k_vset", "k_mlq", "k_mlf", "k_msm", "k_status", "k_fprod",
                   "k_chunk_coop", "k_indiv_coop", "k_fold", "k_exact", "k_uset", "k_gsum1", "k_mln")
 
@@ -188,19 +189,24 @@ def committed_pmc():
     if not p.exists():
         return None
     d = json.loads(p.read_text())
-    out, total = {}, 0
+    out, total, vset = {}, 0, 0.0
+    sets = d.get("sets_per_pass")
     for name, v in d.get("kernels", {}).items():
         if not name.startswith(VERIFY_KERNELS):
             continue
         total += v.get("hbm_bytes_per_launch", 0)
+        if sets and "SQ_INSTS_VALU" in v:
+            vset += v["SQ_INSTS_VALU"] / sets  # per dispatch: every wave's VALU instructions
         wc = v.get("SQ_WAVE_CYCLES")
-        if name.startswith(("k_chain", "k_mlf", "k_mlq", "k_pre")) and wc:
+        if name.startswith(("k_chain", "k_mlf", "k_mlq", "k_mlx", "k_pre")) and wc:
             out[name] = {"valu_issue_frac": round(v["SQ_ACTIVE_INST_VALU"] / wc, 3),
                          "waves_per_simd": v.get("waves_per_simd"), "valu_busy": v.get("valu_busy"),
                          "valu_insts_per_wave": round(v["SQ_INSTS_VALU"] / max(1.0, v["SQ_WAVES"])),
+                         "valu_wave_insts_per_set": round(v["SQ_INSTS_VALU"] / sets) if sets else None,
                          "hbm_bytes_per_launch": v.get("hbm_bytes_per_launch")}
-    return {"source": f"profiles/{PMC_FILE} (copied, not measured by this run)", "kernels": out,
-            "hbm_bytes_per_pass": total, "note": next(iter(d.get("kernels", {}).values()), {}).get("note")}
+    return {"source": f"profiles/{PMC_FILE} (copied, not measured by this run)", "shape": d.get("shape"),
+            "kernels": out, "hbm_bytes_per_pass": total, "sets_per_pass": sets,
+            "valu_wave_insts_per_set": round(vset) if sets else None}
 
 
 def interop_sk(i: int) -> bytes:
@@ -737,8 +743,10 @@ def main() -> None:
     ap.add_argument("--table-keys", type=int, default=1 << 20, help="device pubkey table of the cfg3 / cfg4 records")
     ap.add_argument("--cfg4-sets", type=int, default=125_000,
                     help="sets of this GPU's cfg4 slice (1M sets over 8 GPUs by call)")
-    ap.add_argument("--cfg4-contexts", type=int, default=4, help="contexts of the cfg4 sub-record")
-    ap.add_argument("--cfg4-calls-per-pass", type=int, default=32, help="128-set calls per pass of the cfg4 sub-record")
+    # the cfg4 slice's knee (profiles/r04_sweep_cfg4.json: 4 x 32 0.47M, 8 x 32 0.85M, 12 x 32 1.06M,
+    # 8 x 64 1.49M, 12 x 64 1.38M non-batchable sets/s -- 12 x 64 leaves contexts short of a second pass)
+    ap.add_argument("--cfg4-contexts", type=int, default=8, help="contexts of the cfg4 sub-record")
+    ap.add_argument("--cfg4-calls-per-pass", type=int, default=64, help="128-set calls per pass of the cfg4 sub-record")
     ap.add_argument("--no-merged-check", action="store_true",
                     help="one final exponentiation per chunk only (BLS_DEBUG_NO_MERGED_CHECK)")
     ap.add_argument("--stand-in", default=None, metavar="MODULE:FACTORY",

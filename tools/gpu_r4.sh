@@ -46,6 +46,23 @@ if [ -n "$COOP" ]; then
   timeout -k 10 240 python -u tools/coop_probe.py > $O/coop_probe.json 2> $O/coop_probe.err || { echo "coop probe failed"; tail -5 $O/coop_probe.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/coop_probe.json'));[print(k,v) for k,v in d.items()]"
 fi
+if [ -n "$SOLO" ]; then
+  # one 32-call pass (32,768 cfg2 sets) alone under a kernel trace (+ SQ counters), per
+  # SOLO label "name:VAR=v,..." separated by ";"
+  R=$GRAFT_REPO_ROOT
+  for ab in $(echo "$SOLO" | tr ';' ' '); do
+    label=${ab%%:*}; vars=$(echo "${ab#*:}" | tr ',' ' ')
+    PB="python3 $R/bench.py --probe-only --inflight 1 --calls-per-pass 32 --steps 1 --warmup 1"
+    (cd /tmp && export TMPDIR=/tmp && env $vars timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$O/solo_$label -o run --output-format csv -- $PB > $R/$O/solo_$label.log 2>&1) || { tail -20 $O/solo_$label.log; exit 1; }
+    (cd /tmp && export TMPDIR=/tmp && env $vars timeout -s KILL 120 rocprofv3 --pmc ${SOLO_PMC:-SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE} -d $R/$O/solo_${label}_pmc -o run --output-format csv -- $PB > $R/$O/solo_${label}_pmc.log 2>&1) || { tail -20 $O/solo_${label}_pmc.log; exit 1; }
+    python3 -c "
+import csv,glob
+f=glob.glob('$O/solo_$label/**/*kernel_stats.csv',recursive=True)[0]
+for r in csv.DictReader(open(f)):
+  n=r['Name'].split('(')[0].replace('void ','')
+  if n.startswith(('k_ml','k_chain','k_pre','k_msm','k_gsum')): print('$label', n, r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')"
+  done
+fi
 if [ -n "$PMC" ]; then
   cd /tmp && export TMPDIR=/tmp
   R=$GRAFT_REPO_ROOT
