@@ -73,7 +73,8 @@ typedef struct bls_stats {
   uint32_t merged_check;       /* 0 not run, 1 passed (per-chunk checks skipped), 2 failed (chunks checked) */
   uint32_t n_ml_units;         /* Miller-loop units (chunk x shared signing root pairings), 0 = one per set */
   uint32_t pass_shape;         /* how the aggregated path ran (0 on the per-set path): bit 0 the merged signature
-                                  sum by Pippenger MSM; bits 8-15 items per lane of the f side of the Miller loops */
+                                  sum by Pippenger MSM; bits 8-15 items per lane of the f side of the Miller loops
+                                  (1, 2, 4; 3 = one item per two lanes) */
 } bls_stats;
 
 typedef struct bls_gpu_ctx bls_gpu_ctx;
@@ -307,8 +308,8 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
 /* Test / bench hook: the merged signature sum as a Pippenger multi-scalar
  * multiplication (kernels/k_msm.hip) whatever $BLS_MSM says. */
 #define BLS_DEBUG_MSM 64u
-/* Test / bench hook: items per lane of the Miller loops' f side (1, 2 or 4; 0 = by the
- * process's sets in flight). */
+/* Test / bench hook: items per lane of the Miller loops' f side (1, 2 or 4; 3 = one item
+ * per two lanes; 0 = by the process's sets in flight). */
 #define BLS_DEBUG_MLF_PL(n) ((uint32_t)(n) << 12)
 #define BLS_DEBUG_MLF_PL_MASK 0x7000u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);

@@ -74,9 +74,8 @@ struct CoopEnv {
   const Fp* consts;
   uint32_t n_consts;
   CoopProg fin_fmul, fin_fe1, fin_fe2;
-  // per-set frame (tools/gen_pset.py, kernels/k_pset.hip)
-  CoopProg pset_prep, pset_dbl_r, pset_dbl_all, pset_add_x, pset_add_r, pset_add_xr, pset_phase2, pset_norm2,
-      pset_affine2, pset_ml2;
+  // per-set frame (tools/gen_pset.py, kernels/k_pset.hip; the r chains run beside them)
+  CoopProg pset_prep, pset_dbl_all, pset_add_x, pset_phase2, pset_norm2, pset_affine2, pset_ml2;
   CoopPsetN packed[2];  // [0]: 2 sets per wavefront, [1]: 3 sets
   // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln, the
   // cooperative packings tests force): 1 or 2 sets per wavefront (COOP_FRAME)
@@ -376,10 +375,11 @@ __device__ __forceinline__ void coop_stage_consts(const CoopEnv& env, Fp* cbank)
   __syncthreads();
 }
 
-// lane 0 inverts frame[in] into frame[out]; the whole block waits
+// lane 0 inverts frame[in] into frame[out]; the wavefront waits (wave-local: k_pset's
+// second wavefront never joins the first's barriers after the prologue)
 __device__ __forceinline__ void coop_invert(Fp* frame, int in, int out) {
   if (threadIdx.x == 0) lds_store_fp(frame, out, fp_inv_gcd(fp_canon3(lds_load_fp(frame, in))));
-  __syncthreads();
+  coop_wave_sync();
 }
 
 // cooperative copies between global memory and the frame (n slots)

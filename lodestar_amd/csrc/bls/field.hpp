@@ -1273,6 +1273,38 @@ BLS_HD Fp12 fp12_mul_line2(const Fp12& f, const Fp2& l0, const Fp2& l2, const Fp
   return Fp12{fp6_add(t0, fp6_mul_v(t1)), c1};
 }
 
+// One f over two lanes (kernels/k_mlq.hip k_mlf2): each half computes one part of the
+// products (_prod), the halves swap their parts, and both finish alike (_join).  Host-
+// tested against fp12_sqr / fp12_mul_line with both halves run one after the other
+// (test_hostsim.py::test_fp12_pair_halves).
+//   (A + B w)^2 = (s - ab - v ab) + 2 ab w: half 0 ab = A B, half 1 s = (A + B)(A + v B)
+BLS_HD Fp6 fp12_sqr_half_prod(const Fp12& a, bool h) {
+  return fp6_mul(h ? fp6_add(a.c0, a.c1) : a.c0, h ? fp6_add(a.c0, fp6_mul_v(a.c1)) : a.c1);
+}
+BLS_HD Fp12 fp12_sqr_half_join(const Fp6& own, const Fp6& other, bool h) {
+  const Fp6 ab = h ? other : own, s = h ? own : other;
+  return Fp12{fp6_sub(fp6_sub(s, ab), fp6_mul_v(ab)), fp6_add(ab, ab)};
+}
+//   f (l0 + l2 w^2 + l3 w^3): half 0 aa = f.c0 (l0 + l2 v), half 1 t = (f.c0 + f.c1)(l0 +
+//   (l2 + l3) v); bb = f.c1 l3 v = (xi c2 l3, c0 l3, c1 l3) of f.c1: half 0 c2 l3, half 1
+//   c0 l3, both c1 l3 (q)
+struct LineHalf {
+  Fp6 m;
+  Fp2 p, q;
+};
+BLS_HD LineHalf fp12_line_half_prod(const Fp12& f, const Fp2& l0, const Fp2& l2, const Fp2& l3, bool h) {
+  LineHalf r;
+  r.m = fp6_mul_01(h ? fp6_add(f.c0, f.c1) : f.c0, l0, h ? fp2_add(l2, l3) : l2);
+  r.p = fp2_mul(h ? f.c1.c0 : f.c1.c2, l3);
+  r.q = fp2_mul(f.c1.c1, l3);
+  return r;
+}
+BLS_HD Fp12 fp12_line_half_join(const LineHalf& own, const Fp6& m_other, const Fp2& p_other, bool h) {
+  const Fp6 aa = h ? m_other : own.m, t = h ? own.m : m_other;
+  const Fp6 bb = Fp6{fp2_mul_xi(h ? p_other : own.p), h ? own.p : p_other, own.q};
+  return Fp12{fp6_add(aa, fp6_mul_v(bb)), fp6_sub(fp6_sub(t, aa), bb)};
+}
+
 BLS_HD Fp12 fp12_inv(const Fp12& a) {
   Fp6 n = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
   Fp6 ni = fp6_inv(n);

@@ -180,6 +180,65 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_mlf2: the f side with two lanes per item, for few sets in flight (a pass alone: its
+// 32,768 items run as 1,024 wavefronts, one per SIMD, instead of 512, each with half of
+// the f chain's products).  Lanes 2k and 2k + 1 hold the same f; per step each computes
+// one of the squaring's two Fp6 products and one of the line's two mul_by_01 products
+// (plus one of the Fp2 products of f.c1 l3, and both the third), swaps its products with
+// its partner (DPP quad_perm [1,0,3,2]: one move per word), and both finish the step --
+// 39 Fp products per lane per doubling step instead of 75 (field.hpp fp12_sqr_half_* /
+// fp12_line_half_*).  Same f as ml_f(.., 1) (test_gpu_parity runs every shape).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ Fp pair_swap(const Fp& a) {
+  Fp r;
+#pragma unroll
+  for (int w = 0; w < 12; ++w) r.l[w] = pair_swap(a.l[w]);
+  return r;
+}
+__device__ __forceinline__ Fp2 pair_swap(const Fp2& a) { return Fp2{pair_swap(a.c0), pair_swap(a.c1)}; }
+__device__ __forceinline__ Fp6 pair_swap(const Fp6& a) { return Fp6{pair_swap(a.c0), pair_swap(a.c1), pair_swap(a.c2)}; }
+
+__device__ __forceinline__ Fp12 sqr12_pair(const Fp12& a, bool h) {
+  const Fp6 m = fp12_sqr_half_prod(a, h);
+  return fp12_sqr_half_join(m, pair_swap(m), h);
+}
+
+__device__ __forceinline__ Fp12 mul_line12_pair(const Fp12& f, const Fp2& l0, const Fp2& l2, const Fp2& l3, bool h) {
+  const LineHalf own = fp12_line_half_prod(f, l0, l2, l3, h);
+  return fp12_line_half_join(own, pair_swap(own.m), pair_swap(own.p), h);
+}
+
+template <int W>
+__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlf2(
+    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, const uint32_t* L, uint32_t stride,
+    const uint32_t* items) {
+  const uint32_t t = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  const uint32_t k = t >> 1;
+  const bool h = (t & 1u) != 0u;
+  // both lanes of a pair take the same exits: the partner of every swap is active
+  if (k >= count) return;
+  const uint32_t i = items ? items[k] : first + k;
+  if (!ml_live(b, i, units_paired)) return;
+  Fp12 f = fp12_one();
+  int e = 0;
+  const uint64_t X = BLS_X_ABS;
+  for (int bit = 62; bit >= 0; --bit) {
+    if (bit != 62) f = sqr12_pair(f, h);
+    const int adds = (int)((X >> bit) & 1ull);
+    for (int a = 0; a <= adds; ++a) {
+      Fp2 l0, l2, l3;
+      load_line(L, stride, k, e, l0, l2, l3);
+      f = mul_line12_pair(f, l0, l2, l3, h);
+      ++e;
+    }
+  }
+  if (!h) b.f[i] = fp12_conj(f);
+}
+
 // line buffer words for a launch of `count` items (stride padded to a wavefront)
 size_t mlq_line_words(uint32_t count) {
   const size_t stride = ((size_t)count + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
@@ -190,31 +249,26 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
                          hipStream_t s, const uint32_t* items) {
   if (count == 0) return hipSuccess;
   const uint32_t stride = (count + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
-  // k_mlq at one wavefront per SIMD (256 VGPRs, no spills around the products) by default:
-  // +3 % at 12 x 16 over two (1,088 B of scratch per lane), profiles/r03_ab_mlq_mlf.json;
-  // $BLS_MLQ_WAVES=2 restores two
-  static const int wq = [] {
-    const char* e = getenv("BLS_MLQ_WAVES");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
-  static const int wf = [] {
-    const char* e = getenv("BLS_MLF_WAVES");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
+  // k_mlq / k_mlf at one wavefront per SIMD (512 registers, no spills around the products:
+  // +3 % at 12 x 16 over two per SIMD, profiles/r03_ab_mlq_mlf.json)
   const uint32_t up = (own_only || items) ? 0u : 1u;
-  if (wq == 1) k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
-  else k_mlq<2><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
+  k_mlq<1><<<bls_grid_for(count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
   // Items per k_mlf lane: 2 shares f's squarings between two pairs (fewer instructions:
   // the rate when the device is VALU-bound), 1 halves the f chain (the rate when few sets
   // are in flight and the pass latency sets it): 2.22M vs 2.00M sets/s with 64k sets in
   // flight, 2.76M vs 2.90M with 128k (profiles/r03_ab_mlq_mlf.json).  By default the
   // process's sets in flight (every context's verify call, bls_sets_in_flight) pick:
   // 2 above $BLS_MLF_PL2_MIN (default 98,304) sets, 4 above $BLS_MLF_PL4_MIN (200,000:
-  // 3.55M vs 3.41M sets/s at 12 x 22), else 1.  $BLS_MLF_PER_LANE = 1, 2 or 4 fixes it.
+  // 3.55M vs 3.41M sets/s at 12 x 22), else 1.  $BLS_MLF_PER_LANE = 1, 2, 4 or 3 (MLF_PAIR)
+  // fixes it.
+  // Below $BLS_MLF_PAIR_MAX (32,768) sets in flight: two lanes per item (k_mlf2, MLF_PAIR).
   const uint32_t per_lane = b.mlf_pl ? b.mlf_pl : mlf_per_lane();
+  if (per_lane == MLF_PAIR) {
+    k_mlf2<1><<<bls_grid_for(2 * count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
+    return hipGetLastError();
+  }
   const uint32_t lanes = (count + per_lane - 1) / per_lane;
-  if (wf == 2) k_mlf<2><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
-  else k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
+  k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
   return hipGetLastError();
 }
 
@@ -222,7 +276,11 @@ uint32_t mlf_per_lane() {
   static const uint32_t fixed = [] {
     const char* e = getenv("BLS_MLF_PER_LANE");
     const int v = e ? atoi(e) : 0;
-    return (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
+    return (v == 1 || v == 2 || v == 4 || v == (int)MLF_PAIR) ? (uint32_t)v : 0u;
+  }();
+  static const uint64_t pair_max = [] {
+    const char* e = getenv("BLS_MLF_PAIR_MAX");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 32768ull;
   }();
   static const uint64_t pl2_min = [] {
     const char* e = getenv("BLS_MLF_PL2_MIN");
@@ -234,5 +292,5 @@ uint32_t mlf_per_lane() {
   }();
   if (fixed) return fixed;
   const uint64_t k = bls_sets_in_flight();
-  return k > pl4_min ? 4u : (k > pl2_min ? 2u : 1u);
+  return k > pl4_min ? 4u : (k > pl2_min ? 2u : (k > pair_max ? 1u : MLF_PAIR));
 }

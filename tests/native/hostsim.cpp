@@ -181,6 +181,21 @@ void hs_fp12_frob2(const uint8_t* a, uint8_t* out) { wr_fp12(fp12_frob2(rd_fp12(
 void hs_fp12_mul_line(const uint8_t* f, const uint8_t* l0, const uint8_t* l2, const uint8_t* l3, uint8_t* out) {
   wr_fp12(fp12_mul_line(rd_fp12(f), rd_fp2(l0), rd_fp2(l2), rd_fp2(l3)), out);
 }
+// one f over two lanes (k_mlf2): both halves' products, swapped, joined by each half;
+// out: half 0's result then half 1's (576 bytes each)
+void hs_fp12_sqr_pair(const uint8_t* a, uint8_t* out) {
+  const Fp12 x = rd_fp12(a);
+  const Fp6 m0 = fp12_sqr_half_prod(x, false), m1 = fp12_sqr_half_prod(x, true);
+  wr_fp12(fp12_sqr_half_join(m0, m1, false), out);
+  wr_fp12(fp12_sqr_half_join(m1, m0, true), out + 576);
+}
+void hs_fp12_mul_line_pair(const uint8_t* f, const uint8_t* l0, const uint8_t* l2, const uint8_t* l3, uint8_t* out) {
+  const Fp12 x = rd_fp12(f);
+  const Fp2 a = rd_fp2(l0), b = rd_fp2(l2), c = rd_fp2(l3);
+  const LineHalf h0 = fp12_line_half_prod(x, a, b, c, false), h1 = fp12_line_half_prod(x, a, b, c, true);
+  wr_fp12(fp12_line_half_join(h0, h1.m, h1.p, false), out);
+  wr_fp12(fp12_line_half_join(h1, h0.m, h0.p, true), out + 576);
+}
 void hs_fp12_mul_line2(const uint8_t* f, const uint8_t* l, const uint8_t* m, uint8_t* out) {
   wr_fp12(fp12_mul_line2(rd_fp12(f), rd_fp2(l), rd_fp2(l + 96), rd_fp2(l + 192), rd_fp2(m), rd_fp2(m + 96),
                          rd_fp2(m + 192)),

@@ -185,6 +185,23 @@ def test_fp12_mul_line2(hostsim):
         assert o1.raw == o2.raw
 
 
+def test_fp12_pair_halves(hostsim):
+    """One f over two lanes (k_mlf2, field.hpp fp12_sqr_half_* / fp12_line_half_*): each
+    half's products, swapped with the other's, give both halves the full square and the
+    full sparse line product."""
+    rng = random.Random(14)
+    o1, o2 = _buf(576), _buf(2 * 576)
+    for _ in range(20):
+        f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+        hostsim.hs_fp12_sqr(f12b(f), o1)
+        hostsim.hs_fp12_sqr_pair(f12b(f), o2)
+        assert o2.raw[:576] == o2.raw[576:] == o1.raw
+        ls = [(rng.randrange(P), rng.randrange(P)) for _ in range(3)]
+        hostsim.hs_fp12_mul_line(f12b(f), f2b(ls[0]), f2b(ls[1]), f2b(ls[2]), o1)
+        hostsim.hs_fp12_mul_line_pair(f12b(f), f2b(ls[0]), f2b(ls[1]), f2b(ls[2]), o2)
+        assert o2.raw[:576] == o2.raw[576:] == o1.raw
+
+
 def test_hash_to_g2_golden(hostsim, golden):
     o = _buf(192)
     for v in golden["hash_to_g2"]:

@@ -36,6 +36,18 @@ def _inv(v):
     return pow(v, P - 2, P) if v else 0
 
 
+def _jac(pt, z):
+    """affine G1 point -> Jacobian (X, Y, Z) = (x z^2, y z^3, z)"""
+    return (pt[0] * z * z % P, pt[1] * z ** 3 % P, z)
+
+
+def _r_points(oracle, pk, s, rng):
+    """[s] g1 and [s] pk as the second wavefront of k_pset hands them over (Jacobian,
+    arbitrary Z)"""
+    return (_jac(oracle.E1.mul(oracle.G1, s), rng.randrange(1, P)),
+            _jac(oracle.E1.mul(pk, s), rng.randrange(1, P)))
+
+
 def test_pset_valid_set(progs, oracle):
     pg, consts = progs
     rng = random.Random(11)
@@ -45,16 +57,10 @@ def test_pset_valid_set(progs, oracle):
     pk = oracle.E1.mul(oracle.G1, sk)
     r = rng.randrange(1, 1 << 64)
     fr = _frame_for(oracle, msg, sig, pk, rng.randrange(1, P))
-    flag, in_group = PS.run_pset(pg, consts, fr, r, simulate, _inv)
+    flag, in_group = PS.run_pset(pg, consts, fr, *_r_points(oracle, pk, r, rng), simulate, _inv)
     assert not flag and in_group
     H = oracle.hash_to_g2(msg)
     assert ((fr[PS.HQ], fr[PS.HQ + 1]), (fr[PS.HQ + 2], fr[PS.HQ + 3])) == H
-    X, Y, Z = fr[PS.RG:PS.RG + 3]
-    zi = _inv(Z)
-    assert (X * zi * zi % P, Y * zi ** 3 % P) == oracle.E1.mul(oracle.G1, r)
-    X, Y, Z = fr[PS.RP:PS.RP + 3]
-    zi = _inv(Z)
-    assert (X * zi * zi % P, Y * zi ** 3 % P) == oracle.E1.mul(pk, r)
     f = [(fr[PS.F + 6 * (w % 2) + 2 * (w // 2)], fr[PS.F + 6 * (w % 2) + 2 * (w // 2) + 1]) for w in range(6)]
     assert oracle.f12_is_one(oracle.final_exponentiation(f, hard_multiple=3))
 
@@ -67,7 +73,8 @@ def test_pset_wrong_message_and_non_subgroup(progs, oracle):
     sig = oracle.E2.mul(oracle.hash_to_g2(b"\x01" * 32), sk)   # signs another message
     pk = oracle.E1.mul(oracle.G1, sk)
     fr = _frame_for(oracle, msg, sig, pk, 1)
-    flag, in_group = PS.run_pset(pg, consts, fr, rng.randrange(1, 1 << 64), simulate, _inv)
+    flag, in_group = PS.run_pset(pg, consts, fr, *_r_points(oracle, pk, rng.randrange(1, 1 << 64), rng), simulate,
+                                 _inv)
     assert not flag and in_group
     f = [(fr[PS.F + 6 * (w % 2) + 2 * (w // 2)], fr[PS.F + 6 * (w % 2) + 2 * (w // 2) + 1]) for w in range(6)]
     assert not oracle.f12_is_one(oracle.final_exponentiation(f, hard_multiple=3))
@@ -76,7 +83,7 @@ def test_pset_wrong_message_and_non_subgroup(progs, oracle):
     off = oracle.iso_map(oracle.map_to_curve_sswu(u0))
     assert not oracle.g2_in_subgroup(off)
     fr = _frame_for(oracle, msg, off, pk, 1)
-    flag, in_group = PS.run_pset(pg, consts, fr, 5, simulate, _inv)
+    flag, in_group = PS.run_pset(pg, consts, fr, *_r_points(oracle, pk, 5, rng), simulate, _inv)
     assert not in_group
 
 

@@ -170,13 +170,14 @@ def schedule(c: Circuit, frame_slots: int, reserved: set, lanes: int = LANES) ->
     import copy
     best, err = None, None
     for mode in ("asap", "alap", "list"):
-        try:
-            pg = _schedule_mode(copy.deepcopy(c), frame_slots, reserved, lanes, mode)
-        except RuntimeError as e:
-            err = e
-            continue
-        if best is None or len(pg.steps) < len(best.steps):
-            best = pg
+        for hoist in (True, False):
+            try:
+                pg = _schedule_mode(copy.deepcopy(c), frame_slots, reserved, lanes, mode, hoist)
+            except RuntimeError as e:
+                err = e
+                continue
+            if best is None or len(pg.steps) < len(best.steps):
+                best = pg
     if best is None:
         raise err
     return best
@@ -237,11 +238,14 @@ def _relevel(nodes, roots, mode):
     return order
 
 
-def _schedule_mode(c: Circuit, frame_slots: int, reserved: set, lanes: int, mode: str) -> Program:
+def _schedule_mode(c: Circuit, frame_slots: int, reserved: set, lanes: int, mode: str,
+                   hoist: bool = False) -> Program:
     """Level-schedule circuit `c` into steps of <= `lanes` ops over a frame of
     `frame_slots` slots.  `reserved` slots (the caller's live registers) are never
     used for temporaries.  Products of level L run in phase (L, 0); linear
-    combinations whose deepest reference has level L run in phases (L, 1, depth)."""
+    combinations whose deepest reference has level L run in phases (L, 1, depth).
+    hoist: linear combinations and outputs move into earlier steps with spare lanes
+    (_hoist_lins, _allocate)."""
     nodes = c.nodes
 
     def level_of(n: Node):
@@ -304,7 +308,37 @@ def _schedule_mode(c: Circuit, frame_slots: int, reserved: set, lanes: int, mode
             ns = phases[ph]
             for k in range(0, len(ns), lanes):
                 groups.append((ph[1] == 0, ns[k: k + lanes]))
-    return _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes)
+    if hoist:
+        groups = _hoist_lins(groups, lanes)
+    return _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes, hoist)
+
+
+def _hoist_lins(groups, lanes):
+    """Move every linear combination to the earliest step after the steps that produce
+    its operands that has a spare lane.  Half of a program's steps were linear-only
+    steps, while the product steps of the per-set programs use a quarter of the lanes:
+    a LIN op in a product step costs nothing (its lane skips the product), and a LIN
+    step that empties disappears."""
+    prod = {}
+    for r, (_, ns) in enumerate(groups):
+        for n in ns:
+            prod[n.id] = r
+    kinds = [m for m, _ in groups]
+    out = [list(ns) for _, ns in groups]
+    for r in range(len(out)):
+        if kinds[r]:
+            continue
+        keep = []
+        for n in out[r]:
+            ready = 1 + max((prod[x[1]] for x in _refs(n.a)), default=-1)
+            q = next((g for g in range(ready, r) if len(out[g]) < lanes), None)
+            if q is None:
+                keep.append(n)
+                continue
+            out[q].append(n)
+            prod[n.id] = q
+        out[r] = keep
+    return [(kinds[r], out[r]) for r in range(len(out)) if out[r]]
 
 
 def _list_groups(nodes, lanes):
@@ -348,7 +382,7 @@ def _list_groups(nodes, lanes):
     return groups
 
 
-def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes) -> Program:
+def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes, hoist=False) -> Program:
     last_use = {}
     tail_rank = len(groups)
 
@@ -360,10 +394,36 @@ def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes) -> Program
         for n in ns:
             note(n.a, r)
             note(n.b, r)
-    for _, v in outs:
-        note(v, tail_rank)
-    for z in zchecks:
-        note(z, tail_rank)
+    # hoisted outputs / zero-checks: into the first step after their operands' steps with
+    # a spare lane -- an output only once no later step (and no output) reads the input
+    # slot it overwrites (a step gathers before it writes, so its own step may)
+    at = {}  # index into outs + zchecks -> group
+    if hoist:
+        prod = {n.id: r for r, (_, ns) in enumerate(groups) for n in ns}
+        last_read = {}
+        for r, (_, ns) in enumerate(groups):
+            for n in ns:
+                for l in (n.a, n.b):
+                    for k in l.t:
+                        if k[0] == "in":
+                            last_read[k[1]] = r
+        out_reads = {k[1] for _, v in outs for k in v.t if k[0] == "in"}
+        load = [len(ns) for _, ns in groups]
+        items = [(slot, v) for slot, v in outs] + [(None, z) for z in zchecks]
+        for idx, (slot, v) in enumerate(items):
+            if slot is not None and slot in out_reads:
+                continue
+            ready = 1 + max((prod[x[1]] for x in _refs(v)), default=-1)
+            if slot is not None:
+                ready = max(ready, last_read.get(slot, -1))
+            q = next((g for g in range(ready, len(groups)) if load[g] < lanes), None)
+            if q is not None:
+                at[idx] = q
+                load[q] += 1
+    for idx, (_, v) in enumerate(outs):
+        note(v, at.get(idx, tail_rank))
+    for k, z in enumerate(zchecks):
+        note(z, at.get(len(outs) + k, tail_rank))
 
     free = [s for s in range(frame_slots) if s not in reserved]
     slot_of = {}
@@ -384,11 +444,20 @@ def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes) -> Program
             slot_of[n.id] = s
             busy_until[s] = last_use.get(n.id, r)
             ops.append(Op(n.kind, s, _emit(n.a, slot_of), _emit(n.b, slot_of)))
+        for idx, q in at.items():
+            if q == r:
+                if idx < len(outs):
+                    slot, v = outs[idx]
+                    ops.append(Op(OP_LIN, slot, _emit(v, slot_of)))
+                else:
+                    k = idx - len(outs)
+                    ops.append(Op(OP_LIN, ZCHECK - c.zsets[k], _emit(zchecks[k], slot_of)))
         steps.append(ops)
         if is_mul:
             n_mul += 1
-    tail = [Op(OP_LIN, slot, _emit(v, slot_of)) for slot, v in outs]
-    tail += [Op(OP_LIN, ZCHECK - zs, _emit(z, slot_of)) for z, zs in zip(zchecks, c.zsets)]
+    tail = [Op(OP_LIN, slot, _emit(v, slot_of)) for idx, (slot, v) in enumerate(outs) if idx not in at]
+    tail += [Op(OP_LIN, ZCHECK - zs, _emit(z, slot_of)) for k, (z, zs) in enumerate(zip(zchecks, c.zsets))
+             if len(outs) + k not in at]
     # the outputs land in as few steps as fit the lanes; a later output step may not
     # read a slot an earlier one wrote (outputs are written simultaneously in spirit)
     written = set()

@@ -16,17 +16,20 @@ Miller loop (one inversion per set, for H only).
 
 Scalar multiplications run left to right, one doubling program per bit for every
 chain at once (lanes in parallel) and addition programs chosen per bit by the
-kernel: the |x| bits are fixed, the r bits per set.  The r chains start from sig
-(resp. pk) for an implicit top bit 2^64 and subtract [2^64] sig (resp. pk), a pure
-doubling chain run in the same programs, so every set runs the same 64 steps.
-Additions zero-check H: an exceptional case (possible only for adversarial
-signatures off the subgroup, or with negligible probability) flags the set for the
-exact single-lane path.
+kernel: the |x| bits are fixed.  The r chains: with one set per wavefront (k_pset)
+the block's second wavefront computes RG and RP with two single-lane GLV
+multiplications while the first runs the |x| chains, and writes them into the frame
+before the Miller loop (k_pset.hip); the packed programs (S sets per wavefront,
+k_psetn) run them here, starting from g1 (resp. pk) for an implicit top bit 2^64
+and subtracting [2^64] g1 (a constant) resp. [2^64] pk, a pure doubling chain run in
+the same programs, so every set runs the same 64 steps.  Additions zero-check H: an
+exceptional case (possible only for adversarial signatures off the subgroup, or
+with negligible probability) flags the set for the exact single-lane path.
 
 Frame (slots):
   Q0 0..3  Q1 4..7  SIG 8..11 (affine)  PK 12..14 (G1 Jacobian)
   A 15..20 (cofactor chain [|x|]P)  C 21..26 (subgroup chain [|x|]sig)
-  D3 27..29 ([r + 2^64] g1)  D2 33..35 ([r + 2^64] pk)  E2 42..44 ([2^64] pk)
+  D3 27..29 ([r + 2^64] g1)  D2 33..35 ([r + 2^64] pk)  E2 42..44 ([2^64] pk)  (packed only)
   PP 45..50 (P = iso(q0) + iso(q1))  H 51..56  RG 57..59  RP 63..65
   HQ 66..69 (affine)  INV_IN 74  INV_OUT 75  DIFF 76..79 (subgroup test)
   F 80..91 (f_i)  temporaries 92..FRAME-1
@@ -151,10 +154,12 @@ def dbl(fo, p):
     d = fo.sc(fo.sub(fo.sub(fo.sqr(fo.add(X, b)), a), cc), 2)
     e = fo.sc(a, 3)
     f = fo.sqr(e)
-    x3 = fo.mat(fo.sub(f, fo.sc(d, 2)))
+    # no materialisation: the outputs (or the next doubling's operands, inside one
+    # program) take the linear combinations directly -- 4 steps instead of 6
+    x3 = fo.sub(f, fo.sc(d, 2))
     y3 = fo.sub(fo.mul(e, fo.sub(d, x3)), fo.sc(cc, 8))
-    z3 = fo.sc(fo.mul(Y, Z), 2)
-    return x3, fo.mat(y3), fo.mat(z3)
+    z3 = fo.mul(fo.sc(Y, 2), Z)
+    return x3, y3, z3
 
 
 def add_gen(fo, p, q, check=True):
@@ -174,10 +179,10 @@ def add_gen(fo, p, q, check=True):
     i = fo.sqr(fo.sc(h, 2))
     j = fo.mul(h, i)
     v = fo.mul(u1, i)
-    x3 = fo.mat(fo.sub(fo.sub(fo.sqr(r), j), fo.sc(v, 2)))
+    x3 = fo.sub(fo.sub(fo.sqr(r), j), fo.sc(v, 2))
     y3 = fo.sub(fo.mul(r, fo.sub(v, x3)), fo.sc(fo.mul(s1, j), 2))
     z3 = fo.mul(fo.sub(fo.sub(fo.sqr(fo.add(Z1, Z2)), z1z1), z2z2), h)
-    return x3, fo.mat(y3), fo.mat(z3)
+    return x3, y3, z3  # linear combinations, as dbl's
 
 
 def add_mixed(fo, p, q, check=True):
@@ -195,10 +200,10 @@ def add_mixed(fo, p, q, check=True):
     j = fo.mul(h, i)
     r = fo.sc(fo.sub(s2, Y1), 2)
     v = fo.mul(X1, i)
-    x3 = fo.mat(fo.sub(fo.sub(fo.sqr(r), j), fo.sc(v, 2)))
+    x3 = fo.sub(fo.sub(fo.sqr(r), j), fo.sc(v, 2))
     y3 = fo.sub(fo.mul(r, fo.sub(v, x3)), fo.sc(fo.mul(Y1, j), 2))
     z3 = fo.sub(fo.sub(fo.sqr(fo.add(Z1, h)), z1z1), hh)
-    return x3, fo.mat(y3), fo.mat(z3)
+    return x3, y3, z3
 
 
 def neg_pt(fo, p):
@@ -283,7 +288,11 @@ def add_program_name(prefix: str, S: int, xb: int, rmask: int) -> str:
 
 def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G1Y, S=1, prefix="pset"):
     """The per-set programs for S sets packed in one wavefront (set s at register
-    offset s * SET_SLOTS; its zero-checks carry its set index)."""
+    offset s * SET_SLOTS; its zero-checks carry its set index).  One set per wavefront
+    (S = 1, k_pset) leaves the r chains to the block's second wavefront (RG, RP written
+    into the frame before pset_ml2 by single-lane GLV multiplications): its programs
+    carry only the |x| chains, and the r bits choose nothing."""
+    r_chains = S > 1
     progs = []
     offs = [SET_SLOTS * s for s in range(S)]
     regs = set(range(0, SET_SLOTS * S))
@@ -311,10 +320,11 @@ def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G
         sig = aff(f2, o + SIG)
         sigj = (sig[0], sig[1], f2.one())
         out_jac(f2, o + C, sigj)
-        out_jac(f1, o + D3, (f1.c.const(G1X), f1.c.const(G1Y), f1.one()))
-        pk = jac(f1, o + PK)
-        for base in (D2, E2):
-            out_jac(f1, o + base, pk)
+        if r_chains:
+            out_jac(f1, o + D3, (f1.c.const(G1X), f1.c.const(G1Y), f1.one()))
+            pk = jac(f1, o + PK)
+            for base in (D2, E2):
+                out_jac(f1, o + base, pk)
 
     per_set(c, prep)
     progs.append(schedule(c, FRAME, regs))
@@ -332,8 +342,9 @@ def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G
         per_set(c, body)
         progs.append(schedule(c, FRAME, regs))
 
-    dbl_prog("dbl_r", (), (D2, E2, D3))
-    dbl_prog("dbl_all", (A, C), (D2, E2, D3))
+    if r_chains:
+        dbl_prog("dbl_r", (), (D2, E2, D3))
+    dbl_prog("dbl_all", (A, C), (D2, E2, D3) if r_chains else ())
 
     def add_prog(xb, rmask):
         c, t, f1, f2 = new(add_program_name(prefix, S, xb, rmask)[len(prefix) + 1:])
@@ -351,7 +362,7 @@ def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G
         progs.append(schedule(c, FRAME, regs))
 
     for xb in (0, 1):
-        for rmask in range(1 << S):
+        for rmask in range(1 << S if r_chains else 1):
             if xb or rmask:
                 add_prog(xb, rmask)
 
@@ -377,9 +388,9 @@ def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G
         t3 = add_gen(f2, t3, neg_pt(f2, t1))               # - t1
         hh = add_gen(f2, t3, neg_pt(f2, P))                # - P
         out_jac(f2, o + H, hh)
-        # RG = D3 - [2^64] g1 (a constant), RP = D2 - E2
-        out_jac(f1, o + RG, add_mixed(f1, jac(f1, o + D3), (c.const(G1_2_64[0]), c.const(P_MOD - G1_2_64[1]))))
-        out_jac(f1, o + RP, add_gen(f1, jac(f1, o + D2), neg_pt(f1, jac(f1, o + E2))))
+        if r_chains:  # RG = D3 - [2^64] g1 (a constant), RP = D2 - E2
+            out_jac(f1, o + RG, add_mixed(f1, jac(f1, o + D3), (c.const(G1_2_64[0]), c.const(P_MOD - G1_2_64[1]))))
+            out_jac(f1, o + RP, add_gen(f1, jac(f1, o + D2), neg_pt(f1, jac(f1, o + E2))))
         # subgroup: psi(sig) == -C (= [x] sig): (psi.x) Z^2 == X and (psi.y) Z^3 == -Y
         X, Y, Z = jac(f2, o + C)
         f2.zero(Z)                                         # [|x|] sig hit infinity: exact path
@@ -506,23 +517,23 @@ def miller_loop_multi(t, pairs, miller_dbl, miller_add, X_ABS):
     return t.conj12(f)
 
 
-def run_pset(pg, consts, frame, r, simulate, inv):
+def run_pset(pg, consts, frame, rg, rp, simulate, inv):
     """The k_pset controller (lodestar_amd/csrc/kernels/k_pset.hip) over the
-    simulator: returns the zero-check flag.  pg: name -> Program; inv: Fp inverse."""
+    simulator: returns the zero-check flag and the subgroup result.  rg, rp: [s] g1 and
+    [s] pk as G1 Jacobian triples (the kernel's second wavefront writes them into the
+    frame before pset_ml2); pg: name -> Program; inv: Fp inverse."""
     flag = simulate(pg["pset_prep"], frame, consts)
-    flag |= simulate(pg["pset_dbl_r"], frame, consts)
-    if (r >> 63) & 1:
-        flag |= simulate(pg["pset_add_r"], frame, consts)
     for i in range(62, -1, -1):
         flag |= simulate(pg["pset_dbl_all"], frame, consts)
-        xb, rb = (X_ABS_BITS >> i) & 1, (r >> i) & 1
-        if xb or rb:
-            flag |= simulate(pg["pset_add_xr" if xb and rb else ("pset_add_x" if xb else "pset_add_r")], frame, consts)
+        if (X_ABS_BITS >> i) & 1:
+            flag |= simulate(pg["pset_add_x"], frame, consts)
     flag |= simulate(pg["pset_phase2"], frame, consts)
     in_group = all(frame[DIFF + k] == 0 for k in range(4))
     flag |= simulate(pg["pset_norm2"], frame, consts)
     frame[INV_OUT] = inv(frame[INV_IN])
     flag |= simulate(pg["pset_affine2"], frame, consts)
+    frame[RG:RG + 3] = list(rg)
+    frame[RP:RP + 3] = list(rp)
     flag |= simulate(pg["pset_ml2"], frame, consts)
     return flag, in_group
 
