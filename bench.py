@@ -176,6 +176,45 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None
         wm["k_pre"], ps, merged / n_sets)
 
 
+def reference_work_per_set(reqs_per_chunk: int = 16, pairs_per_loop: int = 8) -> tuple[float, str]:
+    """SURVEY §8d's reference-algorithm work W_set (blst-style verifyMultipleSignatures,
+    no dedup, no units, no merged check): decompression + subgroup check, hash_to_G2,
+    64-bit r sig and r pk, one Miller-loop pair per set with the squarings shared by
+    `pairs_per_loop` pairs (blst's multi-pairing), and per chunk of `reqs_per_chunk`
+    sets one signature pair and one final exponentiation.  Same stage counts as
+    work_per_set (work_model.json, coop_programs.json)."""
+    pg = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
+    wm = json.loads((ROOT / "lodestar_amd" / "_native" / "work_model.json").read_text())
+    fe = pg["fin_fe1"]["mul_ops"] + pg["fin_fe2"]["mul_ops"]
+    # f side per pair: 62 Fp12 squarings (36 products) shared, 68 sparse line products (39)
+    f_pair = 62 * 36 / pairs_per_loop + 68 * 39
+    per_set = (wm["k_pre"] + wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_sig"] + wm["chain_r_pk"]
+               + wm["ml_lines"] + f_pair + wm["gsum_add"])
+    per_chunk = wm["ml_lines"] + wm["ml_f_one"] + fe
+    return per_set + per_chunk / reqs_per_chunk, (
+        f"decompress + hash_to_G2 {wm['k_pre']:.0f} + cofactor {wm['chain_h']:.0f} + subgroup "
+        f"{wm['chain_subgroup']:.0f} + r sig {wm['chain_r_sig']:.0f} + r pk {wm['chain_r_pk']:.0f} + Miller pair "
+        f"{wm['ml_lines'] + f_pair:.0f} ({pairs_per_loop} pairs per loop) + sig sum {wm['gsum_add']:.0f} + per chunk of "
+        f"{reqs_per_chunk} (signature pair + final exponentiation) {per_chunk:.0f}")
+
+
+def latency_curve(ctxs, works, points, sets_per_call: int, steps: int = 5) -> dict:
+    """sets/s and ms per call at (contexts, calls per pass) points below the headline's:
+    the call latency a host gets for the rate it asks (each point one warm-up pass, then
+    `steps` timed passes, verdicts checked)."""
+    res = {}
+    for c, k in points:
+        if c > len(ctxs) or k > len(works[0][0]):
+            continue
+        batches = [w[0][:k] for w in works[:c]]
+        timed_calls(ctxs[:c], batches, 1)
+        el, _, ok = timed_calls(ctxs[:c], batches, steps)
+        assert ok, f"latency curve {c}x{k}: verification failed"
+        res[f"{c}x{k}"] = {"sets_in_flight": c * k * sets_per_call, "sets_per_s": round(c * k * sets_per_call * steps / el, 1),
+                           "ms_per_call": round(el / steps * 1e3, 3)}
+    return res
+
+
 PMC_FILE = "r04_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
 VERIFY_KERNELS = ("k_pk", "k_pre", "k_chain", "k_gsum", "k_vset", "k_mlq", "k_mlf", "k_msm", "k_status", "k_fprod",
                   "k_chunk_coop", "k_indiv_coop", "k_fold", "k_exact", "k_uset", "k_gsum1", "k_mln")
@@ -1011,6 +1050,14 @@ def main() -> None:
                 roof["traffic_note"] = ("HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md) summed over every "
                                         "verify kernel of one pass of the committed counter run, NOT measured by this "
                                         f"run: {pmc['source']}")
+            w_ref, w_ref_note = reference_work_per_set()
+            roof["reference_equivalent"] = {
+                "fp_products_per_set": round(w_ref), "work": w_ref_note,
+                "achieved": round(per_gpu * w_ref * MADS_PER_FPM / 1e12, 4),
+                "frac": round(per_gpu * w_ref * MADS_PER_FPM / 1e12 / peak, 5),
+                "note": "SURVEY 8d: the reference algorithm's Fp products per set (blst-style, no dedup / units / "
+                        "merged check) at this line's rate -- the work the reference would do for the same sets; "
+                        "`frac` above prices the products this build executes"}
             out["p50_latency_ms_128"] = round(statistics.median(lat), 3)
             out["stage_ms"] = {k: round(float(x), 3) for k, x in zip(STAGE_NAMES, stage_ms)}
             out["roofline"] = roof
@@ -1020,6 +1067,11 @@ def main() -> None:
                 out["cpu_baseline"]["gpu_over_measured_pool"] = round(value / max(1e-9, out["cpu_baseline"]["value"]), 2)
                 out["cpu_baseline"]["gpu_over_whole_host_extrapolated"] = round(
                     value / max(1e-9, out["cpu_baseline"]["whole_host_sets_per_s_extrapolated"]), 2)
+    if world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records and K > 1:
+        curve = latency_curve(ctxs, works, ((4, 16), (8, 16)), args.sets)
+        curve[f"{inflight}x{K}"] = {"sets_in_flight": inflight * K * args.sets, "sets_per_s": round(value, 1),
+                                    "ms_per_call": out["ms_per_step"], "note": "the headline line"}
+        out["latency_curve"] = curve
     for c in ctxs:
         c.close()
     ctxs = []
