@@ -87,14 +87,18 @@ def test_pset_wrong_message_and_non_subgroup(progs, oracle):
     assert not in_group
 
 
-def test_pset2_two_sets_per_wavefront(progs, oracle):
-    """The 2-set packed programs (k_pset2): a valid set next to a set whose signature
-    signs another message; each half of the frame gets its own f_i and flags."""
+@pytest.mark.parametrize("S", [2, 3])
+def test_psetn_sets_per_wavefront(progs, oracle, S):
+    """The packed programs (k_psetn<S>, S sets per wavefront): valid sets next to a set
+    whose signature signs another message; each part of the frame gets its own f_i and
+    flags (S = 3 caught an output the scheduler hoisted into a slot the last program
+    also uses for temporaries)."""
     pg, consts = progs
-    rng = random.Random(13)
-    frame = [0] * GC.FRAME2
+    rng = random.Random(13 + S)
+    frame = [0] * (GC.FRAME2 if S == 2 else GC.FRAME3)
     rs, expect_one = [], []
-    for s, good in enumerate((True, False)):
+    for s in range(S):
+        good = s != 1
         sk = rng.randrange(1, oracle.R)
         msg = bytes(rng.randrange(256) for _ in range(32))
         sig = oracle.E2.mul(oracle.hash_to_g2(msg if good else b"\x02" * 32), sk)
@@ -104,9 +108,9 @@ def test_pset2_two_sets_per_wavefront(progs, oracle):
         frame[o:o + PS.SET_SLOTS] = fr[:PS.SET_SLOTS]
         rs.append(rng.randrange(1, 1 << 64))
         expect_one.append(good)
-    flag, in_group = PS.run_pset2(pg, consts, frame, rs, simulate, _inv)
-    assert flag == 0 and in_group == [True, True]
-    for s in range(2):
+    flag, in_group = PS.run_psetn(pg, consts, frame, rs, simulate, _inv)
+    assert flag == 0 and in_group == [True] * S
+    for s in range(S):
         o = PS.SET_SLOTS * s + PS.F
         f = [(frame[o + 6 * (w % 2) + 2 * (w // 2)], frame[o + 6 * (w % 2) + 2 * (w // 2) + 1]) for w in range(6)]
         assert oracle.f12_is_one(oracle.final_exponentiation(f, hard_multiple=3)) == expect_one[s]

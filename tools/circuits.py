@@ -395,8 +395,9 @@ def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes, hoist=Fals
             note(n.a, r)
             note(n.b, r)
     # hoisted outputs / zero-checks: into the first step after their operands' steps with
-    # a spare lane -- an output only once no later step (and no output) reads the input
-    # slot it overwrites (a step gathers before it writes, so its own step may)
+    # a spare lane -- an output only into a reserved slot (never a temporary) and once no
+    # later step (and no output) reads the input slot it overwrites (a step gathers
+    # before it writes, so its own step may)
     at = {}  # index into outs + zchecks -> group
     if hoist:
         prod = {n.id: r for r, (_, ns) in enumerate(groups) for n in ns}
@@ -411,7 +412,8 @@ def _allocate(c, groups, outs, zchecks, frame_slots, reserved, lanes, hoist=Fals
         load = [len(ns) for _, ns in groups]
         items = [(slot, v) for slot, v in outs] + [(None, z) for z in zchecks]
         for idx, (slot, v) in enumerate(items):
-            if slot is not None and slot in out_reads:
+            # (an output slot outside `reserved` may hold temporaries until the tail)
+            if slot is not None and (slot in out_reads or slot not in reserved):
                 continue
             ready = 1 + max((prod[x[1]] for x in _refs(v)), default=-1)
             if slot is not None:

@@ -541,30 +541,38 @@ def run_pset(pg, consts, frame, rg, rp, simulate, inv):
 X_ABS_BITS = 0xD201000000010000
 
 
-def run_pset2(pg, consts, frame, rs, simulate, inv):
-    """The k_pset2 controller (two sets per wavefront) over the simulator: returns the
-    zero-check flag bits and the per-set subgroup results.  frame: 2 * SET_SLOTS
-    registers + temporaries; rs: the two scalars."""
-    r0, r1 = rs
-    flag = simulate(pg["pset2_prep"], frame, consts)
-    flag |= simulate(pg["pset2_dbl_r"], frame, consts)
-    m = ((r0 >> 63) & 1) | (((r1 >> 63) & 1) << 1)
-    if m:
-        flag |= simulate(pg[add_program_name("pset2", 2, 0, m)], frame, consts)
+def run_psetn(pg, consts, frame, rs, simulate, inv):
+    """The k_psetn<S> controller (S = len(rs) sets per wavefront) over the simulator:
+    returns the zero-check flag bits and the per-set subgroup results.  frame: S *
+    SET_SLOTS registers + temporaries; rs: the sets' scalars."""
+    S = len(rs)
+    pre = f"pset{S}"
+
+    def bits(i):
+        return sum(((r >> i) & 1) << s for s, r in enumerate(rs))
+
+    flag = simulate(pg[f"{pre}_prep"], frame, consts)
+    flag |= simulate(pg[f"{pre}_dbl_r"], frame, consts)
+    if bits(63):
+        flag |= simulate(pg[add_program_name(pre, S, 0, bits(63))], frame, consts)
     for i in range(62, -1, -1):
-        flag |= simulate(pg["pset2_dbl_all"], frame, consts)
-        xb = (X_ABS_BITS >> i) & 1
-        m = ((r0 >> i) & 1) | (((r1 >> i) & 1) << 1)
+        flag |= simulate(pg[f"{pre}_dbl_all"], frame, consts)
+        xb, m = (X_ABS_BITS >> i) & 1, bits(i)
         if xb or m:
-            flag |= simulate(pg[add_program_name("pset2", 2, xb, m)], frame, consts)
-    flag |= simulate(pg["pset2_phase2"], frame, consts)
-    in_group = [all(frame[SET_SLOTS * s + DIFF + k] == 0 for k in range(4)) for s in range(2)]
-    flag |= simulate(pg["pset2_norm2"], frame, consts)
-    for s in range(2):
+            flag |= simulate(pg[add_program_name(pre, S, xb, m)], frame, consts)
+    flag |= simulate(pg[f"{pre}_phase2"], frame, consts)
+    in_group = [all(frame[SET_SLOTS * s + DIFF + k] == 0 for k in range(4)) for s in range(S)]
+    flag |= simulate(pg[f"{pre}_norm2"], frame, consts)
+    for s in range(S):
         frame[SET_SLOTS * s + INV_OUT] = inv(frame[SET_SLOTS * s + INV_IN])
-    flag |= simulate(pg["pset2_affine2"], frame, consts)
-    flag |= simulate(pg["pset2_ml2"], frame, consts)
+    flag |= simulate(pg[f"{pre}_affine2"], frame, consts)
+    flag |= simulate(pg[f"{pre}_ml2"], frame, consts)
     return flag, in_group
+
+
+def run_pset2(pg, consts, frame, rs, simulate, inv):
+    """The k_psetn<2> controller (two sets per wavefront)."""
+    return run_psetn(pg, consts, frame, rs, simulate, inv)
 
 
 # ----------------------------------------------------------------------------
