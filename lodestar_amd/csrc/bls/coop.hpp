@@ -375,8 +375,7 @@ __device__ __forceinline__ void coop_stage_consts(const CoopEnv& env, Fp* cbank)
   __syncthreads();
 }
 
-// lane 0 inverts frame[in] into frame[out]; the wavefront waits (wave-local: k_pset's
-// second wavefront never joins the first's barriers after the prologue)
+// lane 0 inverts frame[in] into frame[out]; the wavefront (the block) waits
 __device__ __forceinline__ void coop_invert(Fp* frame, int in, int out) {
   if (threadIdx.x == 0) lds_store_fp(frame, out, fp_inv_gcd(fp_canon3(lds_load_fp(frame, in))));
   coop_wave_sync();

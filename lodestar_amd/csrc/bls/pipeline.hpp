@@ -100,7 +100,10 @@ struct PipeBufs {
   uint32_t* chain_live;  // n_sets + virtual: 1 = k_mln runs this set's Miller loop
   uint8_t* chain_st;     // 4 n_sets: per set, role 0 H = O, role 1 outside G2, role 3 [r] pk = O
   G2J* rtab2;            // 15 n_sets: [1..15] sig per set (k_chain role 2's 4-bit window table)
-  G1J* rtab1;            // 15 n_sets: [1..15] pk per set (role 3)
+  G1J* rtab1;            // 15 n_sets: [1..15] pk per set (role 3); per-set path: 30 n_sets (rpts)
+  // per-set path (k_pset): RP = [s] pk at 2 i, RG = [s] g1 at 2 i + 1, made by k_pre's extra
+  // lanes (kernels/k_pre.hip); nullable
+  G1J* rpts;
   const uint32_t* gsets; // set indices of the groups being summed, group-major (k_gsum level 0)
   // Miller-loop units (sum r_i pk_i per signing root): with committee-shared
   // roots, the batchable sets of one chunk that sign the same root share ONE Miller loop

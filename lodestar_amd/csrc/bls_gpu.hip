@@ -1011,7 +1011,8 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.chain_live = sigagg ? c.take<uint32_t>(n_total) : nullptr;
     b.chain_st = sigagg ? c.take<uint8_t>(4ull * n) : nullptr;
     b.rtab2 = sigagg ? c.take<G2J>(15ull * n) : nullptr;
-    b.rtab1 = sigagg ? c.take<G1J>(15ull * n) : nullptr;
+    b.rtab1 = c.take<G1J>((sigagg ? 15ull : 30ull) * n);
+    b.rpts = sigagg ? nullptr : c.take<G1J>(2ull * n);
     gtmp[0] = sigagg ? c.take<G2J>(gtmp_cap) : nullptr;
     gtmp[1] = sigagg ? c.take<G2J>(gtmp_cap) : nullptr;
     utmp[0] = use_units ? c.take<G1J>(unit_gsum.level_off[1] + 1) : nullptr;

@@ -264,7 +264,12 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   // Below $BLS_MLF_PAIR_MAX (32,768) sets in flight: two lanes per item (k_mlf2, MLF_PAIR).
   const uint32_t per_lane = b.mlf_pl ? b.mlf_pl : mlf_per_lane();
   if (per_lane == MLF_PAIR) {
-    k_mlf2<1><<<bls_grid_for(2 * count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
+    static const int w2 = [] {
+      const char* e = getenv("BLS_MLF2_WAVES");
+      return e && atoi(e) == 1 ? 1 : 2;
+    }();
+    if (w2 == 2) k_mlf2<2><<<bls_grid_for(2 * count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
+    else k_mlf2<1><<<bls_grid_for(2 * count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
     return hipGetLastError();
   }
   const uint32_t lanes = (count + per_lane - 1) / per_lane;

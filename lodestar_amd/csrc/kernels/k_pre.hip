@@ -8,12 +8,42 @@
 
 using namespace bls;
 
-__global__ __launch_bounds__(BLS_BLOCK) void k_pre(PipeBufs b) { stage_pre(b, blockIdx.x * BLS_BLOCK + threadIdx.x); }
+// Per-set path (k_pset): RP = [s] pk and RG = [s] g1 for the set's batch scalar s (GLV:
+// curve.hpp jac_mul_glv, the scalar convention of k_chain and k_msm), two lanes per set
+// after the SSWU and decode lanes (from a wavefront boundary, so no wavefront mixes the
+// kinds).  The ~0.9 ms GLV chain runs beside the ~1.4 ms SSWU chains on other CUs: off
+// the small call's critical path (in k_pset's second wavefront it slowed the first by
+// 0.35 ms, profiles/r04_ab_pset_rpoints.json).  RP at infinity (a public key of small
+// order) sends the set to the exact path.
+__device__ __noinline__ void pre_rpts(const PipeBufs& b, uint32_t j) {
+  const uint32_t i = j >> 1, which = j & 1u;
+  if (b.pk_status[i] != BLS_OK || jac_is_inf(b.pk[i])) return;  // errors out; f_i unused
+  const G1J p = which == 0 ? b.pk[i] : jac_from_aff(g1_generator());
+  uint32_t a, c;
+  glv_split(set_scalar(b.seed, b.scalar_base + i), a, c);
+  const G1J q = jac_mul_glv<Fp>(p, a, c, b.rtab1 + 15ull * j);
+  b.rpts[j] = q;
+  if (which == 0 && jac_is_inf(q)) b.set_flag[i] = 1u;
+}
+
+__device__ __forceinline__ uint32_t pre_rpts_base(const PipeBufs& b) {
+  return (pre_lanes(b) + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
+}
+
+// two wavefronts per SIMD (the rate on the aggregated path): the GLV lanes' registers
+// must not lower it, so they spill instead
+__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_pre(PipeBufs b) {
+  const uint32_t t = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  const uint32_t base = pre_rpts_base(b);
+  if (t < base) stage_pre(b, t);
+  else if (b.rpts && t < base + 2 * b.n_sets) pre_rpts(b, t - base);
+}
 
 __global__ __launch_bounds__(BLS_BLOCK) void k_qdup(PipeBufs b) { stage_qdup(b, blockIdx.x * BLS_BLOCK + threadIdx.x); }
 
 hipError_t launch_k_pre(const PipeBufs& b, hipStream_t s) {
-  k_pre<<<bls_grid_for(pre_lanes(b)), BLS_BLOCK, 0, s>>>(b);
+  const uint32_t lanes = (pre_lanes(b) + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK + (b.rpts ? 2 * b.n_sets : 0u);
+  k_pre<<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !b.msg_rep) return e;
   k_qdup<<<bls_grid_for(8 * b.n_sets), BLS_BLOCK, 0, s>>>(b);

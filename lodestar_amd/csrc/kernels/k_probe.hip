@@ -7,6 +7,8 @@
 //                      miller_loop: f in registers, no squaring shared between pairs),
 //                      register budget for 1 or 2 wavefronts per SIMD
 //   fpm_d28          : a dependent chain of 28-bit-digit Montgomery products per lane
+//   glv_g1           : [s] P on G1 by jac_mul_glv with the window table in LDS (k_pset's
+//                      second wavefront), one point per lane
 #define BLS_FP_D28 1
 #include <string>
 
@@ -65,11 +67,22 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_probe_fpm_d28(Fp* io, uint32_t n)
   io[i] = a;
 }
 
+__global__ __launch_bounds__(BLS_BLOCK) void k_probe_glv_g1(G1J* out, uint32_t n) {
+  __shared__ G1J tab[4][15];
+  const uint32_t i = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (i >= n || threadIdx.x >= 4) return;
+  const G1J p = jac_from_aff(g1_generator());
+  uint32_t a, b;
+  glv_split(0x9e3779b97f4a7c15ull * (i + 1), a, b);
+  out[i] = jac_mul_glv<Fp>(p, a, b, tab[threadIdx.x]);
+}
+
 // bytes of output per lane for probe `name`, or 0 if unknown
 size_t kernel_probe_out_bytes(const char* name) {
   const std::string s(name);
   if (s == "ml_simt_w1" || s == "ml_simt_w2") return sizeof(Fp12);
   if (s == "fpm_d28") return sizeof(Fp);
+  if (s == "glv_g1") return sizeof(G1J);
   return 0;
 }
 
@@ -78,6 +91,7 @@ hipError_t launch_kernel_probe(const char* name, void* out, uint32_t lanes, hipS
   const unsigned grid = bls_grid_for(lanes);
   if (s == "ml_simt_w1") k_probe_ml_w1<<<grid, BLS_BLOCK, 0, st>>>((Fp12*)out, lanes);
   else if (s == "ml_simt_w2") k_probe_ml_w2<<<grid, BLS_BLOCK, 0, st>>>((Fp12*)out, lanes);
+  else if (s == "glv_g1") k_probe_glv_g1<<<grid, BLS_BLOCK, 0, st>>>((G1J*)out, lanes);
   else if (s == "fpm_d28") k_probe_fpm_d28<<<grid, BLS_BLOCK, 0, st>>>((Fp*)out, lanes);
   else return hipErrorInvalidValue;
   return hipGetLastError();

@@ -1,5 +1,5 @@
-// Per-set cooperative kernel: a block of two wavefronts per signature set.  The first
-// runs the "pset" programs of tools/gen_pset.py (interpreter: bls/coop.hpp):
+// Per-set cooperative kernel: one 64-lane wavefront per signature set runs the "pset"
+// programs of tools/gen_pset.py (interpreter: bls/coop.hpp):
 //
 //   P = iso(q0) + iso(q1)                               pset_prep
 //   A = [|x|]P, C = [|x|]sig (fixed bits of |x|)        pset_dbl_all / pset_add_x
@@ -7,33 +7,26 @@
 //   affine H with one lane-0 inversion                  pset_norm2, pset_affine2
 //   f_i = ML(RP, H) * ML(-RG, sig)                      pset_ml2
 //
-// while two lanes of the second compute RG = [s] g1 and RP = [s] pk for the set's batch
-// scalar s (GLV: curve.hpp jac_mul_glv, the scalar convention of k_chain and k_msm) and
-// write them into the frame; the first polls an LDS word for them before pset_ml2.  The
-// r chains used to run as interpreter programs beside the |x| chains (a 64-bit
-// double-and-add: ~290 more steps on the set's critical path, ~0.6 ms of the 128-set
-// call); the two GLV lanes finish in a fraction of the time the first wavefront spends
-// before the Miller loop.
+// RG = [s] g1 and RP = [s] pk for the set's batch scalar s come from k_pre's extra lanes
+// (GLV, kernels/k_pre.hip pre_rpts), computed beside the SSWU maps: the r chains used to
+// run here as interpreter programs beside the |x| chains (a 64-bit double-and-add, ~290
+// more steps on the set's critical path; then a second wavefront of this kernel, which
+// slowed the first by 0.35 ms, profiles/r04_ab_pset_rpoints.json).
 //
 // Reference semantics: Signature.fromBytes(.., validate=true) (maybeBatch.ts:23,36)
 // for the subgroup test, hash_to_G2 + the random-scalar pairing product of
 // verifyMultipleSignatures ([ext] blst) for f_i.  A zero-checked exceptional
-// addition, an infinity signature, RP at infinity (a public key of small order) or a
-// flag from k_pre sends the set to k_exact (pipeline.hpp stage_exact_set; kept out of
-// this kernel so its registers and stack do not lower this kernel's occupancy).
-// Flagged sets are counted; the host launches k_exact (and redoes status + chunks) only
-// when the count is non-zero.
+// addition, an infinity signature, RP at infinity (a public key of small order, flagged
+// by k_pre) or another flag from k_pre sends the set to k_exact (pipeline.hpp
+// stage_exact_set; kept out of this kernel so its registers and stack do not lower this
+// kernel's occupancy).  Flagged sets are counted; the host launches k_exact (and redoes
+// status + chunks) only when the count is non-zero.
 #define BLS_FP_D28 1  // 28-bit-digit Montgomery product (bls/field.hpp)
 #include "../launchers.hpp"
 
 using namespace bls;
 
-struct PsetShared {
-  CoopLds c;         // frame + constant bank + zero-check flag (first wavefront)
-  G1J tab[2][15];    // GLV window tables of the two r lanes
-  uint32_t r_done;   // RG, RP are in the frame
-  uint32_t r_flag;   // RP at infinity: exact path
-};
+typedef CoopLds PsetShared;
 
 // frame registers (tools/gen_pset.py)
 enum : int {
@@ -61,26 +54,7 @@ __device__ __forceinline__ void pset_flag(const PipeBufs& b, uint32_t i) {
   atomicAdd(b.flag_count, 1u);
 }
 
-// second wavefront, lanes 0 (RP = [s] pk) and 1 (RG = [s] g1): one instance of the GLV
-// body for both lanes (same scalar, so no divergence between them)
-__device__ __noinline__ void pset_r_points(const PipeBufs& b, uint32_t i, PsetShared* sh) {
-  const int lane = (int)threadIdx.x - COOP_LANES;
-  const G1J p = lane == 0 ? b.pk[i] : jac_from_aff(g1_generator());
-  uint32_t a, c;
-  glv_split(set_scalar(b.seed, b.scalar_base + i), a, c);
-  const G1J q = jac_mul_glv<Fp>(p, a, c, sh->tab[lane]);
-  const int slot = lane == 0 ? PS_RP : PS_RG;
-  lds_store_fp(sh->c.frame, slot + 0, q.x);
-  lds_store_fp(sh->c.frame, slot + 1, q.y);
-  lds_store_fp(sh->c.frame, slot + 2, q.z);
-  if (lane == 0) {
-    sh->r_flag = jac_is_inf(q) ? 1u : 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __hip_atomic_store(&sh->r_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-
-__global__ __launch_bounds__(2 * COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
+__global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
   __shared__ PsetShared sh;
   const uint32_t i = blockIdx.x;
   const int lane = threadIdx.x;
@@ -92,52 +66,40 @@ __global__ __launch_bounds__(2 * COOP_LANES) void k_pset(PipeBufs b, CoopEnv env
     if (lane == 0) pset_flag(b, i);
     return;
   }
-  // prologue, both wavefronts: the block's only two barriers
-  coop_stage_consts(env, sh.c.cbank);
-  if (lane < 8) lds_store_fp(sh.c.frame, PS_Q0 + lane, b.q[8ull * i + lane]);
-  if (lane >= 8 && lane < 12) lds_store_fp(sh.c.frame, PS_SIG + lane - 8, reinterpret_cast<const Fp*>(&b.sig[i])[lane - 8]);
-  if (lane >= 12 && lane < 15) lds_store_fp(sh.c.frame, PS_PK + lane - 12, reinterpret_cast<const Fp*>(&b.pk[i])[lane - 12]);
-  if (lane == 0) {
-    sh.c.flag = 0;
-    sh.r_done = 0;
-  }
+  coop_stage_consts(env, sh.cbank);
+  const Fp* rp = reinterpret_cast<const Fp*>(b.rpts + 2ull * i);  // RP (x, y, z), RG (x, y, z)
+  if (lane < 8) lds_store_fp(sh.frame, PS_Q0 + lane, b.q[8ull * i + lane]);
+  if (lane >= 8 && lane < 12) lds_store_fp(sh.frame, PS_SIG + lane - 8, reinterpret_cast<const Fp*>(&b.sig[i])[lane - 8]);
+  if (lane >= 12 && lane < 15) lds_store_fp(sh.frame, PS_PK + lane - 12, reinterpret_cast<const Fp*>(&b.pk[i])[lane - 12]);
+  if (lane >= 15 && lane < 18) lds_store_fp(sh.frame, PS_RP + lane - 15, rp[lane - 15]);
+  if (lane >= 18 && lane < 21) lds_store_fp(sh.frame, PS_RG + lane - 18, rp[3 + lane - 18]);
+  if (lane == 0) sh.flag = 0;
   __syncthreads();
-  if (lane >= COOP_LANES) {
-    if (lane < COOP_LANES + 2) pset_r_points(b, i, &sh);
-    return;
-  }
 
-  coop_run(env, env.pset_prep, sh.c.frame, sh.c.cbank, &sh.c.flag);
+  coop_run(env, env.pset_prep, sh.frame, sh.cbank, &sh.flag);
   for (int k = 62; k >= 0; --k) {
-    coop_run(env, env.pset_dbl_all, sh.c.frame, sh.c.cbank, &sh.c.flag);
-    if ((PS_X_ABS >> k) & 1ull) coop_run(env, env.pset_add_x, sh.c.frame, sh.c.cbank, &sh.c.flag);
+    coop_run(env, env.pset_dbl_all, sh.frame, sh.cbank, &sh.flag);
+    if ((PS_X_ABS >> k) & 1ull) coop_run(env, env.pset_add_x, sh.frame, sh.cbank, &sh.flag);
   }
-  coop_run(env, env.pset_phase2, sh.c.frame, sh.c.cbank, &sh.c.flag);
-  if (sh.c.flag) {
+  coop_run(env, env.pset_phase2, sh.frame, sh.cbank, &sh.flag);
+  if (sh.flag) {
     if (lane == 0) pset_flag(b, i);
     return;
   }
-  if (!coop_is_zero(sh.c.frame, PS_DIFF, 4)) {  // psi(sig) != [x] sig: not in G2
+  if (!coop_is_zero(sh.frame, PS_DIFF, 4)) {  // psi(sig) != [x] sig: not in G2
     if (lane == 0) b.sig_status[i] = BLS_POINT_NOT_IN_GROUP;
     pset_store_one(&b.f[i]);
     return;
   }
-  coop_run(env, env.pset_norm2, sh.c.frame, sh.c.cbank, &sh.c.flag);
-  if (sh.c.flag) {
+  coop_run(env, env.pset_norm2, sh.frame, sh.cbank, &sh.flag);
+  if (sh.flag) {
     if (lane == 0) pset_flag(b, i);
     return;
   }
-  coop_invert(sh.c.frame, PS_INV_IN, PS_INV_OUT);
-  coop_run(env, env.pset_affine2, sh.c.frame, sh.c.cbank, &sh.c.flag);
-  // RG, RP from the second wavefront (long done at this point)
-  while (__hip_atomic_load(&sh.r_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (sh.r_flag) {
-    if (lane == 0) pset_flag(b, i);
-    return;
-  }
-  coop_run(env, env.pset_ml2, sh.c.frame, sh.c.cbank, &sh.c.flag);
-  if (lane < 12) reinterpret_cast<Fp*>(&b.f[i])[lane] = coop_get(sh.c.frame, PS_F + lane);
+  coop_invert(sh.frame, PS_INV_IN, PS_INV_OUT);
+  coop_run(env, env.pset_affine2, sh.frame, sh.cbank, &sh.flag);
+  coop_run(env, env.pset_ml2, sh.frame, sh.cbank, &sh.flag);
+  if (lane < 12) reinterpret_cast<Fp*>(&b.f[i])[lane] = coop_get(sh.frame, PS_F + lane);
 }
 
 // S sets per wavefront (tools/gen_pset.py build_pset(S): set s at frame offset 92 s,
@@ -358,7 +320,7 @@ hipError_t launch_k_pset(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
   } else if (S == 2 && env.packed[0].ml2.n > 0) {
     k_psetn<2, COOP_FRAME2><<<(b.n_sets + 1) / 2, COOP_LANES, 0, s>>>(b, env);
   } else {
-    k_pset<<<b.n_sets, 2 * COOP_LANES, 0, s>>>(b, env);
+    k_pset<<<b.n_sets, COOP_LANES, 0, s>>>(b, env);
   }
   return hipGetLastError();
 }

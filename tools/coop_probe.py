@@ -19,7 +19,8 @@ ROOT = Path(__file__).resolve().parent.parent
 progs = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
 with GpuContext(0) as g:
     out = {}
-    names = sys.argv[1:] or ["pset_dbl_all:100", "pset_ml2:3", "fin_fe2:2", "fin_fe1:2", "pset_prep:3"]
+    names = sys.argv[1:] or ["pset_dbl_all:100", "pset_add_x:100", "pset_phase2:3", "pset_ml2:3", "fin_fe2:2", "fin_fe1:2",
+                             "pset_prep:3"]
     for item in names:
         name, reps = item.split(":")[0], int(item.split(":")[1])
         n_steps = progs[name]["steps"]

@@ -46,6 +46,10 @@ if [ -n "$COOP" ]; then
   timeout -k 10 240 python -u tools/coop_probe.py > $O/coop_probe.json 2> $O/coop_probe.err || { echo "coop probe failed"; tail -5 $O/coop_probe.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/coop_probe.json'));[print(k,v) for k,v in d.items()]"
 fi
+if [ -n "$KPROBE" ]; then
+  timeout -k 10 120 python -u tools/kprobe.py > $O/kprobe.json 2> $O/kprobe.err || { echo "kprobe failed"; tail -5 $O/kprobe.err; exit 1; }
+  cat $O/kprobe.json
+fi
 if [ -n "$SOLO" ]; then
   # one 32-call pass (32,768 cfg2 sets) alone under a kernel trace (+ SQ counters), per
   # SOLO label "name:VAR=v,..." separated by ";"

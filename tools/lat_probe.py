@@ -22,6 +22,7 @@ def main() -> None:
     ap.add_argument("--sets", type=int, default=128)
     ap.add_argument("--runs", type=int, default=10)
     ap.add_argument("--batchable", action="store_true", help="one batchable request per set (cfg2 shape)")
+    ap.add_argument("--no-check", action="store_true", help="timing builds that skip work: verdicts not checked")
     args = ap.parse_args()
     gpu = GpuContext(0)
     _, _, sets, _ = bench.make_workload(gpu, max(args.sets, 128), 0)
@@ -34,7 +35,7 @@ def main() -> None:
         v, st = gpu.verify_packed(call)
         lat.append((time.perf_counter() - t) * 1e3)
         stages.append([round(x, 3) for x in st.stage_ms[:]])
-        assert all(x == 1 for x in v)
+        assert args.no_check or all(x == 1 for x in v)
     print(json.dumps({"sets": args.sets, "batchable": args.batchable, "p50_ms": round(statistics.median(lat), 3),
                       "stage_names": bench.STAGE_NAMES, "stage_ms_last": stages[-1]}))
     gpu.close()
