@@ -181,9 +181,8 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
 }
 
 // ---------------------------------------------------------------------------
-// k_mlf2: the f side with two lanes per item, for few sets in flight (a pass alone: its
-// 32,768 items run as 1,024 wavefronts, one per SIMD, instead of 512, each with half of
-// the f chain's products).  Lanes 2k and 2k + 1 hold the same f; per step each computes
+// k_mlf2: the f side with two lanes per item, for few sets in flight (a pass of 16,384
+// sets runs as 544 wavefronts instead of 272, each with half of the f chain's products).  Lanes 2k and 2k + 1 hold the same f; per step each computes
 // one of the squaring's two Fp6 products and one of the line's two mul_by_01 products
 // (plus one of the Fp2 products of f.c1 l3, and both the third), swaps its products with
 // its partner (DPP quad_perm [1,0,3,2]: one move per word), and both finish the step --
@@ -261,7 +260,10 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   // 2 above $BLS_MLF_PL2_MIN (default 98,304) sets, 4 above $BLS_MLF_PL4_MIN (200,000:
   // 3.55M vs 3.41M sets/s at 12 x 22), else 1.  $BLS_MLF_PER_LANE = 1, 2, 4 or 3 (MLF_PAIR)
   // fixes it.
-  // Below $BLS_MLF_PAIR_MAX (32,768) sets in flight: two lanes per item (k_mlf2, MLF_PAIR).
+  // Up to $BLS_MLF_PAIR_MAX (16,384) sets in flight: two lanes per item (k_mlf2, MLF_PAIR;
+  // at two waves per SIMD, $BLS_MLF2_WAVES=1 for one): a solo pass's f side 4.7 vs 7.1 ms
+  // at 8,192 sets, 5.2 vs 7.2 ms at 16,384, but 8.8 vs 7.4 ms at 32,768
+  // (profiles/r04_ab_mlf_pair.json).
   const uint32_t per_lane = b.mlf_pl ? b.mlf_pl : mlf_per_lane();
   if (per_lane == MLF_PAIR) {
     static const int w2 = [] {
@@ -285,7 +287,7 @@ uint32_t mlf_per_lane() {
   }();
   static const uint64_t pair_max = [] {
     const char* e = getenv("BLS_MLF_PAIR_MAX");
-    return e ? (uint64_t)strtoull(e, nullptr, 10) : 32768ull;
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 16384ull;
   }();
   static const uint64_t pl2_min = [] {
     const char* e = getenv("BLS_MLF_PL2_MIN");

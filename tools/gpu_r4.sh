@@ -56,7 +56,7 @@ if [ -n "$SOLO" ]; then
   R=$GRAFT_REPO_ROOT
   for ab in $(echo "$SOLO" | tr ';' ' '); do
     label=${ab%%:*}; vars=$(echo "${ab#*:}" | tr ',' ' ')
-    PB="python3 $R/bench.py --probe-only --inflight 1 --calls-per-pass 32 --steps 1 --warmup 1"
+    PB="python3 $R/bench.py --probe-only --inflight 1 --calls-per-pass ${SOLO_CPP:-32} --steps 1 --warmup 1"
     (cd /tmp && export TMPDIR=/tmp && env $vars timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$O/solo_$label -o run --output-format csv -- $PB > $R/$O/solo_$label.log 2>&1) || { tail -20 $O/solo_$label.log; exit 1; }
     (cd /tmp && export TMPDIR=/tmp && env $vars timeout -s KILL 120 rocprofv3 --pmc ${SOLO_PMC:-SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE} -d $R/$O/solo_${label}_pmc -o run --output-format csv -- $PB > $R/$O/solo_${label}_pmc.log 2>&1) || { tail -20 $O/solo_${label}_pmc.log; exit 1; }
     python3 -c "
