@@ -471,6 +471,39 @@ def test_sharded_call_two_ranks(gpu, oracle):
         assert res[r][3][0] == -CODE_BAD_ENCODING                                  # pubkey error beats signature
 
 
+def test_sharded_call_two_ranks_large(gpu, oracle):
+    """The sharded call at the per-GPU scale of a pass: 2,048 sets over two processes
+    (1,024 per rank, the aggregated path on each), all valid, then one set signing another
+    message in rank 1's shard: the call fails and only shard 1 is reported bad."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    n = 2048
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"r2big-%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    raw = [oracle.g1_serialize(oracle.sk_to_pk(int.from_bytes(s, "big"))) for s in sks]
+    good = [(raw[i % 16], msgs[i], sigs[i].tobytes()) for i in range(n)]
+    bad = list(good)
+    bad[1500] = (raw[1500 % 16], msgs[7], sigs[1500].tobytes())
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad], q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=110) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert res[r][0] == (True, {"bad_shards": []})
+        assert res[r][1] == (False, {"bad_shards": [1]})
+
+
 # ---------------------------------------------------------------------------
 # BASELINE configs as parity cases (size-independent properties)
 # ---------------------------------------------------------------------------
