@@ -698,12 +698,27 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     reference's pool splits the work across its workers the same way, one message per
     worker (multithread/index.ts:153-166).  Rank 0 prints the JSON line; a rank that
     fails stops the others; returns the worst exit status."""
+    import threading
+
     port = _free_port()
     procs = []
+
+    def forward(pipe):
+        # rank 0's stdout: the JSON line to stdout, anything else a library printed there
+        # (gloo's connection notes) to stderr, so stdout holds the one line
+        for line in iter(pipe.readline, b""):
+            (sys.stdout if line.lstrip().startswith(b"{") else sys.stderr).buffer.write(line)
+            (sys.stdout if line.lstrip().startswith(b"{") else sys.stderr).flush()
+
+    fwd = None
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+        if r == 0:
+            fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+            fwd.start()
     worst = 0
     try:
         while any(p.poll() is None for p in procs):
@@ -725,6 +740,8 @@ def launch_ranks(n: int, argv: list[str]) -> int:
         for p in procs:
             if p.poll() is None:
                 p.kill()
+        if fwd is not None:
+            fwd.join(timeout=10)
     return worst or next((p.returncode for p in procs if p.returncode), 0)
 
 
@@ -802,10 +819,16 @@ def main() -> None:
     if world != max(1, args.gpus):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
     dist, device = None, None
+    # $BLS_BENCH_SHARE_DEVICE=1: a rehearsal of the N-rank line on a box with fewer GPUs --
+    # every rank on cuda:0, control collectives over gloo (the data path has none); the
+    # line says so in `data`.  Not a measurement of N GPUs.
+    share = os.environ.get("BLS_BENCH_SHARE_DEVICE") == "1" and world > 1
+    if share:
+        local_rank = 0
     if world > 1:
         import torch.distributed as dist
 
-        if args.stand_in:
+        if args.stand_in or share:
             dist.init_process_group("gloo")
         else:
             import torch
@@ -956,6 +979,8 @@ def main() -> None:
                "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
                "dtype": "u32 (381-bit Fp, 12x32-bit Montgomery limbs)",
                "data": "synthetic: interop keys, sha256 messages, GPU-made signatures", "config": config}
+        if share:
+            out["data"] += f"; REHEARSAL: {world} ranks sharing one GPU (BLS_BENCH_SHARE_DEVICE), not an N-GPU figure"
         out.update(extra)
 
     if args.probe_only:

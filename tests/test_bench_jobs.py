@@ -216,8 +216,8 @@ def test_bench_gpus2_launches_two_ranks():
            "--cfg4-invalid", "0.1", "--stand-in", "tests.test_bench_jobs:OracleCtx"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(root))
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out.stdout  # rank 0 alone prints
+    lines = out.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout  # rank 0's JSON line alone on stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["value"] > 0 and "DRY RUN" in r["data"]
     assert r["job"]["sets"] == 16 and r["job"]["calls"] == 2  # this rank's half of the 32-set job

@@ -46,6 +46,18 @@ if [ -n "$COOP" ]; then
   timeout -k 10 240 python -u tools/coop_probe.py > $O/coop_probe.json 2> $O/coop_probe.err || { echo "coop probe failed"; tail -5 $O/coop_probe.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/coop_probe.json'));[print(k,v) for k,v in d.items()]"
 fi
+if [ -n "$REHEARSE" ]; then
+  # bench.py --gpus 2 with both ranks on this box's one GPU (launcher, gloo control
+  # collectives, rank-0 line): cfg2 and the cfg4 job mode
+  export BLS_BENCH_SHARE_DEVICE=1
+  timeout -k 10 300 python -u bench.py --gpus 2 --inflight 4 --calls-per-pass 8 --steps 3 --warmup 1 --no-cpu-baseline --no-sub-records > $O/rehearse_cfg2.json 2> $O/rehearse_cfg2.err || { echo "rehearse cfg2 failed"; tail -20 $O/rehearse_cfg2.err; exit 1; }
+  timeout -k 10 300 python -u bench.py --gpus 2 --mode cfg4 --inflight 4 --steps 2 --warmup 1 > $O/rehearse_cfg4.json 2> $O/rehearse_cfg4.err || { echo "rehearse cfg4 failed"; tail -20 $O/rehearse_cfg4.err; exit 1; }
+  unset BLS_BENCH_SHARE_DEVICE
+  python3 -c "
+import json
+for f in ('rehearse_cfg2','rehearse_cfg4'):
+  d=json.load(open('$O/'+f+'.json')); print(f, d['n_gpus'], d['value'], d['ms_per_step'], d['data'][-80:])"
+fi
 if [ -n "$KPROBE" ]; then
   timeout -k 10 120 python -u tools/kprobe.py > $O/kprobe.json 2> $O/kprobe.err || { echo "kprobe failed"; tail -5 $O/kprobe.err; exit 1; }
   cat $O/kprobe.json
