@@ -89,10 +89,12 @@ def pset_products_per_set(S: int) -> float:
     pg = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
     m = {k: v["mul_ops"] for k, v in pg.items()}
     if S == 1:
-        n = m["pset_prep"] + m["pset_dbl_r"] + 0.5 * m["pset_add_r"] + 63 * m["pset_dbl_all"]
-        for i in range(62, -1, -1):
-            n += (0.5 * m["pset_add_xr"] + 0.5 * m["pset_add_x"]) if (X_ABS >> i) & 1 else 0.5 * m["pset_add_r"]
-        return n + m["pset_phase2"] + m["pset_norm2"] + m["pset_affine2"] + m["pset_ml2"]
+        # the |x| chains only; RG and RP come from k_pre's GLV lanes (two G1 scalar
+        # multiplications, work_model.json chain_r_pk each)
+        wm = json.loads((ROOT / "lodestar_amd" / "_native" / "work_model.json").read_text())
+        n = m["pset_prep"] + 63 * m["pset_dbl_all"]
+        n += sum(m["pset_add_x"] for i in range(62, -1, -1) if (X_ABS >> i) & 1)
+        return n + m["pset_phase2"] + m["pset_norm2"] + m["pset_affine2"] + m["pset_ml2"] + 2 * wm["chain_r_pk"]
     p = f"pset{S}_"
 
     def add(xb):

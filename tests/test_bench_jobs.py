@@ -196,6 +196,13 @@ def test_work_pricing_follows_pass_shape():
     assert chains - msm > 0.8 * wm["chain_r_sig"]  # the [r] sig chains leave, the MSM costs little
     # every set's loop and the pass's one signature loop (1 / n per set) follow the shape
     assert msm - quad == pytest.approx((wm["ml_f_pair"] - wm["ml_f_quad"]) * (1 + 1 / n))
+    # the per-set path's pricing follows the programs the kernel runs (one set per
+    # wavefront: the |x| chains + k_pre's two GLV multiplications; packed: the r chains in
+    # the programs), for every packing
+    for S in (1, 2, 3):
+        assert 10_000 < bench.pset_products_per_set(S) < 25_000
+    small, note = bench.work_per_set(128)
+    assert "k_pset" in note and small > bench.pset_products_per_set(1)
 
 
 def test_bench_gpus2_launches_two_ranks():
