@@ -109,11 +109,14 @@ def pset_products_per_set(S: int) -> float:
 
 
 SIGAGG_MIN_SETS = 512   # bls_gpu.hip use_sigagg: the aggregated-signature path from this call size on
+PERSET_MAX_INFLIGHT = 12288  # ... while more sets than this are in flight
 
 
-def sigagg_of(n_sets: int) -> bool:
+def sigagg_of(n_sets: int, in_flight: int | None = None) -> bool:
     e = os.environ.get("BLS_SIGAGG")
-    return (e != "0") if e not in (None, "") else n_sets >= SIGAGG_MIN_SETS
+    if e not in (None, ""):
+        return e != "0"
+    return n_sets >= SIGAGG_MIN_SETS and (in_flight if in_flight is not None else n_sets) > PERSET_MAX_INFLIGHT
 
 
 def mlf_products(wm: dict, shape: int | None) -> float:
@@ -139,7 +142,9 @@ def work_per_set(n_sets: int, reqs_per_chunk: int = 16, shape: int | None = None
     m = {k: v["mul_ops"] for k, v in pg.items()}
     chunks = max(1, n_sets // reqs_per_chunk)
     merged = (n_sets + chunks - 1) * m["fin_fmul"] + m["fin_fe1"] + m["fin_fe2"]
-    if sigagg_of(n_sets):
+    # the library's pass shape says which path ran (0: the per-set path, chosen for calls
+    # of >= 512 sets too while few sets are in flight, bls_gpu.hip use_sigagg)
+    if (shape != 0) if shape is not None else sigagg_of(n_sets):
         # a set's Miller loop: k_mlq lines + k_mlf f side (1, 2 or 4 pairs sharing f's
         # squarings, as blst's multi-pairing does; kernels/k_mlq.hip); a chunk's
         # signature-sum pair runs the same loop
@@ -1015,7 +1020,7 @@ def main() -> None:
         shape = max(shapes, key=shapes.get) if shapes else None  # the timed passes' usual shape
         fpm_set, fpm_note = work_per_set(args.sets * K, shape=shape)  # one device pass: K calls
         mad_set = fpm_set * MADS_PER_FPM
-        agg = sigagg_of(args.sets * K)
+        agg = (shape != 0) if shape is not None else sigagg_of(args.sets * K, inflight * args.sets * K)
         solo_st = []
         for _ in range(3):
             if K > 1:
@@ -1095,7 +1100,7 @@ def main() -> None:
                 out["cpu_baseline"]["gpu_over_whole_host_extrapolated"] = round(
                     value / max(1e-9, out["cpu_baseline"]["whole_host_sets_per_s_extrapolated"]), 2)
     if world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records and K > 1:
-        curve = latency_curve(ctxs, works, ((4, 16), (8, 16)), args.sets)
+        curve = latency_curve(ctxs, works, ((1, 4), (4, 16), (8, 16)), args.sets)
         curve[f"{inflight}x{K}"] = {"sets_in_flight": inflight * K * args.sets, "sets_per_s": round(value, 1),
                                     "ms_per_call": out["ms_per_step"], "note": "the headline line"}
         out["latency_curve"] = curve
