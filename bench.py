@@ -109,14 +109,16 @@ def pset_products_per_set(S: int) -> float:
 
 
 SIGAGG_MIN_SETS = 512   # bls_gpu.hip use_sigagg: the aggregated-signature path from this call size on
-PERSET_MAX_INFLIGHT = 12288  # ... while more sets than this are in flight
+PERSET_MAX_INFLIGHT = 12288  # ... while more sets than this are in flight, or the call has more than
+PERSET_MAX_CALL = 2048       # ... this many sets
 
 
 def sigagg_of(n_sets: int, in_flight: int | None = None) -> bool:
     e = os.environ.get("BLS_SIGAGG")
     if e not in (None, ""):
         return e != "0"
-    return n_sets >= SIGAGG_MIN_SETS and (in_flight if in_flight is not None else n_sets) > PERSET_MAX_INFLIGHT
+    return n_sets >= SIGAGG_MIN_SETS and (n_sets > PERSET_MAX_CALL or (
+        in_flight if in_flight is not None else n_sets) > PERSET_MAX_INFLIGHT)
 
 
 def mlf_products(wm: dict, shape: int | None) -> float:

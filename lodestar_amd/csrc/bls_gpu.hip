@@ -562,14 +562,18 @@ int bls_gpu_validate_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, u
 // (decode, hash_to_G2, per-set programs, exact path, status), then either the
 // chunk / individual verdicts or a product tree of every f_i.
 // Aggregated-signature path (k_chain + k_gsum + k_vset + k_mln single-pair Miller
-// loops, one signature Miller loop per chunk) from SIGAGG_MIN_SETS sets on while the
-// process has more than $BLS_PERSET_MAX_INFLIGHT (12,288) sets in flight (this call's
-// included); otherwise the all-cooperative k_pset / k_psetn (a set's chains spread over
-// a wavefront instead of one lane: shorter calls while the device has room, fewer sets
-// per second once it is full -- 4 x 4096-set calls 9.7 vs 16.8 ms, 3 x 4 18.7 vs 20.9 ms,
-// 4 x 4 23.9 vs 21.6 ms, profiles/r04_ab_perset_low_load.json).  BLS_DEBUG_SIGAGG_ON / _OFF
-// or $BLS_SIGAGG (0 / 1) force a path.
+// loops, one signature Miller loop per chunk) from SIGAGG_MIN_SETS sets on, except for
+// calls of at most PERSET_MAX_CALL sets while the process has at most
+// $BLS_PERSET_MAX_INFLIGHT (12,288) sets in flight (this call's included): those run the
+// all-cooperative k_pset / k_psetn (a set's chains spread over a wavefront instead of one
+// lane: shorter calls while the device has room, fewer sets per second once it is full --
+// 4 x 1024-set calls in flight 9.7 vs 16.8 ms per call, 12 x 1024 18.7 vs 20.9 ms, 16 x 1024
+// 23.9 vs 21.6 ms, profiles/r04_ab_perset_low_load.json).  A call of more sets would fill
+// every SIMD with its wavefronts (2 sets each, two per SIMD) and hold the main-thread
+// lane's context behind it (test_napi.py: a 4096-set pool call finished first).
+// BLS_DEBUG_SIGAGG_ON / _OFF or $BLS_SIGAGG (0 / 1) force a path.
 #define SIGAGG_MIN_SETS 512u
+#define PERSET_MAX_CALL 2048u
 static bool use_sigagg(const bls_gpu_ctx* ctx, uint32_t n) {
   static const int env = [] {
     const char* e = getenv("BLS_SIGAGG");
@@ -582,7 +586,7 @@ static bool use_sigagg(const bls_gpu_ctx* ctx, uint32_t n) {
   if (ctx->debug_flags & BLS_DEBUG_SIGAGG_ON) return true;
   if (ctx->debug_flags & BLS_DEBUG_SIGAGG_OFF) return false;
   if (env >= 0) return env != 0;
-  return n >= SIGAGG_MIN_SETS && bls_sets_in_flight() > perset_max;
+  return n >= SIGAGG_MIN_SETS && (n > PERSET_MAX_CALL || bls_sets_in_flight() > perset_max);
 }
 
 // $BLS_DEBUG_SYNC: synchronise after every kernel of a verify call and log its name
