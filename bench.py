@@ -1102,7 +1102,7 @@ def main() -> None:
                 out["cpu_baseline"]["gpu_over_whole_host_extrapolated"] = round(
                     value / max(1e-9, out["cpu_baseline"]["whole_host_sets_per_s_extrapolated"]), 2)
     if world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records and K > 1:
-        curve = latency_curve(ctxs, works, ((1, 4), (4, 16), (8, 16)), args.sets)
+        curve = latency_curve(ctxs, works, ((4, 1), (8, 1), (4, 16), (8, 16)), args.sets)
         curve[f"{inflight}x{K}"] = {"sets_in_flight": inflight * K * args.sets, "sets_per_s": round(value, 1),
                                     "ms_per_call": out["ms_per_step"], "note": "the headline line"}
         out["latency_curve"] = curve
