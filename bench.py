@@ -246,7 +246,7 @@ def committed_pmc():
         if sets and "SQ_INSTS_VALU" in v:
             vset += v["SQ_INSTS_VALU"] / sets  # per dispatch: every wave's VALU instructions
         wc = v.get("SQ_WAVE_CYCLES")
-        if name.startswith(("k_chain", "k_mlf", "k_mlq", "k_mlx", "k_pre")) and wc:
+        if name.startswith(("k_chain", "k_mlf", "k_mlq", "k_pre")) and wc:
             out[name] = {"valu_issue_frac": round(v["SQ_ACTIVE_INST_VALU"] / wc, 3),
                          "waves_per_simd": v.get("waves_per_simd"), "valu_busy": v.get("valu_busy"),
                          "valu_insts_per_wave": round(v["SQ_INSTS_VALU"] / max(1.0, v["SQ_WAVES"])),
