@@ -605,6 +605,131 @@ static void dbg_sync(hipStream_t s, const char* what) {
   fflush(stderr);
 }
 
+// Group testing of a failed chunk's requests (instead of one final exponentiation per
+// request, worker.ts:91-98).  Each request's product F_t (its sets' f and, on the
+// aggregated path, its own signature-sum pairing) is left by k_indiv_coop; a test is
+// FE(prod of a group's F_t) == 1 (k_group_coop), the same random-scalar batch check the
+// reference runs over a chunk.  With the chunk's requests of status OK indexed 0 .. m-1:
+//   pass A: the group of all of them if the chunk failed on an erroneous request (its
+//           batch would throw, worker.ts:81-87: the others may all be valid), and for
+//           each bit j of the index the group of those with bit j set;
+//   a single invalid request b fails exactly the bit groups of b's index, so
+//   pass B: {b} alone (must fail) and the others together (must pass);
+//   pass C: any other outcome (two or more invalid, an index past m): every request
+//           alone.
+// With one invalid request in a chunk of 16 that is 6 final exponentiations instead of
+// 16; verdicts and the worker counters are the reference's (a test that passes is the
+// batch the reference's retry would have passed request by request, with the same
+// soundness).  $BLS_GROUP_TEST_MIN (default 4; 0 = off) is the smallest chunk tested so.
+static uint32_t group_test_min() {
+  static const uint32_t v = [] {
+    const char* e = getenv("BLS_GROUP_TEST_MIN");
+    const long x = e ? atol(e) : 4;
+    return x <= 0 ? 0xFFFFFFFFu : (uint32_t)(x < 2 ? 2 : x);
+  }();
+  return v;
+}
+
+// run the tests (goff: offsets into gmem, indices into the indiv list); results in gv
+static int run_group_tests(bls_gpu_ctx* ctx, PipeBufs& b, const std::vector<uint32_t>& goff,
+                           const std::vector<uint32_t>& gmem, std::vector<int32_t>& gv, hipStream_t s) {
+  gv.assign(goff.size() - 1, 0);
+  if (gv.empty()) return 0;
+  stage_copy(ctx, b.grp_off, goff.data(), sizeof(uint32_t) * goff.size());  // the stream is idle
+  stage_copy(ctx, b.grp_members, gmem.data(), sizeof(uint32_t) * gmem.size());
+  b.n_grp = (uint32_t)gv.size();
+  HIPC(ctx, launch_k_group_coop(b, ctx->coop, s)); dbg_sync(s, "k_group_coop");
+  HIPC(ctx, hipStreamSynchronize(s));
+  memcpy(gv.data(), res_host(ctx, b.grp_verdict), sizeof(int32_t) * gv.size());
+  return 0;
+}
+
+static int verify_groups(bls_gpu_ctx* ctx, PipeBufs& b, const std::vector<std::pair<uint32_t, uint32_t>>& chunks,
+                         std::vector<int32_t>& verdict, hipStream_t s, size_t grp_cap, size_t grp_mem_cap) {
+  struct Chunk {
+    std::vector<uint32_t> ok;  // indiv indices of the requests of status OK
+    bool has_err = false;
+    uint32_t first = 0, nbits = 0;
+    int32_t b = -1;            // the one invalid request's position in ok (pass B), -1 none
+  };
+  std::vector<Chunk> cs;
+  std::vector<uint32_t> goff{0}, gmem;
+  auto add_test = [&](const std::vector<uint32_t>& m) {
+    gmem.insert(gmem.end(), m.begin(), m.end());
+    goff.push_back((uint32_t)gmem.size());
+  };
+  for (const auto& ch : chunks) {
+    Chunk c;
+    for (uint32_t t = ch.first; t < ch.second; ++t) {
+      if (verdict[t] == 2) c.ok.push_back(t);
+      else c.has_err = true;  // its -code stays
+    }
+    if (c.ok.empty()) continue;
+    c.first = (uint32_t)goff.size() - 1;
+    if (c.has_err || c.ok.size() == 1) add_test(c.ok);
+    const uint32_t m = (uint32_t)c.ok.size();
+    while (m > 1 && (1u << c.nbits) < m) ++c.nbits;
+    for (uint32_t j = 0; j < c.nbits; ++j) {
+      std::vector<uint32_t> g;
+      for (uint32_t k = 0; k < m; ++k)
+        if ((k >> j) & 1u) g.push_back(c.ok[k]);
+      add_test(g);
+    }
+    cs.push_back(std::move(c));
+  }
+  if (gmem.size() > grp_mem_cap || goff.size() - 1 > grp_cap) {
+    snprintf(ctx->err, sizeof(ctx->err), "group-test plan exceeds its workspace");
+    return -3;
+  }
+  std::vector<int32_t> gv;
+  if (run_group_tests(ctx, b, goff, gmem, gv, s)) return -1;
+  // decode pass A; plan pass B
+  std::vector<uint32_t> goff_b{0}, gmem_b, alone;  // alone: requests for pass C
+  std::vector<size_t> in_b;
+  for (size_t i = 0; i < cs.size(); ++i) {
+    Chunk& c = cs[i];
+    uint32_t idx = c.first;
+    const uint32_t m = (uint32_t)c.ok.size();
+    if (c.has_err || m == 1) {
+      const bool pass = gv[idx++] == 1;
+      if (pass || m == 1) {
+        for (uint32_t t : c.ok) verdict[t] = pass ? 1 : 0;
+        continue;
+      }
+    }
+    uint32_t bad = 0;
+    for (uint32_t j = 0; j < c.nbits; ++j)
+      if (gv[idx + j] != 1) bad |= 1u << j;
+    if (bad >= m) {
+      alone.insert(alone.end(), c.ok.begin(), c.ok.end());
+      continue;
+    }
+    c.b = (int32_t)bad;
+    gmem_b.push_back(c.ok[bad]);
+    goff_b.push_back((uint32_t)gmem_b.size());
+    for (uint32_t k = 0; k < m; ++k)
+      if (k != bad) gmem_b.push_back(c.ok[k]);
+    goff_b.push_back((uint32_t)gmem_b.size());
+    in_b.push_back(i);
+  }
+  if (run_group_tests(ctx, b, goff_b, gmem_b, gv, s)) return -1;
+  for (size_t q = 0; q < in_b.size(); ++q) {
+    Chunk& c = cs[in_b[q]];
+    if (gv[2 * q] == 0 && gv[2 * q + 1] == 1) {
+      for (uint32_t k = 0; k < c.ok.size(); ++k) verdict[c.ok[k]] = (int32_t)k == c.b ? 0 : 1;
+    } else {
+      alone.insert(alone.end(), c.ok.begin(), c.ok.end());
+    }
+  }
+  // pass C: one test per request
+  std::vector<uint32_t> goff_c{0};
+  for (size_t k = 0; k < alone.size(); ++k) goff_c.push_back((uint32_t)k + 1);
+  if (run_group_tests(ctx, b, goff_c, alone, gv, s)) return -1;
+  for (size_t k = 0; k < alone.size(); ++k) verdict[alone[k]] = gv[k] == 1 ? 1 : 0;
+  return 0;
+}
+
+
 // Pippenger merged signature sum (k_msm) instead of the per-set [r] sig chains (k_chain
 // role 2, ~1.6k Fp products per set) and the k_gsum levels: ~10 % fewer instructions per
 // set, but its serial stages (segments, buckets, the windows' dependent additions) make
@@ -983,6 +1108,10 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   MsmBufs msm;
   memset(&msm, 0, sizeof(msm));
   G1J* utmp[2] = {nullptr, nullptr};
+  // group tests over failed chunks (passes reuse the buffers): pass A <= 1 + 13 tests per
+  // chunk (chunks of < 8192 requests) of <= 8 m members in all, pass B 2 tests, pass C one
+  // test per request
+  const size_t grp_cap = (size_t)R + 14ull * n_chunks + 2, grp_mem_cap = 8ull * R + 16;
   auto carve = [&](Carver& c, PipeBufs& b, size_t& input_end) {
     b.req_off = c.take<uint32_t>(R + 1);
     b.chunk_off = c.take<uint32_t>(n_chunks + 1);
@@ -998,6 +1127,8 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.sigs = c.take<uint8_t>(96ull * n);
     b.sig_lens = in->signature_lens ? c.take<uint32_t>(n) : nullptr;
     b.indiv_reqs = c.take<uint32_t>(R);
+    b.grp_off = c.take<uint32_t>(grp_cap + 1);
+    b.grp_members = c.take<uint32_t>(grp_mem_cap);
     own_sets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
     b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
     b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
@@ -1042,6 +1173,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       msm.win = c.take<G2J>(4);
     }
     b.req_status = c.take<int32_t>(R);
+    b.indiv_f = c.take<Fp12>(R);
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
       ptree[1] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
@@ -1051,6 +1183,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   auto carve_res = [&](Carver& c, PipeBufs& b) {
     b.chunk_ok = c.take<int32_t>(n_chunks);
     b.indiv_verdict = c.take<int32_t>(R);
+    b.grp_verdict = c.take<int32_t>(grp_cap);
     b.req_status_host = c.take<int32_t>(R);
     b.flag_count_host = c.take<uint32_t>(1);
     merged_ok = merged ? c.take<int32_t>(1) : nullptr;
@@ -1312,10 +1445,23 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     return 0;
   }
 
+  // Requests verified on their own: the non-batchable ones, then the failed chunks'
+  // (worker.ts:91-98).  A failed chunk of >= GT_MIN_REQS requests is group-tested
+  // instead of paying one final exponentiation per request (verify_groups below); its
+  // requests follow the directly verified ones in the list.
   std::vector<uint32_t> indiv = plan.nonbatch_reqs;
-  for (uint32_t ch = 0; ch < n_chunks; ++ch)
-    if (chunk_ok[ch] != 1)
+  std::vector<std::pair<uint32_t, uint32_t>> gt_chunks;  // [beg, end) of a group-tested chunk in indiv
+  const uint32_t gt_min = group_test_min();
+  for (int pass = 0; pass < 2; ++pass)
+    for (uint32_t ch = 0; ch < n_chunks; ++ch) {
+      if (chunk_ok[ch] == 1) continue;
+      const uint32_t m = plan.chunk_off[ch + 1] - plan.chunk_off[ch];
+      if ((m >= gt_min) != (pass == 1)) continue;
+      const uint32_t beg = (uint32_t)indiv.size();
       for (uint32_t k = plan.chunk_off[ch]; k < plan.chunk_off[ch + 1]; ++k) indiv.push_back(plan.chunk_reqs[k]);
+      if (pass == 1) gt_chunks.push_back({beg, (uint32_t)indiv.size()});
+    }
+  const uint32_t n_direct = gt_chunks.empty() ? (uint32_t)indiv.size() : gt_chunks.front().first;
   std::vector<int32_t> indiv_verdict(indiv.size() + 1, 0);
   std::vector<uint32_t> groups;  // k_fold groups; outlives the async copy (synchronised below)
   GsumPlan indiv_gsum;           // likewise
@@ -1385,12 +1531,19 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       stage_copy(ctx, b.fold_groups, groups.data(), sizeof(uint32_t) * groups.size());
       HIPC(ctx, launch_k_fold(b, ctx->coop, s)); dbg_sync(s, "k_fold");
     }
+    b.n_indiv_direct = n_direct;
     HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, s)); dbg_sync(s, "k_indiv_coop");
-    HIPC(ctx, hipEventRecord(ctx->ev[8], s));
+    if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev[8], s));
   }
-  HIPC(ctx, hipEventRecord(ctx->ev1, s));
+  if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev1, s));
   HIPC(ctx, hipStreamSynchronize(s));
   if (!indiv.empty()) memcpy(indiv_verdict.data(), res_host(ctx, b.indiv_verdict), sizeof(int32_t) * indiv.size());
+  if (!gt_chunks.empty()) {
+    if (const int rc = verify_groups(ctx, b, gt_chunks, indiv_verdict, s, grp_cap, grp_mem_cap)) return rc;
+    HIPC(ctx, hipEventRecord(ctx->ev[8], s));
+    HIPC(ctx, hipEventRecord(ctx->ev1, s));
+    HIPC(ctx, hipStreamSynchronize(s));
+  }
   assemble_verdicts(in, plan, chunk_ok.data(), indiv, indiv_verdict.data(), verdicts, stats);
   if (stats) {
     float ms = 0.f;

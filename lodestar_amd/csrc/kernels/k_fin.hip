@@ -3,7 +3,9 @@
 //   k_chunk_coop  one task per chunk of >= 16 batchable requests
 //                 (worker.ts:56-88: random-scalar batch over the chunk's sets)
 //   k_indiv_coop  one task per request verified on its own
-//                 (failed chunks' requests and non-batchable requests, worker.ts:91-98)
+//                 (failed chunks' requests and non-batchable requests, worker.ts:91-98);
+//                 a failed chunk's requests under group testing only leave their product
+//   k_group_coop  one task per group test: FE(prod of its requests' products) == 1
 // Task: F = prod f_i, verdict = (FE(F) == 1).  Each f_i holds both pairings of its
 // set (k_pset), or (aggregated-signature path, b.sigagg) only e(r pk, H) and the task
 // multiplies in its group's virtual set ML(-g1, sum r_i sig_i).
@@ -84,8 +86,42 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
   const uint32_t stride = b.fold > 1 ? b.fold : 1u;  // f's pre-multiplied in groups by k_fold
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set(b, env, sh, i, first);
   if (b.sigagg) fin_accumulate_set(b, env, sh, b.indiv_vbase + t, first);  // the request's own signature sum
+  if (t >= b.n_indiv_direct) {  // group-tested: the product only (k_group_coop)
+    if (threadIdx.x < 12) reinterpret_cast<Fp*>(&b.indiv_f[t])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
+    if (threadIdx.x == 0) b.indiv_verdict[t] = 2;
+    return;
+  }
   bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) b.indiv_verdict[t] = ok ? 1 : 0;
+}
+
+// One group test: the requests' products (k_indiv_coop, indiv_f) multiplied, then one
+// final exponentiation -- the same check as the requests' batch over their sets with the
+// call's scalars (each product already holds both pairings of every set, or the
+// request's own signature-sum pairing).
+__global__ __launch_bounds__(COOP_LANES) void k_group_coop(PipeBufs b, CoopEnv env) {
+  BLS_TAIL_PRIO();
+  __shared__ FinShared sh;
+  const uint32_t g = blockIdx.x;
+  const uint32_t beg = b.grp_off[g], end = b.grp_off[g + 1];
+  fin_init(env, sh);
+  for (uint32_t k = beg; k < end; ++k) {
+    const Fp* src = reinterpret_cast<const Fp*>(&b.indiv_f[b.grp_members[k]]);
+    if (k == beg) {
+      coop_load(sh.frame, FIN_F, src, 12);
+    } else {
+      coop_load(sh.frame, FIN_G, src, 12);
+      coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
+    }
+  }
+  bool ok = fin_finish(env, sh);
+  if (threadIdx.x == 0) b.grp_verdict[g] = ok ? 1 : 0;
+}
+
+hipError_t launch_k_group_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
+  if (b.n_grp == 0) return hipSuccess;
+  k_group_coop<<<b.n_grp, COOP_LANES, 0, s>>>(b, env);
+  return hipGetLastError();
 }
 
 // Fold the f_i of individually verified requests in groups of b.fold consecutive sets

@@ -879,6 +879,40 @@ def test_failed_chunk_requests_verified_alone(gpu, oracle, table, n, bad):
     assert (st.batch_retries, st.batch_sigs_success, st.merged_check) == (retries, ok, 2)
 
 
+def test_failed_chunks_group_tested(gpu, oracle, table, verify_path):
+    """Failed chunks are group-tested (bls_gpu.hip verify_groups: bit-index groups, then
+    the decoded request alone and the rest together, else every request alone): one
+    invalid request at the first / a middle / the last position, two in one chunk (the
+    every-request-alone pass), an undecodable signature with every other request valid
+    (the group of the rest passes), an undecodable one next to an invalid one, and the
+    same with chunks of 5 requests.  Verdicts and worker counters are the reference's."""
+    n = 1024
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"gt-%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+    bad = {16 + 0, 32 + 7, 48 + 15, 64 + 3, 64 + 12, 96 + 9, 1000}
+    undecodable = {80 + 4, 96 + 2}
+    for per_req in (1, 3):  # single-set requests (chunks of 16) and 3-set requests (chunks of 5-6)
+        reqs, expect = [], []
+        for r in range(n // per_req):
+            ss, code = [], 1
+            for i in range(r * per_req, (r + 1) * per_req):
+                sig = sigs[i].tobytes()
+                if i in bad:
+                    sig = sigs[(i + 1) % n].tobytes()
+                    code = min(code, 0) if code >= 0 else code
+                if i in undecodable:
+                    sig, code = bytes(96), -CODE_BAD_ENCODING
+                ss.append(([i % 16], msgs[i], sig))
+            reqs.append((True, ss))
+            expect.append(code)
+        v, st = gpu.verify_packed(pack_requests(reqs))
+        assert list(v) == expect, per_req
+        if per_req == 1:
+            retries, ok = _expected_stats(oracle, expect)
+            assert (st.batch_retries, st.batch_sigs_success) == (retries, ok)
+
+
 def test_msm_signature_sum_matches_chains(gpu, oracle, table, verify_path):
     """The Pippenger merged signature sum (BLS_DEBUG_MSM, kernels/k_msm.hip) gives the
     verdicts and worker stats of the per-set [r] sig chains: 2,048 batchable sets (buckets
