@@ -121,18 +121,24 @@ struct PipeBufs {
   uint32_t* ml_lines;  // line buffer of the split SIMT Miller loops (k_mlq -> k_mlf), nullable
   uint32_t* set_flag;  // n_sets: 1 = take the exact single-lane path (stage_exact_set)
   uint32_t* flag_count;  // 1 word: sets flagged by the cooperative kernel (GPU path)
-  // Group tests over a failed chunk's requests (bls_gpu.hip verify_body): requests
-  // t >= n_indiv_direct leave their product F_t in indiv_f (no final exponentiation,
-  // indiv_verdict[t] = 2); k_group_coop checks FE(prod of the F_t of each group) == 1
-  uint32_t n_indiv_direct;
-  Fp12* indiv_f;                  // n_indiv
-  const uint32_t* grp_off;        // n_grp + 1
-  const uint32_t* grp_members;    // indices t into the indiv list
-  uint32_t n_grp;
   // outputs
   int32_t* chunk_ok;       // n_chunks: 1 ok, 0 failed (retry)
-  int32_t* indiv_verdict;  // n_indiv: 1 / 0 / -code (2: product left in indiv_f)
-  int32_t* grp_verdict;    // n_grp: 1 / 0
+  int32_t* indiv_verdict;  // n_indiv: 1 / 0 / -code (2: product left for the group tests)
+};
+
+// Group tests over failed chunks' requests (bls_gpu.hip verify_groups; kernels/k_fin.hip):
+// requests t >= n_direct of the indiv list leave their product F_t in f (no final
+// exponentiation); k_group_coop checks FE(prod of the F_t of each group) == 1.  Kernel
+// arguments of their own, not PipeBufs fields: PipeBufs is passed by value to every
+// kernel and a larger one grows the scratch frame of kernels that take its address
+// (k_chain 3,440 -> 3,488 B per lane cost 13 % of the plateau, gpurun_out/r4u, r4v).
+struct GroupBufs {
+  uint32_t n_direct;
+  Fp12* f;                   // n_indiv
+  const uint32_t* off;       // n + 1
+  const uint32_t* members;   // indices t into the indiv list
+  uint32_t n;
+  int32_t* verdict;          // n: 1 / 0 (host-mapped)
 };
 
 BLS_HD void scalar_words_from_be32(const uint8_t* b, uint32_t k[8]) {

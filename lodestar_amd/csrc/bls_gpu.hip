@@ -631,21 +631,22 @@ static uint32_t group_test_min() {
 }
 
 // run the tests (goff: offsets into gmem, indices into the indiv list); results in gv
-static int run_group_tests(bls_gpu_ctx* ctx, PipeBufs& b, const std::vector<uint32_t>& goff,
+static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, const std::vector<uint32_t>& goff,
                            const std::vector<uint32_t>& gmem, std::vector<int32_t>& gv, hipStream_t s) {
   gv.assign(goff.size() - 1, 0);
   if (gv.empty()) return 0;
-  stage_copy(ctx, b.grp_off, goff.data(), sizeof(uint32_t) * goff.size());  // the stream is idle
-  stage_copy(ctx, b.grp_members, gmem.data(), sizeof(uint32_t) * gmem.size());
-  b.n_grp = (uint32_t)gv.size();
-  HIPC(ctx, launch_k_group_coop(b, ctx->coop, s)); dbg_sync(s, "k_group_coop");
+  stage_copy(ctx, g.off, goff.data(), sizeof(uint32_t) * goff.size());  // the stream is idle
+  stage_copy(ctx, g.members, gmem.data(), sizeof(uint32_t) * gmem.size());
+  g.n = (uint32_t)gv.size();
+  HIPC(ctx, launch_k_group_coop(b, ctx->coop, g, s)); dbg_sync(s, "k_group_coop");
   HIPC(ctx, hipStreamSynchronize(s));
-  memcpy(gv.data(), res_host(ctx, b.grp_verdict), sizeof(int32_t) * gv.size());
+  memcpy(gv.data(), res_host(ctx, g.verdict), sizeof(int32_t) * gv.size());
   return 0;
 }
 
-static int verify_groups(bls_gpu_ctx* ctx, PipeBufs& b, const std::vector<std::pair<uint32_t, uint32_t>>& chunks,
-                         std::vector<int32_t>& verdict, hipStream_t s, size_t grp_cap, size_t grp_mem_cap) {
+static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
+                         const std::vector<std::pair<uint32_t, uint32_t>>& chunks, std::vector<int32_t>& verdict,
+                         hipStream_t s, size_t grp_cap, size_t grp_mem_cap) {
   struct Chunk {
     std::vector<uint32_t> ok;  // indiv indices of the requests of status OK
     bool has_err = false;
@@ -682,7 +683,7 @@ static int verify_groups(bls_gpu_ctx* ctx, PipeBufs& b, const std::vector<std::p
     return -3;
   }
   std::vector<int32_t> gv;
-  if (run_group_tests(ctx, b, goff, gmem, gv, s)) return -1;
+  if (run_group_tests(ctx, b, gbufs, goff, gmem, gv, s)) return -1;
   // decode pass A; plan pass B
   std::vector<uint32_t> goff_b{0}, gmem_b, alone;  // alone: requests for pass C
   std::vector<size_t> in_b;
@@ -712,7 +713,7 @@ static int verify_groups(bls_gpu_ctx* ctx, PipeBufs& b, const std::vector<std::p
     goff_b.push_back((uint32_t)gmem_b.size());
     in_b.push_back(i);
   }
-  if (run_group_tests(ctx, b, goff_b, gmem_b, gv, s)) return -1;
+  if (run_group_tests(ctx, b, gbufs, goff_b, gmem_b, gv, s)) return -1;
   for (size_t q = 0; q < in_b.size(); ++q) {
     Chunk& c = cs[in_b[q]];
     if (gv[2 * q] == 0 && gv[2 * q + 1] == 1) {
@@ -724,7 +725,7 @@ static int verify_groups(bls_gpu_ctx* ctx, PipeBufs& b, const std::vector<std::p
   // pass C: one test per request
   std::vector<uint32_t> goff_c{0};
   for (size_t k = 0; k < alone.size(); ++k) goff_c.push_back((uint32_t)k + 1);
-  if (run_group_tests(ctx, b, goff_c, alone, gv, s)) return -1;
+  if (run_group_tests(ctx, b, gbufs, goff_c, alone, gv, s)) return -1;
   for (size_t k = 0; k < alone.size(); ++k) verdict[alone[k]] = gv[k] == 1 ? 1 : 0;
   return 0;
 }
@@ -1112,6 +1113,8 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // chunk (chunks of < 8192 requests) of <= 8 m members in all, pass B 2 tests, pass C one
   // test per request
   const size_t grp_cap = (size_t)R + 14ull * n_chunks + 2, grp_mem_cap = 8ull * R + 16;
+  GroupBufs gbufs;
+  memset(&gbufs, 0, sizeof(gbufs));
   auto carve = [&](Carver& c, PipeBufs& b, size_t& input_end) {
     b.req_off = c.take<uint32_t>(R + 1);
     b.chunk_off = c.take<uint32_t>(n_chunks + 1);
@@ -1127,8 +1130,8 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.sigs = c.take<uint8_t>(96ull * n);
     b.sig_lens = in->signature_lens ? c.take<uint32_t>(n) : nullptr;
     b.indiv_reqs = c.take<uint32_t>(R);
-    b.grp_off = c.take<uint32_t>(grp_cap + 1);
-    b.grp_members = c.take<uint32_t>(grp_mem_cap);
+    gbufs.off = c.take<uint32_t>(grp_cap + 1);
+    gbufs.members = c.take<uint32_t>(grp_mem_cap);
     own_sets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
     b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
     b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
@@ -1173,7 +1176,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       msm.win = c.take<G2J>(4);
     }
     b.req_status = c.take<int32_t>(R);
-    b.indiv_f = c.take<Fp12>(R);
+    gbufs.f = c.take<Fp12>(R);
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
       ptree[1] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
@@ -1183,7 +1186,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   auto carve_res = [&](Carver& c, PipeBufs& b) {
     b.chunk_ok = c.take<int32_t>(n_chunks);
     b.indiv_verdict = c.take<int32_t>(R);
-    b.grp_verdict = c.take<int32_t>(grp_cap);
+    gbufs.verdict = c.take<int32_t>(grp_cap);
     b.req_status_host = c.take<int32_t>(R);
     b.flag_count_host = c.take<uint32_t>(1);
     merged_ok = merged ? c.take<int32_t>(1) : nullptr;
@@ -1531,15 +1534,15 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       stage_copy(ctx, b.fold_groups, groups.data(), sizeof(uint32_t) * groups.size());
       HIPC(ctx, launch_k_fold(b, ctx->coop, s)); dbg_sync(s, "k_fold");
     }
-    b.n_indiv_direct = n_direct;
-    HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, s)); dbg_sync(s, "k_indiv_coop");
+    gbufs.n_direct = n_direct;
+    HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, gbufs, s)); dbg_sync(s, "k_indiv_coop");
     if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev[8], s));
   }
   if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev1, s));
   HIPC(ctx, hipStreamSynchronize(s));
   if (!indiv.empty()) memcpy(indiv_verdict.data(), res_host(ctx, b.indiv_verdict), sizeof(int32_t) * indiv.size());
   if (!gt_chunks.empty()) {
-    if (const int rc = verify_groups(ctx, b, gt_chunks, indiv_verdict, s, grp_cap, grp_mem_cap)) return rc;
+    if (const int rc = verify_groups(ctx, b, gbufs, gt_chunks, indiv_verdict, s, grp_cap, grp_mem_cap)) return rc;
     HIPC(ctx, hipEventRecord(ctx->ev[8], s));
     HIPC(ctx, hipEventRecord(ctx->ev1, s));
     HIPC(ctx, hipStreamSynchronize(s));

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv e
   if (threadIdx.x == 0) b.chunk_ok[c] = ok ? 1 : 0;
 }
 
-__global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv env) {
+__global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv env, GroupBufs gb) {
   BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t t = blockIdx.x;
@@ -86,8 +86,8 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
   const uint32_t stride = b.fold > 1 ? b.fold : 1u;  // f's pre-multiplied in groups by k_fold
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set(b, env, sh, i, first);
   if (b.sigagg) fin_accumulate_set(b, env, sh, b.indiv_vbase + t, first);  // the request's own signature sum
-  if (t >= b.n_indiv_direct) {  // group-tested: the product only (k_group_coop)
-    if (threadIdx.x < 12) reinterpret_cast<Fp*>(&b.indiv_f[t])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
+  if (t >= gb.n_direct) {  // group-tested: the product only (k_group_coop)
+    if (threadIdx.x < 12) reinterpret_cast<Fp*>(&gb.f[t])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
     if (threadIdx.x == 0) b.indiv_verdict[t] = 2;
     return;
   }
@@ -99,14 +99,14 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
 // final exponentiation -- the same check as the requests' batch over their sets with the
 // call's scalars (each product already holds both pairings of every set, or the
 // request's own signature-sum pairing).
-__global__ __launch_bounds__(COOP_LANES) void k_group_coop(PipeBufs b, CoopEnv env) {
+__global__ __launch_bounds__(COOP_LANES) void k_group_coop(CoopEnv env, GroupBufs gb) {
   BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t g = blockIdx.x;
-  const uint32_t beg = b.grp_off[g], end = b.grp_off[g + 1];
+  const uint32_t beg = gb.off[g], end = gb.off[g + 1];
   fin_init(env, sh);
   for (uint32_t k = beg; k < end; ++k) {
-    const Fp* src = reinterpret_cast<const Fp*>(&b.indiv_f[b.grp_members[k]]);
+    const Fp* src = reinterpret_cast<const Fp*>(&gb.f[gb.members[k]]);
     if (k == beg) {
       coop_load(sh.frame, FIN_F, src, 12);
     } else {
@@ -115,12 +115,12 @@ __global__ __launch_bounds__(COOP_LANES) void k_group_coop(PipeBufs b, CoopEnv e
     }
   }
   bool ok = fin_finish(env, sh);
-  if (threadIdx.x == 0) b.grp_verdict[g] = ok ? 1 : 0;
+  if (threadIdx.x == 0) gb.verdict[g] = ok ? 1 : 0;
 }
 
-hipError_t launch_k_group_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
-  if (b.n_grp == 0) return hipSuccess;
-  k_group_coop<<<b.n_grp, COOP_LANES, 0, s>>>(b, env);
+hipError_t launch_k_group_coop(const PipeBufs&, const CoopEnv& env, const GroupBufs& g, hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  k_group_coop<<<g.n, COOP_LANES, 0, s>>>(env, g);
   return hipGetLastError();
 }
 
@@ -189,8 +189,8 @@ hipError_t launch_k_chunk_coop(const PipeBufs& b, const CoopEnv& env, hipStream_
   k_chunk_coop<<<b.n_chunks, COOP_LANES, 0, s>>>(b, env);
   return hipGetLastError();
 }
-hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
-  k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env);
+hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, const GroupBufs& g, hipStream_t s) {
+  k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env, g);
   return hipGetLastError();
 }
 

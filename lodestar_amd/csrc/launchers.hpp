@@ -74,8 +74,10 @@ size_t kernel_probe_out_bytes(const char* name);
 hipError_t launch_kernel_probe(const char* name, void* out, uint32_t lanes, hipStream_t s);
 #include "bls/coop.hpp"
 hipError_t launch_k_chunk_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
-hipError_t launch_k_indiv_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
-hipError_t launch_k_group_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
+hipError_t launch_k_indiv_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, const bls::GroupBufs& g,
+                              hipStream_t s);
+hipError_t launch_k_group_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, const bls::GroupBufs& g,
+                              hipStream_t s);
 hipError_t launch_k_fold(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
 #define BLS_FOLD 16u  // sets per k_fold group
 hipError_t launch_k_coop_probe(const bls::CoopEnv& env, bls::CoopProg pg, uint32_t blocks, uint32_t reps,
