@@ -312,6 +312,10 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
  * per two lanes; 0 = by the process's sets in flight). */
 #define BLS_DEBUG_MLF_PL(n) ((uint32_t)(n) << 12)
 #define BLS_DEBUG_MLF_PL_MASK 0x7000u
+/* Test / bench hook: group-test failed chunks of >= 4 requests whatever
+ * $BLS_GROUP_TEST_MIN says (off by default: the tests cut final exponentiations, not
+ * the requests' own signature-sum Miller loops, and their extra rounds cost more). */
+#define BLS_DEBUG_GROUP_TEST 128u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

@@ -88,6 +88,7 @@ DEBUG_SIGAGG_ON = 8
 DEBUG_SIGAGG_OFF = 16
 DEBUG_NO_UNITS = 32
 DEBUG_MSM = 64
+DEBUG_GROUP_TEST = 128
 
 
 def DEBUG_MLF_PL(n: int) -> int:

@@ -620,14 +620,18 @@ static void dbg_sync(hipStream_t s, const char* what) {
 // With one invalid request in a chunk of 16 that is 6 final exponentiations instead of
 // 16; verdicts and the worker counters are the reference's (a test that passes is the
 // batch the reference's retry would have passed request by request, with the same
-// soundness).  $BLS_GROUP_TEST_MIN (default 4; 0 = off) is the smallest chunk tested so.
-static uint32_t group_test_min() {
+// soundness).  Off by default: each request still pays its own signature-sum Miller loop
+// (the larger part of its cost on the aggregated path) and the two extra rounds of
+// dependent launches cost more than the saved exponentiations -- cfg4 per-set requests
+// 0.875M vs 0.910M sets/s (profiles/r04_ab_group_test.json).  $BLS_GROUP_TEST_MIN (the
+// smallest chunk tested so; 0 = off) or BLS_DEBUG_GROUP_TEST (chunks of >= 4) turn it on.
+static uint32_t group_test_min(const bls_gpu_ctx* ctx) {
   static const uint32_t v = [] {
     const char* e = getenv("BLS_GROUP_TEST_MIN");
-    const long x = e ? atol(e) : 4;
+    const long x = e ? atol(e) : 0;
     return x <= 0 ? 0xFFFFFFFFu : (uint32_t)(x < 2 ? 2 : x);
   }();
-  return v;
+  return (ctx->debug_flags & BLS_DEBUG_GROUP_TEST) ? 4u : v;
 }
 
 // run the tests (goff: offsets into gmem, indices into the indiv list); results in gv
@@ -1454,7 +1458,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // requests follow the directly verified ones in the list.
   std::vector<uint32_t> indiv = plan.nonbatch_reqs;
   std::vector<std::pair<uint32_t, uint32_t>> gt_chunks;  // [beg, end) of a group-tested chunk in indiv
-  const uint32_t gt_min = group_test_min();
+  const uint32_t gt_min = group_test_min(ctx);
   for (int pass = 0; pass < 2; ++pass)
     for (uint32_t ch = 0; ch < n_chunks; ++ch) {
       if (chunk_ok[ch] == 1) continue;

@@ -906,11 +906,18 @@ def test_failed_chunks_group_tested(gpu, oracle, table, verify_path):
                 ss.append(([i % 16], msgs[i], sig))
             reqs.append((True, ss))
             expect.append(code)
-        v, st = gpu.verify_packed(pack_requests(reqs))
-        assert list(v) == expect, per_req
-        if per_req == 1:
-            retries, ok = _expected_stats(oracle, expect)
-            assert (st.batch_retries, st.batch_sigs_success) == (retries, ok)
+        from lodestar_amd._abi import DEBUG_GROUP_TEST
+
+        for flags in (0, DEBUG_GROUP_TEST):
+            try:
+                gpu.set_debug_flags(flags)
+                v, st = gpu.verify_packed(pack_requests(reqs))
+            finally:
+                gpu.set_debug_flags(0)
+            assert list(v) == expect, (per_req, flags)
+            if per_req == 1:
+                retries, ok = _expected_stats(oracle, expect)
+                assert (st.batch_retries, st.batch_sigs_success) == (retries, ok)
 
 
 def test_msm_signature_sum_matches_chains(gpu, oracle, table, verify_path):
