@@ -80,6 +80,9 @@ struct CoopEnv {
   // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln, the
   // cooperative packings tests force): 1 or 2 sets per wavefront (COOP_FRAME)
   CoopProg ml1_1, ml1_2;
+  // the device copy of this struct (bls_gpu.hip load_coop_tables): kernels take it by
+  // pointer -- by value it made their arguments (with PipeBufs) ~830 bytes
+  const CoopEnv* dev;
 };
 
 // fin frame registers

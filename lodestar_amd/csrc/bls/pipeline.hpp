@@ -129,9 +129,7 @@ struct PipeBufs {
 // Group tests over failed chunks' requests (bls_gpu.hip verify_groups; kernels/k_fin.hip):
 // requests t >= n_direct of the indiv list leave their product F_t in f (no final
 // exponentiation); k_group_coop checks FE(prod of the F_t of each group) == 1.  Kernel
-// arguments of their own, not PipeBufs fields: PipeBufs is passed by value to every
-// kernel and a larger one grows the scratch frame of kernels that take its address
-// (k_chain 3,440 -> 3,488 B per lane cost 13 % of the plateau, gpurun_out/r4u, r4v).
+// arguments of their own (only the two final-exponentiation kernels use them).
 struct GroupBufs {
   uint32_t n_direct;
   Fp12* f;                   // n_indiv

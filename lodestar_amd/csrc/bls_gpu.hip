@@ -216,9 +216,10 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
     return -1;
   }
   static_assert(sizeof(CoopOp) == 80, "CoopOp layout");
-  // device copy: [ops | consts]
+  // device copy: [ops | consts | the CoopEnv struct (filled at the end)]
   size_t ops_bytes = (steps_bytes + 255) & ~(size_t)255;
-  HIPC(ctx, hipMalloc(&ctx->coop_dev, ops_bytes + (size_t)h.n_consts * sizeof(Fp)));
+  const size_t env_off = (ops_bytes + (size_t)h.n_consts * sizeof(Fp) + 255) & ~(size_t)255;
+  HIPC(ctx, hipMalloc(&ctx->coop_dev, env_off + sizeof(CoopEnv)));
   uint8_t* d = (uint8_t*)ctx->coop_dev;
   HIPC(ctx, hipMemcpy(d, buf.data() + steps_off, steps_bytes, hipMemcpyHostToDevice));
   HIPC(ctx, hipMemcpy(d + ops_bytes, buf.data() + consts_off, (size_t)h.n_consts * sizeof(Fp), hipMemcpyHostToDevice));
@@ -294,6 +295,10 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
       return -1;
     }
   }
+  // kernels take the struct by pointer (its ~370 bytes by value, next to PipeBufs, made
+  // the cooperative kernels' arguments ~830 bytes)
+  ctx->coop.dev = (const CoopEnv*)((uint8_t*)ctx->coop_dev + env_off);
+  HIPC(ctx, hipMemcpy((void*)ctx->coop.dev, &ctx->coop, sizeof(CoopEnv), hipMemcpyHostToDevice));
   return 0;
 }
 

@@ -43,7 +43,8 @@ __device__ void fin_init(const CoopEnv& env, FinShared& sh) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv env) {
+__global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, const CoopEnv* __restrict__ envp) {
+  const CoopEnv& env = *envp;
   BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t c = blockIdx.x;
@@ -71,7 +72,8 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, CoopEnv e
   if (threadIdx.x == 0) b.chunk_ok[c] = ok ? 1 : 0;
 }
 
-__global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv env, GroupBufs gb) {
+__global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, const CoopEnv* __restrict__ envp, GroupBufs gb) {
+  const CoopEnv& env = *envp;
   BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t t = blockIdx.x;
@@ -99,7 +101,8 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, CoopEnv e
 // final exponentiation -- the same check as the requests' batch over their sets with the
 // call's scalars (each product already holds both pairings of every set, or the
 // request's own signature-sum pairing).
-__global__ __launch_bounds__(COOP_LANES) void k_group_coop(CoopEnv env, GroupBufs gb) {
+__global__ __launch_bounds__(COOP_LANES) void k_group_coop(const CoopEnv* __restrict__ envp, GroupBufs gb) {
+  const CoopEnv& env = *envp;
   BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t g = blockIdx.x;
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_group_coop(CoopEnv env, GroupBuf
 
 hipError_t launch_k_group_coop(const PipeBufs&, const CoopEnv& env, const GroupBufs& g, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  k_group_coop<<<g.n, COOP_LANES, 0, s>>>(env, g);
+  k_group_coop<<<g.n, COOP_LANES, 0, s>>>(env.dev, g);
   return hipGetLastError();
 }
 
@@ -128,7 +131,8 @@ hipError_t launch_k_group_coop(const PipeBufs&, const CoopEnv& env, const GroupB
 // (one wavefront per group, groups of all requests in parallel) so k_indiv_coop's
 // sequential product over a large request (a 128-set block call: 127 Fp12 products)
 // shrinks to one product per group.
-__global__ __launch_bounds__(COOP_LANES) void k_fold(PipeBufs b, CoopEnv env) {
+__global__ __launch_bounds__(COOP_LANES) void k_fold(PipeBufs b, const CoopEnv* __restrict__ envp) {
+  const CoopEnv& env = *envp;
   BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t beg = b.fold_groups[2 * blockIdx.x], end = b.fold_groups[2 * blockIdx.x + 1];
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(COOP_LANES) void k_fold(PipeBufs b, CoopEnv env) {
 }
 
 hipError_t launch_k_fold(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
-  k_fold<<<b.n_fold, COOP_LANES, 0, s>>>(b, env);
+  k_fold<<<b.n_fold, COOP_LANES, 0, s>>>(b, env.dev);
   return hipGetLastError();
 }
 
@@ -152,7 +156,8 @@ hipError_t launch_k_fold(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
 // (one block, n <= FPROD_FAN) it runs the final exponentiation of the product
 // instead and writes FE(prod) == 1.
 __global__ __launch_bounds__(COOP_LANES) void k_fprod(const Fp12* in, uint32_t n, Fp12* out, int32_t* verdict,
-                                                      CoopEnv env) {
+                                                      const CoopEnv* __restrict__ envp) {
+  const CoopEnv& env = *envp;
   BLS_TAIL_PRIO();
   __shared__ FinShared sh;
   const uint32_t beg = blockIdx.x * FPROD_FAN;
@@ -181,23 +186,24 @@ hipError_t launch_k_fprod(const Fp12* in, uint32_t n, Fp12* out, int32_t* verdic
                           hipStream_t s) {
   const uint32_t blocks = verdict ? 1u : (n + FPROD_FAN - 1) / FPROD_FAN;
   if (n == 0 || (verdict && n > FPROD_FAN)) return hipErrorInvalidValue;
-  k_fprod<<<blocks, COOP_LANES, 0, s>>>(in, n, out, verdict, env);
+  k_fprod<<<blocks, COOP_LANES, 0, s>>>(in, n, out, verdict, env.dev);
   return hipGetLastError();
 }
 
 hipError_t launch_k_chunk_coop(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
-  k_chunk_coop<<<b.n_chunks, COOP_LANES, 0, s>>>(b, env);
+  k_chunk_coop<<<b.n_chunks, COOP_LANES, 0, s>>>(b, env.dev);
   return hipGetLastError();
 }
 hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, const GroupBufs& g, hipStream_t s) {
-  k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env, g);
+  k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env.dev, g);
   return hipGetLastError();
 }
 
 // Probe: run program `pg` `reps` times on a block-private frame of pseudo-random
 // field elements (timing of the interpreter; results discarded).
-__global__ __launch_bounds__(COOP_LANES) void k_coop_probe(CoopEnv env, CoopProg pg, uint32_t reps, uint32_t* sink,
+__global__ __launch_bounds__(COOP_LANES) void k_coop_probe(const CoopEnv* __restrict__ envp, CoopProg pg, uint32_t reps, uint32_t* sink,
                                                           uint64_t* stamps) {
+  const CoopEnv& env = *envp;
   __shared__ CoopLdsN<COOP_FRAME3> sh;  // large enough for every program (1-, 2- and 3-set frames)
   coop_stage_consts(env, sh.cbank);
   for (int k = threadIdx.x; k < COOP_FRAME3; k += COOP_LANES) {
@@ -214,6 +220,6 @@ __global__ __launch_bounds__(COOP_LANES) void k_coop_probe(CoopEnv env, CoopProg
 
 hipError_t launch_k_coop_probe(const CoopEnv& env, CoopProg pg, uint32_t blocks, uint32_t reps, uint32_t* sink,
                                uint64_t* stamps, hipStream_t s) {
-  k_coop_probe<<<blocks, COOP_LANES, 0, s>>>(env, pg, reps, sink, stamps);
+  k_coop_probe<<<blocks, COOP_LANES, 0, s>>>(env.dev, pg, reps, sink, stamps);
   return hipGetLastError();
 }

@@ -54,7 +54,8 @@ __device__ __forceinline__ void pset_flag(const PipeBufs& b, uint32_t i) {
   atomicAdd(b.flag_count, 1u);
 }
 
-__global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
+__global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, const CoopEnv* __restrict__ envp) {
+  const CoopEnv& env = *envp;
   __shared__ PsetShared sh;
   const uint32_t i = blockIdx.x;
   const int lane = threadIdx.x;
@@ -113,7 +114,8 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, CoopEnv env) {
 #define PSN_SLOTS 92
 
 template <int S, int FRAME_N>
-__global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, CoopEnv env) {
+__global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, const CoopEnv* __restrict__ envp) {
+  const CoopEnv& env = *envp;
   __shared__ CoopLdsN<FRAME_N> sh;
   const CoopPsetN& pg = env.packed[S - 2];
   const int lane = threadIdx.x;
@@ -261,8 +263,9 @@ __device__ __forceinline__ void mln_items(const PipeBufs& b, const CoopEnv& env,
 }
 
 template <int S, class Lds>
-__global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, CoopEnv env, uint32_t first, uint32_t count,
+__global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, const CoopEnv* __restrict__ envp, uint32_t first, uint32_t count,
                                                     uint32_t units_paired) {
+  const CoopEnv& env = *envp;
   __shared__ Lds sh;
   mln_items<S>(b, env, sh.frame, &sh.flag, (int)(sizeof(sh.frame) / sizeof(Fp)), first + (uint32_t)S * blockIdx.x,
                first + count, units_paired);
@@ -306,9 +309,9 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
   if (b.pack == 0 && b.ml_lines) return launch_k_mlqf(b, first, count, own_only, b.ml_lines, s);
   const uint32_t up = own_only ? 0u : 1u;
   if (b.pack == 2 && env.ml1_2.n > 0) {
-    k_mln<2, CoopLds><<<(count + 1) / 2, COOP_LANES, 0, s>>>(b, env, first, count, up);
+    k_mln<2, CoopLds><<<(count + 1) / 2, COOP_LANES, 0, s>>>(b, env.dev, first, count, up);
   } else {
-    k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env, first, count, up);
+    k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env.dev, first, count, up);
   }
   return hipGetLastError();
 }
@@ -316,11 +319,11 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
 hipError_t launch_k_pset(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
   const uint32_t S = (b.pack >= 1 && b.pack <= 3) ? b.pack : pack_for(b.n_sets);
   if (S == 3 && env.packed[1].ml2.n > 0) {
-    k_psetn<3, COOP_FRAME3><<<(b.n_sets + 2) / 3, COOP_LANES, 0, s>>>(b, env);
+    k_psetn<3, COOP_FRAME3><<<(b.n_sets + 2) / 3, COOP_LANES, 0, s>>>(b, env.dev);
   } else if (S == 2 && env.packed[0].ml2.n > 0) {
-    k_psetn<2, COOP_FRAME2><<<(b.n_sets + 1) / 2, COOP_LANES, 0, s>>>(b, env);
+    k_psetn<2, COOP_FRAME2><<<(b.n_sets + 1) / 2, COOP_LANES, 0, s>>>(b, env.dev);
   } else {
-    k_pset<<<b.n_sets, COOP_LANES, 0, s>>>(b, env);
+    k_pset<<<b.n_sets, COOP_LANES, 0, s>>>(b, env.dev);
   }
   return hipGetLastError();
 }
