@@ -84,28 +84,16 @@ def pack_of(n_sets: int) -> int:
 
 def pset_products_per_set(S: int) -> float:
     """Expected Fp products the per-set kernel executes per set with S sets per
-    wavefront (program MUL ops from lodestar_amd/_native/coop_programs.json; r's bits
-    uniform, so each of the 2^S r-masks of an addition step is equally likely)."""
+    wavefront (program MUL ops from lodestar_amd/_native/coop_programs.json): the |x|
+    chains, phase 2 and the two-pair Miller loop, shared by the wavefront's S sets, plus
+    k_pre's two GLV multiplications for RG and RP (work_model.json chain_r_pk each)."""
     pg = json.loads((ROOT / "lodestar_amd" / "_native" / "coop_programs.json").read_text())
+    wm = json.loads((ROOT / "lodestar_amd" / "_native" / "work_model.json").read_text())
     m = {k: v["mul_ops"] for k, v in pg.items()}
-    if S == 1:
-        # the |x| chains only; RG and RP come from k_pre's GLV lanes (two G1 scalar
-        # multiplications, work_model.json chain_r_pk each)
-        wm = json.loads((ROOT / "lodestar_amd" / "_native" / "work_model.json").read_text())
-        n = m["pset_prep"] + 63 * m["pset_dbl_all"]
-        n += sum(m["pset_add_x"] for i in range(62, -1, -1) if (X_ABS >> i) & 1)
-        return n + m["pset_phase2"] + m["pset_norm2"] + m["pset_affine2"] + m["pset_ml2"] + 2 * wm["chain_r_pk"]
-    p = f"pset{S}_"
-
-    def add(xb):
-        progs = [f"{p}add_{xb}{r:0{S}b}" for r in range(1 << S) if xb or r]
-        return sum(m[q] for q in progs) / (1 << S)
-
-    n = m[p + "prep"] + m[p + "dbl_r"] + add(0) + 63 * m[p + "dbl_all"]
-    for i in range(62, -1, -1):
-        n += add((X_ABS >> i) & 1)
+    p = "pset_" if S == 1 else f"pset{S}_"
+    n = m[p + "prep"] + 63 * m[p + "dbl_all"] + sum(m[p + "add_x"] for i in range(63) if (X_ABS >> i) & 1)
     n += m[p + "phase2"] + m[p + "norm2"] + m[p + "affine2"] + m[p + "ml2"]
-    return n / S
+    return n / S + 2 * wm["chain_r_pk"]
 
 
 SIGAGG_MIN_SETS = 512   # bls_gpu.hip use_sigagg: the aggregated-signature path from this call size on

@@ -65,7 +65,7 @@ struct CoopLdsN {
 // Programs of S sets packed in one wavefront (tools/gen_pset.py build_pset(S)):
 // add[(xb << S) | rmask], bit s of rmask = r bit of packed set s; add[0] unused
 struct CoopPsetN {
-  CoopProg prep, dbl_r, dbl_all, add[16], phase2, norm2, affine2, ml2;
+  CoopProg prep, dbl_all, add_x, phase2, norm2, affine2, ml2;
 };
 
 // Programs of the finalisation frame ("fin", tools/gen_coop.py:build_fin)

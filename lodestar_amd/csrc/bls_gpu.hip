@@ -247,25 +247,18 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
     e.name[31] = 0;
     ctx->coop_progs->push_back({std::string(e.name), CoopProg{e.first, e.n_steps}});
   }
-  // packed programs (tools/gen_pset.py S = 2, 3): pset{S}_{prep,...}, pset{S}_add_{xb}{rmask, S bits}
+  // packed programs (tools/gen_pset.py S = 2, 3): pset{S}_{prep, dbl_all, add_x, ...}
   std::vector<std::pair<std::string, CoopProg*>> want_packed;
   for (int S = 2; S <= 3; ++S) {
     CoopPsetN& pn = ctx->coop.packed[S - 2];
     const std::string pre = "pset" + std::to_string(S) + "_";
     want_packed.push_back({pre + "prep", &pn.prep});
-    want_packed.push_back({pre + "dbl_r", &pn.dbl_r});
     want_packed.push_back({pre + "dbl_all", &pn.dbl_all});
+    want_packed.push_back({pre + "add_x", &pn.add_x});
     want_packed.push_back({pre + "phase2", &pn.phase2});
     want_packed.push_back({pre + "norm2", &pn.norm2});
     want_packed.push_back({pre + "affine2", &pn.affine2});
     want_packed.push_back({pre + "ml2", &pn.ml2});
-    for (int xb = 0; xb < 2; ++xb)
-      for (int m = 0; m < (1 << S); ++m) {
-        if (!xb && !m) continue;
-        std::string bits;
-        for (int k = S - 1; k >= 0; --k) bits += ((m >> k) & 1) ? '1' : '0';
-        want_packed.push_back({pre + "add_" + std::to_string(xb) + bits, &pn.add[(xb << S) | m]});
-      }
   }
   for (auto& wp : want_packed) {
     bool found = false;

@@ -106,8 +106,8 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, const CoopEnv* 
 // S sets per wavefront (tools/gen_pset.py build_pset(S): set s at frame offset 92 s,
 // its zero-checks on flag bit s).  The same programs as k_pset scheduled jointly: the
 // narrow chains of one set leave most lanes idle, so further sets ride along at
-// almost no extra steps (r-chain and phase 2 unchanged; Miller loop 689 steps for
-// 2 sets, 935 for 3, vs 486 for 1).  A set that needs no programs (error status,
+// almost no extra steps (the |x| chains and phase 2 unchanged; Miller loop ~690 steps for
+// 2 sets, ~920 for 3, vs 486 for 1); RG and RP from k_pre as in k_pset.  A set that needs no programs (error status,
 // flagged) borrows the inputs of the first live set so every part of the frame holds
 // well-formed points; its results are dropped.  Controller decisions (program
 // choice, early exits) are wave-uniform.
@@ -138,41 +138,28 @@ __global__ __launch_bounds__(COOP_LANES) void k_psetn(PipeBufs b, const CoopEnv*
   }
   if (first_live < 0) return;
   uint32_t src[S];
-  uint64_t r[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    src[s] = i0 + (live[s] ? s : first_live);
-    r[s] = set_scalar(b.seed, b.scalar_base + src[s]);
-  }
+  for (int s = 0; s < S; ++s) src[s] = i0 + (live[s] ? s : first_live);
   coop_stage_consts(env, sh.cbank);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint32_t i = src[s], o = PSN_SLOTS * s;
+    const Fp* rp = reinterpret_cast<const Fp*>(b.rpts + 2ull * i);  // RP (x, y, z), RG (x, y, z)
     if (lane < 8) lds_store_fp(sh.frame, o + PS_Q0 + lane, b.q[8ull * i + lane]);
     if (lane >= 8 && lane < 12)
       lds_store_fp(sh.frame, o + PS_SIG + lane - 8, reinterpret_cast<const Fp*>(&b.sig[i])[lane - 8]);
     if (lane >= 12 && lane < 15)
       lds_store_fp(sh.frame, o + PS_PK + lane - 12, reinterpret_cast<const Fp*>(&b.pk[i])[lane - 12]);
+    if (lane >= 15 && lane < 18) lds_store_fp(sh.frame, o + PS_RP + lane - 15, rp[lane - 15]);
+    if (lane >= 18 && lane < 21) lds_store_fp(sh.frame, o + PS_RG + lane - 18, rp[3 + lane - 18]);
   }
   if (lane == 0) sh.flag = 0;
   __syncthreads();
 
-  auto rbits = [&](int k) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int s = 0; s < S; ++s) m |= (uint32_t)((r[s] >> k) & 1ull) << s;
-    return m;
-  };
   coop_run(env, pg.prep, sh.frame, sh.cbank, &sh.flag);
-  coop_run(env, pg.dbl_r, sh.frame, sh.cbank, &sh.flag);
-  {
-    const uint32_t m = rbits(63);
-    if (m) coop_run(env, pg.add[m], sh.frame, sh.cbank, &sh.flag);
-  }
   for (int k = 62; k >= 0; --k) {
     coop_run(env, pg.dbl_all, sh.frame, sh.cbank, &sh.flag);
-    const uint32_t m = (uint32_t)((PS_X_ABS >> k) & 1ull) << S | rbits(k);
-    if (m) coop_run(env, pg.add[m], sh.frame, sh.cbank, &sh.flag);
+    if ((PS_X_ABS >> k) & 1ull) coop_run(env, pg.add_x, sh.frame, sh.cbank, &sh.flag);
   }
   coop_run(env, pg.phase2, sh.frame, sh.cbank, &sh.flag);
   bool run[S];

@@ -106,7 +106,7 @@ def test_psetn_sets_per_wavefront(progs, oracle, S):
         fr = _frame_for(oracle, msg, sig, pk, rng.randrange(1, P))
         o = PS.SET_SLOTS * s
         frame[o:o + PS.SET_SLOTS] = fr[:PS.SET_SLOTS]
-        rs.append(rng.randrange(1, 1 << 64))
+        rs.append(_r_points(oracle, pk, rng.randrange(1, 1 << 64), rng))
         expect_one.append(good)
     flag, in_group = PS.run_psetn(pg, consts, frame, rs, simulate, _inv)
     assert flag == 0 and in_group == [True] * S

@@ -479,11 +479,11 @@ def build_all():
     consts = ConstBank()
     psi, iso = _curve_constants()
     progs = build_fin(consts)
-    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, psi, iso, G1X, G1Y)
+    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, psi, iso)
     # two / three sets packed per wavefront (k_psetn, large batches)
-    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, psi, iso, G1X, G1Y,
+    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME2, psi, iso,
                                  S=2, prefix="pset2")
-    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME3, psi, iso, G1X, G1Y,
+    progs += gen_pset.build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME3, psi, iso,
                                  S=3, prefix="pset3")
     # single-pair Miller loops of the aggregated-signature path as cooperative programs
     # (k_mln, the packings tests force; the default is the SIMT k_mlq / k_mlf): 1 or 2 sets

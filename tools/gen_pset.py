@@ -14,22 +14,18 @@ in G2 (checked here), so the batch product is the reference's element of GT whil
 both scalar chains run on G1 (3x cheaper than G2) and sig stays affine for the
 Miller loop (one inversion per set, for H only).
 
-Scalar multiplications run left to right, one doubling program per bit for every
-chain at once (lanes in parallel) and addition programs chosen per bit by the
-kernel: the |x| bits are fixed.  The r chains: with one set per wavefront (k_pset)
-the block's second wavefront computes RG and RP with two single-lane GLV
-multiplications while the first runs the |x| chains, and writes them into the frame
-before the Miller loop (k_pset.hip); the packed programs (S sets per wavefront,
-k_psetn) run them here, starting from g1 (resp. pk) for an implicit top bit 2^64
-and subtracting [2^64] g1 (a constant) resp. [2^64] pk, a pure doubling chain run in
-the same programs, so every set runs the same 64 steps.  Additions zero-check H: an
-exceptional case (possible only for adversarial signatures off the subgroup, or
-with negligible probability) flags the set for the exact single-lane path.
+The |x| multiplications run left to right, one doubling program per bit for both
+chains at once (lanes in parallel) and an addition program at the set bits of |x|.
+RG = [s] g1 and RP = [s] pk for the set's batch scalar s come from k_pre's GLV lanes
+(kernels/k_pre.hip pre_rpts) and are loaded into the frame with the set's inputs: as
+interpreter programs (a 64-bit double-and-add beside the |x| chains) they added ~290
+steps to every set's critical path.  Additions zero-check H: an exceptional case
+(possible only for adversarial signatures off the subgroup, or with negligible
+probability) flags the set for the exact single-lane path.
 
 Frame (slots):
   Q0 0..3  Q1 4..7  SIG 8..11 (affine)  PK 12..14 (G1 Jacobian)
   A 15..20 (cofactor chain [|x|]P)  C 21..26 (subgroup chain [|x|]sig)
-  D3 27..29 ([r + 2^64] g1)  D2 33..35 ([r + 2^64] pk)  E2 42..44 ([2^64] pk)  (packed only)
   PP 45..50 (P = iso(q0) + iso(q1))  H 51..56  RG 57..59  RP 63..65
   HQ 66..69 (affine)  INV_IN 74  INV_OUT 75  DIFF 76..79 (subgroup test)
   F 80..91 (f_i)  temporaries 92..FRAME-1
@@ -39,7 +35,7 @@ from __future__ import annotations
 from circuits import Circuit, Lin, schedule
 
 Q0, Q1, SIG, PK = 0, 4, 8, 12
-A, C, D3, D2, E2 = 15, 21, 27, 33, 42
+A, C = 15, 21
 PP, H, RG, RP = 45, 51, 57, 63
 HQ, INV_IN, INV_OUT, DIFF, F = 66, 74, 75, 76, 80
 REGS = set(range(0, 92))
@@ -254,45 +250,14 @@ def const2(t, v):
     return (t.c.const(v[0]) if v[0] else Lin(), t.c.const(v[1]) if v[1] else Lin())
 
 
-P_MOD = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
-_G1 = (0x17F1D3A73197D7942695638C4FA9AC0FC3688C4F9774B905A14E3A3F171BAC586C55E83FF97A1AEFFB3AF00ADB22C6BB,
-       0x08B3F481E3AAA0F1A09E30ED741D8AE4FCF5E095D5D00AF600DB18CB2C04B3EDD03CC744A2888AE40CAA232946C5E7E1)
-
-
-def _g1_dbl_affine(p):
-    x, y = p
-    lam = 3 * x * x * pow(2 * y, P_MOD - 2, P_MOD) % P_MOD
-    x3 = (lam * lam - 2 * x) % P_MOD
-    return x3, (lam * (x - x3) - y) % P_MOD
-
-
-def _g1_2_64():
-    p = _G1
-    for _ in range(64):
-        p = _g1_dbl_affine(p)
-    return p
-
-
-G1_2_64 = _g1_2_64()   # [2^64] g1, subtracted from the [r + 2^64] g1 chain
-
 SET_SLOTS = 92   # registers per set; packed set s uses slots [s * SET_SLOTS, (s + 1) * SET_SLOTS)
 
 
-def add_program_name(prefix: str, S: int, xb: int, rmask: int) -> str:
-    """Addition program for one bit: the |x| bit xb and the r bits of the packed sets
-    (bit s of rmask = set s).  S == 1 keeps the historical names."""
-    if S == 1:
-        return f"{prefix}_add_" + ("x" if xb else "") + ("r" if rmask else "")
-    return f"{prefix}_add_{xb}{rmask:0{S}b}"
-
-
-def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G1Y, S=1, prefix="pset"):
+def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, S=1, prefix="pset"):
     """The per-set programs for S sets packed in one wavefront (set s at register
-    offset s * SET_SLOTS; its zero-checks carry its set index).  One set per wavefront
-    (S = 1, k_pset) leaves the r chains to the block's second wavefront (RG, RP written
-    into the frame before pset_ml2 by single-lane GLV multiplications): its programs
-    carry only the |x| chains, and the r bits choose nothing."""
-    r_chains = S > 1
+    offset s * SET_SLOTS; its zero-checks carry its set index).  The programs carry the
+    |x| chains only: RG = [s] g1 and RP = [s] pk come from k_pre's GLV lanes, loaded into
+    the frame with the set's inputs."""
     progs = []
     offs = [SET_SLOTS * s for s in range(S)]
     regs = set(range(0, SET_SLOTS * S))
@@ -320,11 +285,6 @@ def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G
         sig = aff(f2, o + SIG)
         sigj = (sig[0], sig[1], f2.one())
         out_jac(f2, o + C, sigj)
-        if r_chains:
-            out_jac(f1, o + D3, (f1.c.const(G1X), f1.c.const(G1Y), f1.one()))
-            pk = jac(f1, o + PK)
-            for base in (D2, E2):
-                out_jac(f1, o + base, pk)
 
     per_set(c, prep)
     progs.append(schedule(c, FRAME, regs))
@@ -342,29 +302,17 @@ def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G
         per_set(c, body)
         progs.append(schedule(c, FRAME, regs))
 
-    if r_chains:
-        dbl_prog("dbl_r", (), (D2, E2, D3))
-    dbl_prog("dbl_all", (A, C), (D2, E2, D3) if r_chains else ())
+    dbl_prog("dbl_all", (A, C), ())
 
-    def add_prog(xb, rmask):
-        c, t, f1, f2 = new(add_program_name(prefix, S, xb, rmask)[len(prefix) + 1:])
+    # addition at a set bit of |x|
+    c, t, f1, f2 = new("add_x")
 
-        def body(o):
-            s = o // SET_SLOTS
-            if xb:
-                out_jac(f2, o + A, add_gen(f2, jac(f2, o + A), jac(f2, o + PP)))
-                out_jac(f2, o + C, add_mixed(f2, jac(f2, o + C), aff(f2, o + SIG)))
-            if (rmask >> s) & 1:
-                out_jac(f1, o + D3, add_mixed(f1, jac(f1, o + D3), (c.const(G1X), c.const(G1Y))))
-                out_jac(f1, o + D2, add_gen(f1, jac(f1, o + D2), jac(f1, o + PK)))
+    def add_x(o):
+        out_jac(f2, o + A, add_gen(f2, jac(f2, o + A), jac(f2, o + PP)))
+        out_jac(f2, o + C, add_mixed(f2, jac(f2, o + C), aff(f2, o + SIG)))
 
-        per_set(c, body)
-        progs.append(schedule(c, FRAME, regs))
-
-    for xb in (0, 1):
-        for rmask in range(1 << S if r_chains else 1):
-            if xb or rmask:
-                add_prog(xb, rmask)
+    per_set(c, add_x)
+    progs.append(schedule(c, FRAME, regs))
 
     # phase 2 (straight line): finish the cofactor clearing, the r multiples and the
     # subgroup comparison
@@ -388,9 +336,6 @@ def build_pset(consts, T, miller_dbl, miller_add, X_ABS, FRAME, PSI, ISO, G1X, G
         t3 = add_gen(f2, t3, neg_pt(f2, t1))               # - t1
         hh = add_gen(f2, t3, neg_pt(f2, P))                # - P
         out_jac(f2, o + H, hh)
-        if r_chains:  # RG = D3 - [2^64] g1 (a constant), RP = D2 - E2
-            out_jac(f1, o + RG, add_mixed(f1, jac(f1, o + D3), (c.const(G1_2_64[0]), c.const(P_MOD - G1_2_64[1]))))
-            out_jac(f1, o + RP, add_gen(f1, jac(f1, o + D2), neg_pt(f1, jac(f1, o + E2))))
         # subgroup: psi(sig) == -C (= [x] sig): (psi.x) Z^2 == X and (psi.y) Z^3 == -Y
         X, Y, Z = jac(f2, o + C)
         f2.zero(Z)                                         # [|x|] sig hit infinity: exact path
@@ -520,8 +465,10 @@ def miller_loop_multi(t, pairs, miller_dbl, miller_add, X_ABS):
 def run_pset(pg, consts, frame, rg, rp, simulate, inv):
     """The k_pset controller (lodestar_amd/csrc/kernels/k_pset.hip) over the
     simulator: returns the zero-check flag and the subgroup result.  rg, rp: [s] g1 and
-    [s] pk as G1 Jacobian triples (the kernel's second wavefront writes them into the
-    frame before pset_ml2); pg: name -> Program; inv: Fp inverse."""
+    [s] pk as G1 Jacobian triples (k_pre's GLV lanes; the kernel loads them into the
+    frame with the set's inputs); pg: name -> Program; inv: Fp inverse."""
+    frame[RG:RG + 3] = list(rg)
+    frame[RP:RP + 3] = list(rp)
     flag = simulate(pg["pset_prep"], frame, consts)
     for i in range(62, -1, -1):
         flag |= simulate(pg["pset_dbl_all"], frame, consts)
@@ -532,8 +479,6 @@ def run_pset(pg, consts, frame, rg, rp, simulate, inv):
     flag |= simulate(pg["pset_norm2"], frame, consts)
     frame[INV_OUT] = inv(frame[INV_IN])
     flag |= simulate(pg["pset_affine2"], frame, consts)
-    frame[RG:RG + 3] = list(rg)
-    frame[RP:RP + 3] = list(rp)
     flag |= simulate(pg["pset_ml2"], frame, consts)
     return flag, in_group
 
@@ -541,25 +486,21 @@ def run_pset(pg, consts, frame, rg, rp, simulate, inv):
 X_ABS_BITS = 0xD201000000010000
 
 
-def run_psetn(pg, consts, frame, rs, simulate, inv):
-    """The k_psetn<S> controller (S = len(rs) sets per wavefront) over the simulator:
+def run_psetn(pg, consts, frame, rpts, simulate, inv):
+    """The k_psetn<S> controller (S = len(rpts) sets per wavefront) over the simulator:
     returns the zero-check flag bits and the per-set subgroup results.  frame: S *
-    SET_SLOTS registers + temporaries; rs: the sets' scalars."""
-    S = len(rs)
+    SET_SLOTS registers + temporaries; rpts: per set ([s] g1, [s] pk) as G1 Jacobian
+    triples (k_pre's GLV lanes; the kernel loads them with the set's inputs)."""
+    S = len(rpts)
     pre = f"pset{S}"
-
-    def bits(i):
-        return sum(((r >> i) & 1) << s for s, r in enumerate(rs))
-
+    for s, (rg, rp) in enumerate(rpts):
+        frame[SET_SLOTS * s + RG:SET_SLOTS * s + RG + 3] = list(rg)
+        frame[SET_SLOTS * s + RP:SET_SLOTS * s + RP + 3] = list(rp)
     flag = simulate(pg[f"{pre}_prep"], frame, consts)
-    flag |= simulate(pg[f"{pre}_dbl_r"], frame, consts)
-    if bits(63):
-        flag |= simulate(pg[add_program_name(pre, S, 0, bits(63))], frame, consts)
     for i in range(62, -1, -1):
         flag |= simulate(pg[f"{pre}_dbl_all"], frame, consts)
-        xb, m = (X_ABS_BITS >> i) & 1, bits(i)
-        if xb or m:
-            flag |= simulate(pg[add_program_name(pre, S, xb, m)], frame, consts)
+        if (X_ABS_BITS >> i) & 1:
+            flag |= simulate(pg[f"{pre}_add_x"], frame, consts)
     flag |= simulate(pg[f"{pre}_phase2"], frame, consts)
     in_group = [all(frame[SET_SLOTS * s + DIFF + k] == 0 for k in range(4)) for s in range(S)]
     flag |= simulate(pg[f"{pre}_norm2"], frame, consts)
@@ -568,11 +509,6 @@ def run_psetn(pg, consts, frame, rs, simulate, inv):
     flag |= simulate(pg[f"{pre}_affine2"], frame, consts)
     flag |= simulate(pg[f"{pre}_ml2"], frame, consts)
     return flag, in_group
-
-
-def run_pset2(pg, consts, frame, rs, simulate, inv):
-    """The k_psetn<2> controller (two sets per wavefront)."""
-    return run_psetn(pg, consts, frame, rs, simulate, inv)
 
 
 # ----------------------------------------------------------------------------
