@@ -97,7 +97,7 @@ def pset_products_per_set(S: int) -> float:
 
 
 SIGAGG_MIN_SETS = 512   # bls_gpu.hip use_sigagg: the aggregated-signature path from this call size on
-PERSET_MAX_INFLIGHT = 12288  # ... while more sets than this are in flight, or the call has more than
+PERSET_MAX_INFLIGHT = 20480  # ... while more sets than this are in flight, or the call has more than
 PERSET_MAX_CALL = 2048       # ... this many sets
 
 

@@ -562,11 +562,11 @@ int bls_gpu_validate_pubkeys(bls_gpu_ctx* ctx, const uint8_t* pks, uint32_t n, u
 // Aggregated-signature path (k_chain + k_gsum + k_vset + k_mln single-pair Miller
 // loops, one signature Miller loop per chunk) from SIGAGG_MIN_SETS sets on, except for
 // calls of at most PERSET_MAX_CALL sets while the process has at most
-// $BLS_PERSET_MAX_INFLIGHT (12,288) sets in flight (this call's included): those run the
+// $BLS_PERSET_MAX_INFLIGHT (20,480) sets in flight (this call's included): those run the
 // all-cooperative k_pset / k_psetn (a set's chains spread over a wavefront instead of one
 // lane: shorter calls while the device has room, fewer sets per second once it is full --
-// 4 x 1024-set calls in flight 9.7 vs 16.8 ms per call, 12 x 1024 18.7 vs 20.9 ms, 16 x 1024
-// 23.9 vs 21.6 ms, profiles/r04_ab_perset_low_load.json).  A call of more sets would fill
+// per-set vs aggregated at 12 x 1024-set calls in flight 0.82M vs 0.56M sets/s, 16 x 1024
+// 0.82M vs 0.72M, 24 x 1024 1.02M vs 1.03M, profiles/r04_ab_perset_crossover.json).  A call of more sets would fill
 // every SIMD with its wavefronts (2 sets each, two per SIMD) and hold the main-thread
 // lane's context behind it (test_napi.py: a 4096-set pool call finished first).
 // BLS_DEBUG_SIGAGG_ON / _OFF or $BLS_SIGAGG (0 / 1) force a path.
@@ -579,7 +579,7 @@ static bool use_sigagg(const bls_gpu_ctx* ctx, uint32_t n) {
   }();
   static const uint64_t perset_max = [] {
     const char* e = getenv("BLS_PERSET_MAX_INFLIGHT");
-    return e ? (uint64_t)strtoull(e, nullptr, 10) : 12288ull;
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 20480ull;
   }();
   if (ctx->debug_flags & BLS_DEBUG_SIGAGG_ON) return true;
   if (ctx->debug_flags & BLS_DEBUG_SIGAGG_OFF) return false;
