@@ -312,15 +312,26 @@ __device__ __forceinline__ void coop_wave_sync() {
 }
 
 // One step for this lane: gather, product, then (after the wave's gathers) write.
+// TIMED (the probe, bls_gpu_coop_probe): lane 0 stamps s_memtime at the point `mark`
+// names -- 0: compute done (before the fence), 1: op decoded, 2: operand a summed,
+// 3: operand b summed (product steps), 4: product done.
 template <bool TIMED>
-__device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, uint32_t* flag, uint64_t* stamp) {
+__device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, uint32_t* flag, uint64_t* stamp,
+                                          uint32_t mark = 0) {
   const CoopOpView op = coop_decode(raw);
+  if (TIMED && mark == 1 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   Fp r = fp_zero();
   if (op.kind != 0) {
     r = coop_lin(op.a, op.ca, op.na, slots);
-    if (op.kind == 1) r = fp_mul_lazy(r, coop_lin(op.b, op.cb, op.nb, slots));
+    if (TIMED && mark == 2 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+    if (op.kind == 1) {
+      const Fp rb = coop_lin(op.b, op.cb, op.nb, slots);
+      if (TIMED && mark == 3 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+      r = fp_mul_lazy(r, rb);
+      if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+    }
   }
-  if (TIMED && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+  if (TIMED && mark == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   coop_wave_sync();
   if (op.kind != 0) {
     if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
@@ -344,17 +355,18 @@ __device__ __forceinline__ void coop_run_body(const CoopEnv& env, CoopProg pg, F
   if (pg.n == 0) return;
   LdsU4* slots = (LdsU4*)frame;
   CoopOpRaw A, B;
+  const uint32_t mark = TIMED && stamps ? (uint32_t)stamps[0] : 0u;  // the probe's stamp point
   const uint32_t last = pg.first + pg.n - 1;
   coop_fetch(A, base, pg.first, lane);
   for (uint32_t s = 0; s < pg.n; s += 2) {
     const uint32_t g = pg.first + s;
     if (TIMED && lane == 0) stamps[2 * s] = __builtin_amdgcn_s_memtime();
     coop_fetch(B, base, g + 1 <= last ? g + 1 : last, lane);
-    coop_step<TIMED>(A, slots, flag, stamps ? stamps + 2 * s + 1 : nullptr);
+    coop_step<TIMED>(A, slots, flag, stamps ? stamps + 2 * s + 1 : nullptr, mark);
     if (s + 1 >= pg.n) break;
     if (TIMED && lane == 0) stamps[2 * s + 2] = __builtin_amdgcn_s_memtime();
     coop_fetch(A, base, g + 2 <= last ? g + 2 : last, lane);
-    coop_step<TIMED>(B, slots, flag, stamps ? stamps + 2 * s + 3 : nullptr);
+    coop_step<TIMED>(B, slots, flag, stamps ? stamps + 2 * s + 3 : nullptr, mark);
   }
   if (TIMED && lane == 0) stamps[2 * pg.n] = __builtin_amdgcn_s_memtime();
 }

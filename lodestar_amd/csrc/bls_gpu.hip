@@ -2014,6 +2014,13 @@ extern "C" int bls_gpu_coop_probe(bls_gpu_ctx* ctx, const char* name, uint32_t b
   *us_per_step = ms * 1e3 / ((double)reps * pg.n);
   if (ms_total) *ms_total = ms;
   if (step_stamps) {  // one more run of block 0 with s_memtime stamps: step start, compute done
+    // (or the point $BLS_COOP_PROBE_MARK names, coop.hpp coop_step; steps that do not
+    // reach it keep 0)
+    const char* me = getenv("BLS_COOP_PROBE_MARK");
+    const uint64_t mark = me ? strtoull(me, nullptr, 10) : 0ull;
+    HIPC(ctx, hipMemsetAsync(d_stamps, 0, 8ull * (2 * pg.n + 1), s));
+    HIPC(ctx, hipMemcpyAsync(d_stamps, &mark, 8, hipMemcpyHostToDevice, s));
+    HIPC(ctx, hipStreamSynchronize(s));
     HIPC(ctx, launch_k_coop_probe(ctx->coop, pg, 1, 0, (uint32_t*)ctx->dev_ws, d_stamps, s));
     HIPC(ctx, hipMemcpyAsync(step_stamps, d_stamps, 8ull * (2 * pg.n + 1), hipMemcpyDeviceToHost, s));
     HIPC(ctx, hipStreamSynchronize(s));

@@ -7,6 +7,7 @@ wave sync.  Program names as in lodestar_amd/_native/coop_programs.json.
     python tools/coop_probe.py [name:reps ...]
 """
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -35,4 +36,22 @@ with GpuContext(0) as g:
         out[f"{name}:stamps"] = {"steps": n_steps, "mul_steps": progs[name]["mul_steps"],
                                  "total_ticks_mean": float(total.mean()), "compute_ticks_mean": float(compute.mean()),
                                  "total_ticks_p10_p50_p90": [float(np.percentile(total, q)) for q in (10, 50, 90)]}
+        # where a product step's time goes: ticks from step start to each stamp point
+        # (coop.hpp coop_step, $BLS_COOP_PROBE_MARK), over the steps that reach point 3
+        # (product steps, lane 0 a product)
+        parts = {}
+        for mark in (1, 2, 3, 4, 0):
+            os.environ["BLS_COOP_PROBE_MARK"] = str(mark)
+            _, _, sm = g.coop_probe(name, 1, 1, 2 * n_steps + 1)
+            parts[mark] = sm.astype(np.int64)
+        os.environ.pop("BLS_COOP_PROBE_MARK", None)
+        mul = parts[3][1::2] != 0
+        if mul.any():
+            pts = {}
+            for mark, label in ((1, "decoded"), (2, "operand_a"), (3, "operand_b"), (4, "product"), (0, "compute_done")):
+                sm = parts[mark]
+                d = (sm[1::2] - sm[0:-1:2])[mul]
+                pts[label] = float(np.median(d))
+            pts["step_total"] = float(np.median(np.diff(parts[0][0::2])[mul]))
+            out[f"{name}:product_step_ticks_median"] = {"steps": int(mul.sum()), **pts}
     print(json.dumps(out, indent=1))
