@@ -64,7 +64,9 @@ sys.path.insert(0, str(ROOT))
 # One HIP stream per in-flight batch; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
 # queues (default 4 on this image), and streams sharing a queue serialise.  Give the
 # in-flight contexts their own queues (set before the HIP runtime initialises).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+# (--hwq-child: the deployable-configuration sub-record runs under the queue count its
+# parent gave it, HIP's default 4 included)
+if "--hwq-child" not in sys.argv and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
     os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -213,6 +215,33 @@ def latency_curve(ctxs, works, points, sets_per_call: int, steps: int = 5) -> di
 
 
 PMC_FILE = "r04_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
+# the committed rocprofv3 --kernel-trace --stats summary of the timed 12 x 22 shape (the
+# dominant kernels' average launch time with ~12 passes sharing the device)
+KSTATS_FILE = "r04_kernel_stats_timed_12x22_final.csv"
+KSTATS_SETS = 22528                      # sets per pass of that run (22 calls x 1024)
+PEAK_FILE = "peak_fixed.json"            # the fixed v_mad_u64_u32 peak (median of the committed measurements)
+
+
+def peak_fixed() -> float | None:
+    p = ROOT / "profiles" / PEAK_FILE
+    return json.loads(p.read_text())["peak_fixed_tmad_s"] if p.exists() else None
+
+
+def committed_kernel_times(names=("k_mlf", "k_mlq", "k_chain", "k_pre")) -> dict:
+    """Average launch ns per kernel (by plain name prefix) from the committed timed-shape
+    kernel trace (profiles/KSTATS_FILE)."""
+    import csv
+
+    p = ROOT / "profiles" / KSTATS_FILE
+    out = {}
+    if not p.exists():
+        return out
+    for r in csv.DictReader(open(p)):
+        n = r["Name"].replace("void ", "").split("(")[0]
+        for k in names:
+            if n.split("<")[0] == k:
+                out[n] = float(r["AverageNs"])
+    return out
 VERIFY_KERNELS = ("k_pk", "k_pre", "k_chain", "k_gsum", "k_vset", "k_mlq", "k_mlf", "k_msm", "k_status", "k_fprod",
                   "k_chunk_coop", "k_indiv_coop", "k_fold", "k_exact", "k_uset", "k_gsum1", "k_mln")
 
@@ -439,9 +468,24 @@ def run_calls(ctxs, packed, calls_per_pass: int):
     return time.perf_counter() - t0, out, tot
 
 
+def steady_state(ctxs, w, pbs, calls_per_pass: int, jobs: int) -> dict:
+    """The slice's job `jobs` times back to back in ONE timed region (every context keeps
+    taking its next calls, no barrier between jobs), verdicts checked for every call:
+    the steady-state rate beside the one-job figure (`sets_per_s`, which is close to one
+    pass's latency when a job is a pass or two per context)."""
+    from lodestar_amd import workloads as W
+
+    el, out, _ = run_calls(ctxs, pbs * jobs, calls_per_pass)
+    bad = [k for k in range(len(out)) if not W.verdicts_ok(w, k % len(pbs), out[k])]
+    assert not bad, f"steady state: {len(bad)} calls with wrong verdicts (first {bad[0]})"
+    return {"steady_jobs": jobs, "steady_elapsed_s": round(el, 4),
+            "steady_sets_per_s": round(jobs * w.n_sets / el, 1),
+            "steady_passes_per_context": round(len(out) / len(ctxs) / calls_per_pass, 1)}
+
+
 def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, reps: int = 3,
                 latency_runs: int = 10, cfg4_ctx: int = 4, cfg4_cpp: int = 32, cfg5_sets: int = 131_072,
-                cfg5_roots: int = 256) -> dict:
+                cfg5_roots: int = 256, jobs: int = 5) -> dict:
     """BASELINE configs 3 and 4 at N = 1: cfg3, one block-import call
     (latency, sets/s, pubkeys aggregated/s); cfg4 this GPU's slice of the 1M-set range-sync
     job (1/8: shard by call), once with range sync's own non-batchable 128-set calls and
@@ -496,7 +540,8 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
                         "runs": reps,
                         "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
                         "passes_merged_check_failed": tot["merged_fail"],
-                        "verdicts": "every call matches the sets' validity by construction"}
+                        "verdicts": "every call matches the sets' validity by construction",
+                        **steady_state(c4, w4, pbs, cpp4, jobs)}
         # cfg5: this GPU's slice of the mainnet epoch (1/8 of ~1M attestations over 2048
         # committee roots), calls of 1024 batchable single-set requests on the headline's
         # contexts, invalid sets included (their passes fail the merged check and run the
@@ -518,7 +563,8 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
                              "contexts": n_ctx, "calls_per_pass": cpp5, "runs": reps,
                              "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
                              "passes_merged_check_failed": tot["merged_fail"],
-                             "verdicts": "every call matches the sets' validity by construction"}
+                             "verdicts": "every call matches the sets' validity by construction",
+                             **steady_state(ctxs, w5, pbs, cpp5, jobs)}
     finally:
         for c in ctxs:
             c.close()
@@ -639,7 +685,10 @@ def bench_job(args, ctxs, rank: int, world: int, dist, device, make_backend) -> 
             "dtype": "u32 (381-bit Fp, 12x32-bit Montgomery limbs)",
             "data": "synthetic: interop keys, sha256 messages, GPU-made signatures, invalid sets by construction",
             "config": {"workload": workload, "parallelism": par, "table_keys": args.table_keys,
-                       "contexts_per_gpu": len(ctxs)},
+                       "contexts_per_gpu": len(ctxs),
+                       "runtime": {"hip_runtime": _mapped_hip(),
+                                   "process_group": ({"backend": dist.get_backend(), "world": dist.get_world_size()}
+                                                     if dist is not None and dist.is_initialized() else None)}},
             "job": {k: v for k, v in res.items() if k != "elapsed_s"}}
 
 
@@ -678,6 +727,12 @@ def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int, per_call: 
     if out.returncode != 0:
         raise SystemExit(f"benchNapi.js failed: {out.stderr[-2000:]}")
     return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def _mapped_hip() -> list[str]:
+    from lodestar_amd.native import mapped_hip_runtime
+
+    return mapped_hip_runtime()
 
 
 def _free_port() -> int:
@@ -800,8 +855,13 @@ def main() -> None:
     # 8 x 64 1.49M, 12 x 64 1.38M non-batchable sets/s -- 12 x 64 leaves contexts short of a second pass)
     ap.add_argument("--cfg4-contexts", type=int, default=8, help="contexts of the cfg4 sub-record")
     ap.add_argument("--cfg4-calls-per-pass", type=int, default=64, help="128-set calls per pass of the cfg4 sub-record")
+    ap.add_argument("--hw-queues", default="4,16",
+                    help="GPU_MAX_HW_QUEUES values of the deployable-configuration sub-records (empty: none)")
     ap.add_argument("--no-merged-check", action="store_true",
                     help="one final exponentiation per chunk only (BLS_DEBUG_NO_MERGED_CHECK)")
+    ap.add_argument("--hwq-child", action="store_true",
+                    help="internal: the deployable-configuration sub-record (hw_queues_N), started by the parent "
+                         "before it touches the GPU; waits for a line on stdin, then runs the cfg2 timed region")
     ap.add_argument("--stand-in", default=None, metavar="MODULE:FACTORY",
                     help="dry run of --mode cfg4 / cfg5 without a device: ranks on gloo, contexts from this CPU "
                          "stand-in (tests only)")
@@ -853,6 +913,62 @@ def main() -> None:
             dist.destroy_process_group()
         return
 
+    # The deployable configuration (hw_queues_4 / hw_queues_16): the same cfg2 shape in
+    # child processes whose HIP runtime gets GPU_MAX_HW_QUEUES = 4 (HIP's default, what a
+    # beacon node that sets nothing runs) and 16, started now -- before this process makes
+    # any GPU call -- and released one at a time after this process's own GPU work
+    hwq_children = {}
+    if args.hwq_child:
+        args.probe_only = True
+        if sys.stdin.readline().strip() != "go":  # the parent's go: its own GPU work is done
+            sys.exit(3)  # the parent ended without releasing this child: touch nothing
+    elif (world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records
+          and not args.probe_only and args.hw_queues):
+        for q in (int(x) for x in args.hw_queues.split(",")):
+            hwq_children[q] = subprocess.Popen(
+                [sys.executable, str(Path(__file__).resolve()), "--hwq-child", "--inflight", str(args.inflight),
+                 "--calls-per-pass", str(args.calls_per_pass), "--steps", str(max(3, args.steps // 3)), "--warmup", "1",
+                 "--sets", str(args.sets)],
+                env=dict(os.environ, GPU_MAX_HW_QUEUES=str(q)), stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                stderr=subprocess.PIPE, text=True)
+    try:
+        _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, hwq_children)
+    finally:
+        for p in hwq_children.values():
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+
+
+def run_hwq_children(children: dict) -> dict:
+    """Release each deployable-configuration child in turn (this process's GPU work is
+    over) and collect its line: sets/s and ms per call at its hardware-queue count."""
+    res = {}
+    for q, p in children.items():
+        try:
+            out, err = p.communicate("go\n", timeout=300)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+            res[f"hw_queues_{q}"] = {"error": "timed out"}
+            continue
+        lines = [ln for ln in out.splitlines() if ln.lstrip().startswith("{")]
+        if p.returncode != 0 or not lines:
+            res[f"hw_queues_{q}"] = {"error": f"exit {p.returncode}: {err[-400:]}"}
+            continue
+        d = json.loads(lines[-1])
+        res[f"hw_queues_{q}"] = {
+            "GPU_MAX_HW_QUEUES": q, "sets_per_s": d["value"], "ms_per_call": d["ms_per_step"],
+            "contexts": d["config"]["contexts_per_gpu"], "calls_per_pass": d["config"]["calls_per_pass"],
+            "steps": d["steps"],
+            "note": "the headline's cfg2 shape in a child process started before the parent's first GPU call, its "
+                    f"HIP runtime given GPU_MAX_HW_QUEUES={q}" + (" (HIP's default: what a beacon node that sets "
+                                                                  "nothing runs)" if q == 4 else "") +
+                    "; the headline line runs with 24 (one hardware queue per context)"}
+    return res
+
+
+def _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, hwq_children) -> None:
     from lodestar_amd._abi import DEBUG_NO_MERGED_CHECK, DEBUG_NO_MSG_DEDUP, DEBUG_NO_UNITS
     from lodestar_amd.native import GpuContext
     from lodestar_amd.shard import GpuPartialBackend, global_throughput
@@ -969,6 +1085,13 @@ def main() -> None:
                   "parallelism": "napi x1"}
         scaling = "weak"
 
+    from lodestar_amd.native import mapped_hip_runtime
+
+    # which HIP runtime the library runs under (torch's bundled copy once a rank has
+    # initialised torch.cuda / RCCL, /opt/rocm's otherwise) and the process group
+    config["runtime"] = {"hip_runtime": mapped_hip_runtime(),
+                         "process_group": ({"backend": dist.get_backend(), "world": dist.get_world_size()}
+                                           if dist is not None and dist.is_initialized() else None)}
     out = None
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
@@ -1055,11 +1178,36 @@ def main() -> None:
                 out["pass_shape"] = {"timed": extra_shape, "solo": solo_shape,
                                      "note": "bls_stats.pass_shape -> passes: bit 0 Pippenger signature sum, "
                                              "bits 8-15 items per k_mlf lane (both chosen by the sets in flight)"}
+            pf = peak_fixed()
+            if agg:
+                # the dominant kernel in the timed shape (k_mlf, one lane per 1 / 2 / 4 items), from the
+                # committed trace of that shape: algorithmic MADs per launch / its average launch time
+                times = committed_kernel_times()
+                for name, ns in times.items():
+                    base = name.split("<")[0]
+                    fpm = {"k_mlf": mlf_products(wm, 0x401), "k_mlq": wm["ml_lines"],
+                           "k_chain": wm["chain_h"] + wm["chain_subgroup"] + wm["chain_r_pk"],
+                           "k_pre": wm["k_pre"]}[base]
+                    mads = KSTATS_SETS * fpm * MADS_PER_FPM
+                    kern.setdefault(name, {}).update({
+                        "mad_per_launch_timed_shape": round(mads), "fp_products_per_set": round(fpm, 1),
+                        "launch_ms_timed_committed": round(ns / 1e6, 3),
+                        "achieved_timed": round(mads / (ns * 1e-9) / 1e12, 4),
+                        "frac_timed": round(mads / (ns * 1e-9) / 1e12 / pf, 4) if pf else None,
+                        "source": f"profiles/{KSTATS_FILE} (copied: rocprofv3 kernel trace of the timed 12 x 22 "
+                                  f"shape, {KSTATS_SETS} sets per launch, four items per k_mlf lane; frac against "
+                                  "peak_fixed)"})
+            for v in kern.values():
+                if pf and v.get("achieved_solo") is not None:
+                    v["frac_solo_fixed"] = round(v["achieved_solo"] / pf, 4)
             roof = {"bound": "valu",
                     "kernel": ("every kernel of the pass; dominant: k_chain (per-set scalar chains) and the split "
                                "SIMT Miller loops (k_mlq + k_mlf)") if agg else "k_pset",
                     "achieved": round(achieved, 4),
                     "peak": round(peak, 3), "unit": "TMAD/s (v_mad_u64_u32)", "frac": round(achieved / peak, 5),
+                    "peak_fixed": pf, "frac_fixed": round(achieved / pf, 5) if pf else None,
+                    "peak_fixed_note": f"profiles/{PEAK_FILE}: median of every committed bls_gpu_mad_peak measurement; "
+                                       "`frac_fixed` compares across boxes, `frac` uses this box's own measured peak",
                     "traffic": None,
                     "work": f"{fpm_set:.0f} Fp products/set ({fpm_note}) x {MADS_PER_FPM} MAD x "
                             f"{per_gpu:.0f} sets/s per GPU over the timed region",
@@ -1077,6 +1225,7 @@ def main() -> None:
                 "fp_products_per_set": round(w_ref), "work": w_ref_note,
                 "achieved": round(per_gpu * w_ref * MADS_PER_FPM / 1e12, 4),
                 "frac": round(per_gpu * w_ref * MADS_PER_FPM / 1e12 / peak, 5),
+                "frac_fixed": round(per_gpu * w_ref * MADS_PER_FPM / 1e12 / pf, 5) if pf else None,
                 "note": "SURVEY 8d: the reference algorithm's Fp products per set (blst-style, no dedup / units / "
                         "merged check) at this line's rate -- the work the reference would do for the same sets; "
                         "`frac` above prices the products this build executes"}
@@ -1101,6 +1250,8 @@ def main() -> None:
         out.update(sub_records(args.table_keys, inflight, K, args.cfg4_sets, cfg4_ctx=args.cfg4_contexts,
                                cfg4_cpp=args.cfg4_calls_per_pass, cfg5_sets=args.cfg5_sets,
                                cfg5_roots=args.cfg5_roots))
+    if hwq_children:
+        out.update(run_hwq_children(hwq_children))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -92,13 +92,25 @@ def _check_scratch(src: Path, kernels: list[dict]) -> None:
                              "runtime's ~8 GiB (lodestar_amd/build.py ADMISSION_BUDGET)")
 
 
+# Input-fixture and measurement kernels (signing / key derivation for synthetic inputs,
+# the MAD-peak, self-test and latency probes): never launched by a verify call, so they do
+# not set the per-queue figure a verifier context is admitted against
+FIXTURE_TUS = ("k_sign", "k_probe", "k_peak", "k_selftest")
+FIXTURE_KERNELS = ("k_coop_probe",)
+
+
+def _plain_name(mangled: str) -> str:
+    m = re.match(r"_Z(\d+)", mangled)  # the kernel's plain name from its mangled one
+    return mangled[m.end(): m.end() + int(m.group(1))] if m else mangled
+
+
 def scratch_per_queue(table: list[dict]) -> tuple[int, str]:
-    """The deepest kernel's per-queue reservation (bytes) and its name: what a context's
-    queue may have to hold (any kernel of the library can run on a context's stream)."""
-    worst = max(table, key=lambda k: k["device_scratch_bytes"])
-    m = re.match(r"_Z(\d+)", worst["name"])  # the kernel's plain name from its mangled one
-    name = worst["name"][m.end(): m.end() + int(m.group(1))] if m else worst["name"]
-    return worst["device_scratch_bytes"], name
+    """The deepest verify-path kernel's per-queue reservation (bytes) and its name: what a
+    context's queue may have to hold (any verify-path kernel can run on a context's
+    stream; the fixture and probe kernels, FIXTURE_TUS / FIXTURE_KERNELS, are left out)."""
+    path = [k for k in table if k.get("tu") not in FIXTURE_TUS and _plain_name(k["name"]) not in FIXTURE_KERNELS]
+    worst = max(path, key=lambda k: k["device_scratch_bytes"])
+    return worst["device_scratch_bytes"], _plain_name(worst["name"])
 
 
 def _compile(src: Path, hdr: str, verbose: bool, extra: list[str] | None = None) -> Path:

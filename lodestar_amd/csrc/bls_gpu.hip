@@ -1114,7 +1114,15 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // group tests over failed chunks (passes reuse the buffers): pass A <= 1 + 13 tests per
   // chunk (chunks of < 8192 requests) of <= 8 m members in all, pass B 2 tests, pass C one
   // test per request
-  const size_t grp_cap = (size_t)R + 14ull * n_chunks + 2, grp_mem_cap = 8ull * R + 16;
+  // (carved only when some chunk is large enough to be group-tested, group_test_min)
+  bool gt_possible = false;
+  {
+    const uint32_t gmin = group_test_min(ctx);
+    for (uint32_t ch = 0; ch < n_chunks && !gt_possible; ++ch)
+      gt_possible = plan.chunk_off[ch + 1] - plan.chunk_off[ch] >= gmin;
+  }
+  const size_t grp_cap = gt_possible ? (size_t)R + 14ull * n_chunks + 2 : 0,
+               grp_mem_cap = gt_possible ? 8ull * R + 16 : 0;
   GroupBufs gbufs;
   memset(&gbufs, 0, sizeof(gbufs));
   auto carve = [&](Carver& c, PipeBufs& b, size_t& input_end) {
@@ -1132,7 +1140,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.sigs = c.take<uint8_t>(96ull * n);
     b.sig_lens = in->signature_lens ? c.take<uint32_t>(n) : nullptr;
     b.indiv_reqs = c.take<uint32_t>(R);
-    gbufs.off = c.take<uint32_t>(grp_cap + 1);
+    gbufs.off = c.take<uint32_t>(gt_possible ? grp_cap + 1 : 0);
     gbufs.members = c.take<uint32_t>(grp_mem_cap);
     own_sets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
     b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
@@ -1178,7 +1186,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       msm.win = c.take<G2J>(4);
     }
     b.req_status = c.take<int32_t>(R);
-    gbufs.f = c.take<Fp12>(R);
+    gbufs.f = gt_possible ? c.take<Fp12>(R) : nullptr;
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
       ptree[1] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
@@ -1307,6 +1315,9 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
         b.gsets = gsets_dev;
       }
       HIPC(ctx, hipEventRecord(ctx->ev[4], s));
+      // the f-side shape is chosen once per call (other contexts change the sets in flight
+      // meanwhile): every Miller-loop launch of the call and stats->pass_shape use it
+      if (!b.mlf_pl && k_mln_list_ok(b)) b.mlf_pl = mlf_per_lane();
       HIPC(ctx, launch_k_mln(b, ctx->coop, 0, indiv_vbase, s)); dbg_sync(s, "k_mln");
     } else {
       HIPC(ctx, launch_k_pset(b, ctx->coop, s)); dbg_sync(s, "k_pset");
@@ -1389,7 +1400,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   if (stats) {
     stats->merged_check = merged ? (merged_pass ? 1 : 2) : 0;
     stats->pass_shape =
-        sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? (b.mlf_pl ? b.mlf_pl : mlf_per_lane()) << 8 : 0u)) : 0u;
+        sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? b.mlf_pl << 8 : 0u)) : 0u;
   }
   if (stats) {
     stats->n_flagged = flagged;

@@ -44,9 +44,10 @@ struct MsmBufs {
 #define MSM_BUCKETS 1020u
 size_t msm_seg_cap(uint32_t n_sets);
 #define MSM_STATE_WORDS (MSM_BUCKETS + 2u)
+// k_msm_bin: 22-bit bucket slots, <= 2 entries per set and bucket
 #define MSM_MAX_SETS (1u << 21)
 // mlf_per_lane(): one item per TWO f lanes (kernels/k_mlq.hip k_mlf2)
-#define MLF_PAIR 3u  // k_msm_bin: 22-bit bucket slots, <= 2 entries per set and bucket
+#define MLF_PAIR 3u
 // the merged signature sum into the chunk groups' virtual sets vbase .. vbase + groups
 hipError_t launch_k_msm(const bls::PipeBufs& b, const MsmBufs& m, uint32_t groups, uint32_t vbase, hipStream_t s);
 hipError_t launch_k_gsum(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const bls::G2J* in,

@@ -36,6 +36,17 @@ class AdmissionError(NativeError):
     the process's contexts would pass the budget (include/lodestar_bls.h bls_admission)."""
 
 
+def mapped_hip_runtime() -> list[str]:
+    """Paths of the HIP runtime (libamdhip64) mapped into this process: /opt/rocm's when
+    the library is loaded first, torch's bundled copy (same soname) when torch was
+    imported before it -- the runtime the library's kernels then run under."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
+    except OSError:
+        return []
+
+
 def scratch_plan(n_normal: int, n_high: int, hw_queues: int = 0) -> tuple[bool, dict]:
     """The library's admission accounting for n_normal + n_high contexts (no device
     needed): (admissible, the bls_admission figures)."""

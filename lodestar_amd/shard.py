@@ -22,9 +22,15 @@ def shard_by_request(weights: list[int], world: int) -> list[list[int]]:
     return out
 
 
+def _grouped(dist) -> bool:
+    """A process group exists: the exchange goes through it whatever its size (a
+    world-1 group on the GPU box still runs the RCCL collectives, tests/test_gpu_rccl.py)."""
+    return dist is not None and dist.is_initialized()
+
+
 def global_throughput(local_sets: int, local_elapsed_s: float, dist=None, device=None) -> tuple[float, float]:
     """(sets/s over all ranks, max elapsed): all ranks' sets / the slowest rank's time."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _grouped(dist):
         return local_sets / local_elapsed_s, local_elapsed_s
     import torch
 
@@ -102,8 +108,9 @@ def verify_call_sharded(sets, seed: bytes, backend, dist=None, device=None, loca
     exponentiation (only computed when the call fails and `localize`)."""
     import numpy as np
 
-    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
-    rank = dist.get_rank() if world > 1 else 0
+    grouped = _grouped(dist)
+    world = dist.get_world_size() if grouped else 1
+    rank = dist.get_rank() if grouped else 0
     n = len(sets)
     if n < 2:
         raise ValueError("a sharded call needs >= 2 sets (1-set calls take the non-batched path)")
@@ -118,7 +125,7 @@ def verify_call_sharded(sets, seed: bytes, backend, dist=None, device=None, loca
         if part is not None:
             rec[12:] = np.frombuffer(part, dtype=np.uint8)
     rec[:12] = head.view(np.uint8)
-    recs = _all_gather_bytes(rec, dist, device) if world > 1 else [rec]
+    recs = _all_gather_bytes(rec, dist, device) if grouped else [rec]
     heads = [np.frombuffer(r[:12].tobytes(), dtype=np.int32) for r in recs]
     code = first_error([(int(h[0]), int(h[1]), int(h[2])) for h in heads])
     if code < 0:
@@ -126,14 +133,14 @@ def verify_call_sharded(sets, seed: bytes, backend, dist=None, device=None, loca
     partials = [r[12:].tobytes() for r, h in zip(recs, heads) if int(h[0]) == 0]
     # one final exponentiation for the whole call (rank 0), verdict broadcast
     ok = backend.final_check(partials) if rank == 0 else False
-    if world > 1:
+    if grouped:
         ok = bool(_broadcast_int(int(ok), dist, device))
     info = {"bad_shards": []}
     if not ok and localize:
         mine = 1
         if int(heads[rank][0]) == 0:
             mine = int(backend.final_check([recs[rank][12:].tobytes()]))
-        flags = _all_gather_bytes(np.array([mine], dtype=np.uint8), dist, device) if world > 1 else [[mine]]
+        flags = _all_gather_bytes(np.array([mine], dtype=np.uint8), dist, device) if grouped else [[mine]]
         info["bad_shards"] = [k for k, f in enumerate(flags) if int(f[0]) == 0]
     return ok, info
 

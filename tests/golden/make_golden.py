@@ -13,8 +13,12 @@ Reference data copied as fixture values (data, not source):
            (config/src/chainConfig/presets/minimal.ts:23); the signing root is derived below.
   * KAT-2  100 interop pubkeys (packages/state-transition/test-cache/interop-pubkeys.json).
   * KAT-3  real mainnet G2 points (packages/beacon-node/test/unit/sync/backfill/blocks.json,
-           randao_reveal + signature) and the "valid signature of random data"
-           (beacon-node/test/unit/chain/opPools/aggregatedAttestationPool.test.ts:22-24).
+           randao_reveal + signature), the "valid signature of random data"
+           (beacon-node/test/unit/chain/opPools/aggregatedAttestationPool.test.ts:22-24) and the
+           two selection proofs of state-transition/test/unit/util/aggregator.test.ts:28,37.
+           The "bruteforced" invalid signature of aggregator.test.ts:70 goes to
+           kat3_unpinned with the oracle's decode code: the reference test only hashes it, so
+           its decode outcome is parity unpinned.
 """
 from __future__ import annotations
 
@@ -73,8 +77,24 @@ def main() -> None:
         g2.append(b["signature"][2:])
     g2.append("b2afb700f6c561ce5e1b4fedaec9d7c06b822d38c720cf588adfda748860a940adf51634b6788f298c552de40183b5a2"
               "03b2bbe8b7dd147f0bb5bc97080a12efbb631c8888cb31a99cc4706eb3711865b8ea818c10126e4d818b542e9dbf9ae8")
+    # aggregator.test.ts:28,37: selection proofs (valid G2 points)
+    agg_src = (REF / "state-transition/test/unit/util/aggregator.test.ts").read_text()
+    agg_hex = [h for h in (ln.strip().strip('"') for ln in agg_src.splitlines()) if h.startswith("0x") and len(h) == 194]
+    assert len(agg_hex) == 4, "aggregator.test.ts: four 96-byte hex literals expected"
+    g2 += [agg_hex[0][2:], agg_hex[1][2:]]
     out["kat3_g2_points"] = [{"compressed": h, "uncompressed": g2_uncompressed(O.signature_from_bytes(bytes.fromhex(h)))}
                              for h in g2]
+    # aggregator.test.ts:70 (":68 NOTE: Invalid sig, bruteforced last characters"): the oracle's
+    # decode code, parity unpinned (the reference never decodes it)
+    unp = []
+    for h in (agg_hex[3][2:],):
+        try:
+            O.signature_from_bytes(bytes.fromhex(h), validate=True)
+            code = 0
+        except O.BlsError as e:
+            code = e.code
+        unp.append({"compressed": h, "code": code, "source": "aggregator.test.ts:70", "parity": "unpinned"})
+    out["kat3_unpinned"] = unp
 
     # ---- oracle-derived vectors (pinned by KAT-1/2/3 above)
     sks = [O.interop_secret_key(i) for i in range(8)]

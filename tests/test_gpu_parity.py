@@ -419,7 +419,7 @@ def test_sharded_partials_final_check(gpu, oracle, table):
     assert p is None and st == -CODE_BAD_ENCODING and err == (1, 4 - beg)
 
 
-def _sharded_gpu_rank(rank, world, port, sets, q):
+def _sharded_gpu_rank(rank, world, port, sets, q, flags=0):
     import os
 
     import torch.distributed as dist
@@ -431,6 +431,7 @@ def _sharded_gpu_rank(rank, world, port, sets, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = []
     with GpuContext(0) as gpu:
+        gpu.set_debug_flags(flags)  # the parent's per-set path (the module's verify_path)
         be = GpuPartialBackend(gpu)
         for ss in sets:
             out.append(verify_call_sharded(ss, bytes(32), be, dist))
@@ -457,7 +458,8 @@ def test_sharded_call_two_ranks(gpu, oracle):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad, two_inf, order], q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad, two_inf, order], q,
+                                                        gpu.base_debug_flags)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=100) for _ in procs)
@@ -473,8 +475,12 @@ def test_sharded_call_two_ranks(gpu, oracle):
 
 def test_sharded_call_two_ranks_large(gpu, oracle):
     """The sharded call at the per-GPU scale of a pass: 2,048 sets over two processes
-    (1,024 per rank, the aggregated path on each), all valid, then one set signing another
-    message in rank 1's shard: the call fails and only shard 1 is reported bad."""
+    (1,024 per rank), all valid, then one set signing another message in rank 1's shard:
+    the call fails and only shard 1 is reported bad.  Each rank's partial runs on the
+    module's path (the verify_path fixture's debug flag is handed to the children: a
+    1,024-set shard would otherwise take the per-set path whenever few sets are in
+    flight, bls_gpu.hip use_sigagg), so the aggregated sharded path is covered at pass
+    scale too."""
     import socket
 
     import torch.multiprocessing as mp
@@ -492,7 +498,8 @@ def test_sharded_call_two_ranks_large(gpu, oracle):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad], q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_gpu_rank, args=(r, 2, port, [good, bad], q, gpu.base_debug_flags))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=110) for _ in procs)
@@ -765,6 +772,10 @@ def test_kat3_mainnet_points_gpu_decode(gpu, golden, oracle, table):
     out, codes = gpu.g2_decompress(comp, validate=True)
     assert list(codes) == [0] * len(pts)
     assert [o.tobytes().hex() for o in out] == [p["uncompressed"] for p in pts]
+    # aggregator.test.ts:70's bruteforced signature: the oracle's code (parity unpinned)
+    unp = golden["kat3_unpinned"]
+    _, codes = gpu.g2_decompress(b"".join(bytes.fromhex(u["compressed"]) for u in unp), validate=True)
+    assert list(codes) == [u["code"] for u in unp]
     # the oracle-derived negatives through the same entry point
     cases = golden["sig_decode"]
     _, codes = gpu.g2_decompress(b"".join(bytes.fromhex(c["bytes"]) for c in cases), validate=True)
