@@ -855,8 +855,9 @@ def main() -> None:
     # 8 x 64 1.49M, 12 x 64 1.38M non-batchable sets/s -- 12 x 64 leaves contexts short of a second pass)
     ap.add_argument("--cfg4-contexts", type=int, default=8, help="contexts of the cfg4 sub-record")
     ap.add_argument("--cfg4-calls-per-pass", type=int, default=64, help="128-set calls per pass of the cfg4 sub-record")
-    ap.add_argument("--hw-queues", default="4,16",
-                    help="GPU_MAX_HW_QUEUES values of the deployable-configuration sub-records (empty: none)")
+    ap.add_argument("--hw-queues", default="unset,4,16",
+                    help="GPU_MAX_HW_QUEUES values of the deployable-configuration sub-records ('unset': the "
+                         "variable removed; empty: none)")
     ap.add_argument("--no-merged-check", action="store_true",
                     help="one final exponentiation per chunk only (BLS_DEBUG_NO_MERGED_CHECK)")
     ap.add_argument("--hwq-child", action="store_true",
@@ -924,13 +925,15 @@ def main() -> None:
             sys.exit(3)  # the parent ended without releasing this child: touch nothing
     elif (world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records
           and not args.probe_only and args.hw_queues):
-        for q in (int(x) for x in args.hw_queues.split(",")):
+        for q in args.hw_queues.split(","):
+            env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+            if q != "unset":
+                env["GPU_MAX_HW_QUEUES"] = str(int(q))
             hwq_children[q] = subprocess.Popen(
                 [sys.executable, str(Path(__file__).resolve()), "--hwq-child", "--inflight", str(args.inflight),
                  "--calls-per-pass", str(args.calls_per_pass), "--steps", str(max(3, args.steps // 3)), "--warmup", "1",
                  "--sets", str(args.sets)],
-                env=dict(os.environ, GPU_MAX_HW_QUEUES=str(q)), stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                stderr=subprocess.PIPE, text=True)
+                env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
         _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, hwq_children)
     finally:
@@ -961,10 +964,11 @@ def run_hwq_children(children: dict) -> dict:
             "GPU_MAX_HW_QUEUES": q, "sets_per_s": d["value"], "ms_per_call": d["ms_per_step"],
             "contexts": d["config"]["contexts_per_gpu"], "calls_per_pass": d["config"]["calls_per_pass"],
             "steps": d["steps"],
-            "note": "the headline's cfg2 shape in a child process started before the parent's first GPU call, its "
-                    f"HIP runtime given GPU_MAX_HW_QUEUES={q}" + (" (HIP's default: what a beacon node that sets "
-                                                                  "nothing runs)" if q == 4 else "") +
-                    "; the headline line runs with 24 (one hardware queue per context)"}
+            "note": "the headline's cfg2 shape in a child process started before the parent's first GPU call, " + (
+                "GPU_MAX_HW_QUEUES unset: what a beacon node that configures nothing runs (the library sets 24 as it "
+                "loads, bls_gpu.hip bls_default_hw_queues)" if q == "unset" else
+                f"its HIP runtime given GPU_MAX_HW_QUEUES={q} explicitly" + (" (HIP's own default)" if q == "4" else ""))
+                    + "; the headline line runs with 24 (one hardware queue per context)"}
     return res
 
 

@@ -801,7 +801,23 @@ BLS_HD Fp fp_from_mont(const Fp& a) {
   return fp_mul(a, one);
 }
 
+}  // namespace bls
+#include "lazy28.hpp"
+namespace bls {
+
 // a^e for an exponent given as a limb accessor (wave-uniform, MSB first).
+// BLS_LAZY_POW (every device build; the CPU test harness and the work model define it,
+// the CPU baseline does not): the chain runs in the lazy 28-bit-digit form
+// (lazy28.hpp lz_pow_const: no limb re-cut, pack or final subtraction per product).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(BLS_LAZY_POW)
+#define BLS_LAZY_POW 1
+#endif
+#ifdef BLS_LAZY_POW
+template <uint32_t (*E)(int), int BITS>
+BLS_HD Fp fp_pow_const(const Fp& a) {
+  return lz_pow_const<E, BITS>(a);
+}
+#else
 template <uint32_t (*E)(int), int BITS>
 BLS_HD Fp fp_pow_const(const Fp& a) {
   // sliding window of width 4 over the fixed exponent, odd powers a, a^3, .., a^15
@@ -831,6 +847,7 @@ BLS_HD Fp fp_pow_const(const Fp& a) {
   }
   return r;
 }
+#endif
 
 BLS_HD Fp fp_inv(const Fp& a) { return fp_pow_const<e_p_minus_2, E_P_MINUS_2_BITS>(a); }
 

@@ -333,6 +333,23 @@ uint32_t g_adm_normal[ADM_MAX_DEV], g_adm_high[ADM_MAX_DEV];
 std::atomic<uint64_t> g_adm_budget_override{0};
 thread_local char g_init_err[512];
 
+// The HIP runtime maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues per
+// priority (HIP's default 4), and streams sharing a queue serialise: 12 contexts x 22
+// calls give 2.27M sets/s on 4 queues against 3.42M on 16 and 3.65M on 24
+// (bench.py hw_queues_4 / hw_queues_16, profiles/r05_bench_first.json).  When the
+// variable is unset as the library loads, it is set to BLS_DEFAULT_HW_QUEUES here, before
+// the library's first HIP call, so a host that configures nothing (the beacon node
+// loading the N-API addon) gets a queue per context; an explicit value is kept, and
+// $BLS_KEEP_HW_QUEUES=1 leaves the runtime's default alone.  (A process whose HIP runtime
+// was initialised before this library loaded keeps the queues it started with; the
+// admission arithmetic then over-counts queues, the safe direction.)
+#define BLS_DEFAULT_HW_QUEUES "24"
+__attribute__((constructor)) void bls_default_hw_queues() {
+  const char* e = getenv("GPU_MAX_HW_QUEUES");
+  if ((e && *e) || getenv("BLS_KEEP_HW_QUEUES")) return;
+  setenv("GPU_MAX_HW_QUEUES", BLS_DEFAULT_HW_QUEUES, 0);
+}
+
 uint32_t hw_queues_env() {
   const char* e = getenv("GPU_MAX_HW_QUEUES");
   const long v = e && *e ? strtol(e, nullptr, 10) : 0;

@@ -10,9 +10,12 @@
 //   G1 = 96 B uncompressed (x || y); G2 = 192 B uncompressed (ZCash order x.c1 x.c0 y.c1 y.c0).
 #include <string.h>
 
+// the device's exponentiation chains (field.hpp fp_pow_const -> lazy28.hpp lz_pow_const)
+#define BLS_LAZY_POW 1
 #include "bls/pairing.hpp"
 #include "bls/hash_to_curve.hpp"
 #include "bls/pipeline.hpp"
+#include "bls/lazy12.hpp"
 
 unsigned long long bls_fpm_counter = 0;
 
@@ -463,4 +466,82 @@ int hs_pre_dedup_check(const uint8_t* msgs, uint32_t n, uint32_t* uniq_out, uint
   return (int)u;
 }
 
+}  // extern "C"
+
+// ---- bls/lazy28.hpp: the 14 x 28-bit lazy representation (R' = 2^392) --------------
+extern "C" {
+
+// the raw product on digit vectors (little-endian uint32 x 14 each): out = x y / 2^392
+// mod p, normalised digits
+void hs_lz_mul_raw(const int32_t* x, const int32_t* y, int32_t* out, int sqr) {
+  if (sqr) lz_sqr_core(x, out);
+  else lz_mul_core(x, y, out);
+}
+
+// canonical Fp (48 B big-endian, plain values) through the lazy forms and back, in
+// the order test_hostsim.py::test_lazy28_fp_ops expects (9 outputs of 48 B)
+void hs_lz_fp_ops(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  const auto x = lz_from_fp(rd_fp(a)), y = lz_from_fp(rd_fp(b));
+  const auto xy = lz_mul(x, y);
+  wr_fp(lz_to_fp(xy), out);                                       // a b
+  wr_fp(lz_to_fp(lz_sqr(x)), out + 48);                           // a^2
+  wr_fp(lz_to_fp(lz_add(x, y)), out + 96);                        // a + b
+  wr_fp(lz_to_fp(lz_sub(x, y)), out + 144);                       // a - b
+  wr_fp(lz_to_fp(lz_neg(xy)), out + 192);                         // -(a b)
+  wr_fp(lz_to_fp(lz_half(xy)), out + 240);                        // a b / 2
+  wr_fp(lz_to_fp(lz_norm(lz_sub(xy, lz_dbl(xy)))), out + 288);    // -(a b)
+  const auto s = lz_sub(lz_add(xy, xy), lz_mul(y, y));
+  wr_fp(lz_to_fp(lz_mul(s, lz_norm(lz_sub(y, x)))), out + 336);   // (2ab - b^2)(b - a)
+  wr_fp(lz_to_fp(x), out + 384);                                  // a (round trip)
+}
+
+// Fp2 (96 B: c0 || c1) through l2_*: out = mul, sqr, mul_xi, conj, sub, mul_fp (6 x 96 B)
+void hs_lz_fp2_ops(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  const auto x = l2_from_fp2(rd_fp2(a)), y = l2_from_fp2(rd_fp2(b));
+  const auto m = l2_mul(x, y);
+  wr_fp2(l2_to_fp2(m), out);
+  wr_fp2(l2_to_fp2(l2_sqr(x)), out + 96);
+  wr_fp2(l2_to_fp2(l2_mul_xi(m)), out + 192);
+  wr_fp2(l2_to_fp2(l2_conj(m)), out + 288);
+  wr_fp2(l2_to_fp2(l2_sub(m, l2_sqr(y))), out + 384);
+  wr_fp2(l2_to_fp2(l2_mul_fp(m, y.c0)), out + 480);
+}
+
+}  // extern "C"
+
+// ---- bls/lazy12.hpp: the Miller loop's f-side formulas in the lazy form ----------------
+typedef LzN<2> LzT;  // inputs brought to |value| < 2 p, as the kernels' products leave them
+static L2<LzT> rd_l2(const uint8_t* b) {
+  const Fp2 a = rd_fp2(b);
+  return L2<LzT>{lz_mul(lz_from_fp(a.c0), lz_one()), lz_mul(lz_from_fp(a.c1), lz_one())};
+}
+static L12<LzT> rd_l12(const uint8_t* b) {
+  return L12<LzT>{L6<LzT>{rd_l2(b), rd_l2(b + 2 * 96), rd_l2(b + 4 * 96)},
+                  L6<LzT>{rd_l2(b + 96), rd_l2(b + 3 * 96), rd_l2(b + 5 * 96)}};
+}
+template <class T>
+static void wr_l12(const L12<T>& f, uint8_t* b) {
+  Fp12 r;
+  r.c0 = Fp6{l2_to_fp2(f.c0.c0), l2_to_fp2(f.c0.c1), l2_to_fp2(f.c0.c2)};
+  r.c1 = Fp6{l2_to_fp2(f.c1.c0), l2_to_fp2(f.c1.c1), l2_to_fp2(f.c1.c2)};
+  wr_fp12(r, b);
+}
+extern "C" {
+// f (576 B), lines l = (l0, l2, l3), m (3 x 96 B each): out = lazy sqr, mul_line,
+// mul_line2, conj, then field.hpp's fp12_sqr, fp12_mul_line, fp12_mul_line2 (7 x 576 B)
+void hs_lz_fp12_ops(const uint8_t* fb, const uint8_t* lb, const uint8_t* mb, uint8_t* out) {
+  const auto f = rd_l12(fb);
+  const auto l0 = rd_l2(lb), l2 = rd_l2(lb + 96), l3 = rd_l2(lb + 192);
+  const auto m0 = rd_l2(mb), m2 = rd_l2(mb + 96), m3 = rd_l2(mb + 192);
+  wr_l12(l12_sqr(f), out);
+  wr_l12(l12_mul_line(f, l0, l2, l3), out + 576);
+  wr_l12(l12_mul_line2(f, l0, l2, l3, m0, m2, m3), out + 2 * 576);
+  wr_l12(l12_conj(f), out + 3 * 576);
+  const Fp12 g = rd_fp12(fb);
+  const Fp2 L0 = rd_fp2(lb), L2v = rd_fp2(lb + 96), L3 = rd_fp2(lb + 192);
+  const Fp2 M0 = rd_fp2(mb), M2 = rd_fp2(mb + 96), M3 = rd_fp2(mb + 192);
+  wr_fp12(fp12_sqr(g), out + 4 * 576);
+  wr_fp12(fp12_mul_line(g, L0, L2v, L3), out + 5 * 576);
+  wr_fp12(fp12_mul_line2(g, L0, L2v, L3, M0, M2, M3), out + 6 * 576);
+}
 }  // extern "C"

@@ -32,6 +32,27 @@ def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
         abi.load_library()
 
 
+def test_default_hw_queues_set_on_load():
+    """Loading the library sets GPU_MAX_HW_QUEUES (unset) to 24 before its first HIP call,
+    so a host that configures nothing gets one hardware queue per context
+    (bls_gpu.hip bls_default_hw_queues); an explicit value is kept."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import os, sys; sys.path.insert(0, %r); from lodestar_amd._abi import load_library; load_library(); "
+            "print(os.environ.get('GPU_MAX_HW_QUEUES'))" % str(ROOT))
+    env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "BLS_KEEP_HW_QUEUES")}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.stdout.strip() == "24", out.stderr[-500:]
+    out = subprocess.run([sys.executable, "-c", code], env=dict(env, GPU_MAX_HW_QUEUES="4"), capture_output=True,
+                         text=True, timeout=120)
+    assert out.stdout.strip() == "4"
+    out = subprocess.run([sys.executable, "-c", code], env=dict(env, BLS_KEEP_HW_QUEUES="1"), capture_output=True,
+                         text=True, timeout=120)
+    assert out.stdout.strip() == "None"
+
+
 def test_device_count_without_gpu():
     from lodestar_amd._abi import load_library
 
@@ -51,7 +72,11 @@ def test_scratch_admission_accounting():
 
     lib = load_library()
     res = json.loads((ROOT / "lodestar_amd" / "_native" / "kernel_resources.json").read_text())
-    per_queue = max(k["device_scratch_bytes"] for k in res["kernels"])
+    from lodestar_amd.build import FIXTURE_KERNELS, FIXTURE_TUS, _plain_name
+
+    # the deepest verify-path kernel (fixture and probe kernels never run on a verifier context)
+    per_queue = max(k["device_scratch_bytes"] for k in res["kernels"]
+                    if k["tu"] not in FIXTURE_TUS and _plain_name(k["name"]) not in FIXTURE_KERNELS)
     assert res["scratch_per_queue"] == per_queue > 0
     assert res["scratch_worst_kernel"].encode() == lib.bls_scratch_worst_kernel()
     lib.bls_gpu_set_scratch_budget(0)

@@ -7,6 +7,7 @@
 //
 // Build + run: python tools/work_model.py (writes lodestar_amd/_native/work_model.json).
 #define BLS_COUNT_OPS 1
+#define BLS_LAZY_POW 1  // the device's exponentiation chains (lazy28.hpp lz_pow_const)
 #include <stdio.h>
 
 #include "bls/hash_to_curve.hpp"
