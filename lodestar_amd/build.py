@@ -42,7 +42,9 @@ def sources() -> list[Path]:
 # A/B build variants: extra defines -> lodestar_amd/_native/liblodestar_bls_<name>.so
 # (the round-3 variants that lost were removed from the sources; their A/B records stay
 # under profiles/r03_ab_*.json)
-VARIANTS: dict[str, list[str]] = {}
+VARIANTS: dict[str, list[str]] = {
+    "mlflz": ["-DBLS_LAZY_MLF=1"],   # both Miller-loop kernels in the lazy 28-bit-digit form (slower, k_mlq.hip)
+}
 
 
 # Scratch: the HIP runtime backs each hardware queue with scratch for a full device of the

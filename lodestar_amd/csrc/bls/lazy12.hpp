@@ -94,6 +94,15 @@ template <class A>
 BLS_HD auto l12_norm(const L12<A>& a) {
   return l12_make(l6_norm(a.c0), l6_norm(a.c1));
 }
+template <class A>
+BLS_HD L6<LzN<2>> l6_reduce(const L6<A>& a) {
+  return L6<LzN<2>>{l2_reduce(a.c0), l2_reduce(a.c1), l2_reduce(a.c2)};
+}
+// every coefficient back to |value| < 2 p (lz_reduce): the Miller loop's f between steps
+template <class A>
+BLS_HD L12<LzN<2>> l12_reduce(const L12<A>& a) {
+  return L12<LzN<2>>{l6_reduce(a.c0), l6_reduce(a.c1)};
+}
 
 // complex squaring (field.hpp fp12_sqr): (A + B w)^2 = (s - ab - v ab) + 2 ab w,
 // ab = A B, s = (A + B)(A + v B)
@@ -126,6 +135,60 @@ BLS_HD auto l12_mul_line2(const L12<F>& f, const L2<L>& l0, const L2<L>& l2, con
   const auto t1 = l6_mul_v(l6_mul_01(f.c1, a3, a5));  // f.c1 (a3 v + a5 v^2)
   const auto c1 = l6_sub(l6_sub(l6_mul(l6_add(f.c0, f.c1), l6_make(a0, l2_add(a2, a3), l2_add(m22, a5))), t0), t1);
   return l12_make(l6_add(t0, l6_mul_v(t1)), c1);
+}
+
+// ---- the line side (kernels/k_mlq.hip k_mlq) ------------------------------------------
+// pairing.hpp's miller_dbl_step / miller_add_step in the lazy form, each followed by the
+// line's evaluation at the prepared G1 point (l0 z^3, l2 XZ, l3 Y: products, so the three
+// line coefficients come out normalised with |value| < 2 p, the form k_mlf reads).
+// T = LzN<2>: every coordinate a product's output or reduced (lz_reduce), so the type closes
+template <class T>
+struct LProj {
+  L2<T> x, y, z;
+};
+typedef LzN<2> LzL;  // a stored line coefficient
+template <class P>
+struct LEval {
+  P xz, y, z3;
+};
+
+template <class T, class P>
+BLS_HD void lz_dbl_line(LProj<T>& t, const LEval<P>& e1, L2<LzL> l[3]) {
+  const auto a = l2_half(l2_mul(t.x, t.y));
+  const auto b = l2_sqr(t.y);
+  const auto c = l2_sqr(t.z);
+  const auto e = l2_mul_xi(l2_mulc<4>(l2_norm(l2_mulc<3>(c))));  // 3 b' c, b' = 4 (1 + u)
+  const auto f = l2_mulc<3>(e);
+  const auto g = l2_half(l2_add(b, f));
+  const auto h = l2_sub(l2_sqr(l2_add(t.y, t.z)), l2_add(b, c));
+  const auto i = l2_sub(e, b);
+  const auto j = l2_sqr(t.x);
+  const auto e2 = l2_sqr(e);
+  t.x = l2_widen<T>(l2_mul(a, l2_sub(b, f)));
+  t.y = l2_widen<T>(l2_reduce(l2_sub(l2_sqr(g), l2_mulc<3>(e2))));  // the one sum T keeps
+  t.z = l2_widen<T>(l2_mul(b, h));
+  l[0] = l2_widen<LzL>(l2_mul_fp(i, e1.z3));
+  l[1] = l2_widen<LzL>(l2_mul_fp(l2_mulc<3>(j), e1.xz));
+  l[2] = l2_widen<LzL>(l2_mul_fp(l2_neg(h), e1.y));
+}
+
+template <class T, class Q, class P>
+BLS_HD void lz_add_line(LProj<T>& t, const L2<Q>& qx, const L2<Q>& qy, const LEval<P>& e1, L2<LzL> l[3]) {
+  const auto theta = l2_sub(t.y, l2_mul(qy, t.z));
+  const auto lambda = l2_sub(t.x, l2_mul(qx, t.z));
+  const auto c = l2_sqr(theta);
+  const auto d = l2_sqr(lambda);
+  const auto e = l2_mul(lambda, d);
+  const auto f = l2_mul(t.z, c);
+  const auto g = l2_mul(t.x, d);
+  const auto h = l2_sub(l2_add(e, f), l2_dbl(g));
+  const auto ty = l2_sub(l2_mul(theta, l2_sub(g, h)), l2_mul(e, t.y));
+  t.x = l2_widen<T>(l2_mul(lambda, h));
+  t.y = l2_widen<T>(l2_reduce(ty));
+  t.z = l2_widen<T>(l2_mul(t.z, e));
+  l[0] = l2_widen<LzL>(l2_mul_fp(l2_sub(l2_mul(theta, qx), l2_mul(lambda, qy)), e1.z3));
+  l[1] = l2_widen<LzL>(l2_mul_fp(l2_neg(theta), e1.xz));
+  l[2] = l2_widen<LzL>(l2_mul_fp(lambda, e1.y));
 }
 
 }  // namespace bls

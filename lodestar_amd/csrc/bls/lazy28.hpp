@@ -32,6 +32,13 @@
 
 #include "field.hpp"  // (field.hpp includes this header after its Fp basics)
 
+#if defined(BLS_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long bls_lz_norm_counter;  // host-only: carry passes (tests, work model)
+#define LZ_COUNT_NORM() (++bls_lz_norm_counter)
+#else
+#define LZ_COUNT_NORM() ((void)0)
+#endif
+
 namespace bls {
 
 #define LZ_M28 0xFFFFFFFll
@@ -126,6 +133,7 @@ BLS_HD auto lz_mulc(const Lz<D, V>& a) {
     for (int k = 0; k < 14; ++k) r.d[k] = (int32_t)C * a.d[k];
     return r;
   } else {
+    static_assert(D > LZ_M28, "C (2^28 - 1) must fit 31 bits");
     return lz_mulc<C>(lz_norm(a));
   }
 }
@@ -136,6 +144,7 @@ using LzN = Lz<lz_max(LZ_M28, lz_top_norm(V)), V>;
 template <int64_t D, int64_t V>
 BLS_HD Lz<lz_max(LZ_M28, lz_top_norm(V)), V> lz_norm(const Lz<D, V>& a) {
   static_assert(D <= LZ_DMAX, "carry room");
+  LZ_COUNT_NORM();
   LzN<V> r;
   int32_t c = 0;
 #pragma unroll
@@ -150,20 +159,46 @@ BLS_HD Lz<lz_max(LZ_M28, lz_top_norm(V)), V> lz_norm(const Lz<D, V>& a) {
 // a product's output: normalised digits, |value| < 2 p
 typedef LzN<2> LzP;
 
+// Value reduction in one carry pass: q ~ value / p from the top digit alone (value =
+// d13 2^364 + L with |L| < 2^31 2^337, i.e. < 2^-13 p), then the digits of value - q p
+// with carries (64-bit per digit: |q p_k| < 2^40).  q = floor(d13 C / 2^32) with C =
+// floor(2^396 / p) = 40323 is at most ~1.03 below value / p and never above it by more
+// than 0.03: the result is in (-p/32, 1.1 p).
+// ~5 VALU instructions a digit; what keeps a loop-carried value (the Miller loop's f)
+// from growing past the bounds its next products need.
+#define LZ_QC 40323ll
+template <int64_t D, int64_t V>
+BLS_HD LzN<2> lz_reduce(const Lz<D, V>& a) {
+  const int32_t q = (int32_t)(((int64_t)a.d[13] * LZ_QC) >> 32);
+  LzN<2> r;
+  int32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 13; ++k) {
+    const int64_t t = (int64_t)a.d[k] + c - (int64_t)q * lz_p28(k);
+    r.d[k] = (int32_t)((uint32_t)t & (uint32_t)LZ_M28);
+    c = (int32_t)(t >> 28);
+  }
+  r.d[13] = (int32_t)((int64_t)a.d[13] + c - (int64_t)q * lz_p28(13));
+  return r;
+}
+
 // a / 2 mod p: (a + (a odd ? p : 0)) / 2, halved digit by digit (each digit's low bit
 // moves down as 2^27 into the digit below; the value's parity is digit 0's)
 template <int64_t D, int64_t V>
-BLS_HD Lz<(D + LZ_M28) / 2 + (1ll << 27), V> lz_half(const Lz<D, V>& a) {
-  static_assert(D + LZ_M28 <= LZ_DMAX, "room for p");
-  const int32_t mask = -(a.d[0] & 1);
-  int32_t s[14];
+BLS_HD auto lz_half(const Lz<D, V>& a) {
+  if constexpr (D + LZ_M28 <= LZ_DMAX) {
+    const int32_t mask = -(a.d[0] & 1);
+    int32_t s[14];
 #pragma unroll
-  for (int k = 0; k < 14; ++k) s[k] = a.d[k] + ((int32_t)lz_p28(k) & mask);
-  Lz<(D + LZ_M28) / 2 + (1ll << 27), V> r;
+    for (int k = 0; k < 14; ++k) s[k] = a.d[k] + ((int32_t)lz_p28(k) & mask);
+    Lz<(D + LZ_M28) / 2 + (1ll << 27), V> r;
 #pragma unroll
-  for (int k = 0; k < 13; ++k) r.d[k] = (s[k] >> 1) + ((s[k + 1] & 1) << 27);
-  r.d[13] = s[13] >> 1;
-  return r;
+    for (int k = 0; k < 13; ++k) r.d[k] = (s[k] >> 1) + ((s[k + 1] & 1) << 27);
+    r.d[13] = s[13] >> 1;
+    return r;
+  } else {
+    return lz_half(lz_norm(a));
+  }
 }
 
 // ---- the product -----------------------------------------------------------------
@@ -422,6 +457,10 @@ BLS_HD auto l2_mulc(const L2<A>& a) {
 template <class A>
 BLS_HD auto l2_norm(const L2<A>& a) {
   return l2_join(lz_norm(a.c0), lz_norm(a.c1));
+}
+template <class A>
+BLS_HD L2<LzN<2>> l2_reduce(const L2<A>& a) {
+  return L2<LzN<2>>{lz_reduce(a.c0), lz_reduce(a.c1)};
 }
 template <class A>
 BLS_HD auto l2_half(const L2<A>& a) {

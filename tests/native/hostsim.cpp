@@ -18,6 +18,7 @@
 #include "bls/lazy12.hpp"
 
 unsigned long long bls_fpm_counter = 0;
+unsigned long long bls_lz_norm_counter = 0;
 
 using namespace bls;
 
@@ -493,6 +494,12 @@ void hs_lz_fp_ops(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   const auto s = lz_sub(lz_add(xy, xy), lz_mul(y, y));
   wr_fp(lz_to_fp(lz_mul(s, lz_norm(lz_sub(y, x)))), out + 336);   // (2ab - b^2)(b - a)
   wr_fp(lz_to_fp(x), out + 384);                                  // a (round trip)
+  // lz_reduce of a large signed combination: 4 (2ab - 7 b^2 - 7 a) (|value| up to 128 p)
+  const auto big = lz_sub(lz_sub(lz_add(xy, xy), lz_mulc<7>(lz_mul(y, y))), lz_mulc<7>(lz_mul(x, lz_one())));
+  const auto red = lz_reduce(lz_add(lz_add(big, big), lz_add(big, big)));
+  for (int k = 0; k < 13; ++k)
+    if (red.d[k] < 0 || red.d[k] > (int32_t)LZ_M28) out[0] ^= 0xFF;  // digits normalised
+  wr_fp(lz_to_fp(red), out + 432);
 }
 
 // Fp2 (96 B: c0 || c1) through l2_*: out = mul, sqr, mul_xi, conj, sub, mul_fp (6 x 96 B)
@@ -536,7 +543,7 @@ void hs_lz_fp12_ops(const uint8_t* fb, const uint8_t* lb, const uint8_t* mb, uin
   wr_l12(l12_sqr(f), out);
   wr_l12(l12_mul_line(f, l0, l2, l3), out + 576);
   wr_l12(l12_mul_line2(f, l0, l2, l3, m0, m2, m3), out + 2 * 576);
-  wr_l12(l12_conj(f), out + 3 * 576);
+  wr_l12(l12_conj(l12_reduce(l12_sqr(f))), out + 3 * 576);
   const Fp12 g = rd_fp12(fb);
   const Fp2 L0 = rd_fp2(lb), L2v = rd_fp2(lb + 96), L3 = rd_fp2(lb + 192);
   const Fp2 M0 = rd_fp2(mb), M2 = rd_fp2(mb + 96), M3 = rd_fp2(mb + 192);
@@ -545,3 +552,52 @@ void hs_lz_fp12_ops(const uint8_t* fb, const uint8_t* lb, const uint8_t* mb, uin
   wr_fp12(fp12_mul_line2(g, L0, L2v, L3, M0, M2, M3), out + 6 * 576);
 }
 }  // extern "C"
+
+// pairing.hpp miller_dbl_step / miller_add_step + line evaluation against lazy12.hpp
+// lz_dbl_line / lz_add_line: Q (G2 affine, 192 B), P (G1, 96 B): runs `steps` steps of
+// each kind from T = Q; out = the last dbl line (3 x 96 B), the last add line, T (3 x 96 B)
+// for the lazy form, then the same for the reference form (2 x 864 B)
+extern "C" void hs_lz_line_steps(const uint8_t* qb, const uint8_t* pb, int steps, uint8_t* out) {
+  const G2A q = rd_g2(qb);
+  const G1A p = rd_g1(pb);
+  const G1Eval P = g1_eval_from_aff(p);
+  // lazy
+  {
+    const LEval<LzT> e1{lz_mul(lz_from_fp(P.xz), lz_one()), lz_mul(lz_from_fp(P.y), lz_one()),
+                        lz_mul(lz_from_fp(P.z3), lz_one())};
+    const L2<LzT> qx{lz_mul(lz_from_fp(q.x.c0), lz_one()), lz_mul(lz_from_fp(q.x.c1), lz_one())};
+    const L2<LzT> qy{lz_mul(lz_from_fp(q.y.c0), lz_one()), lz_mul(lz_from_fp(q.y.c1), lz_one())};
+    typedef Lz<3 * LZ_M28, 8> TT;
+    const L2<LzT> one{lz_widen<LzT>(lz_one()), lz_widen<LzT>(lz_zero())};
+    LProj<TT> t{l2_widen<TT>(qx), l2_widen<TT>(qy), l2_widen<TT>(one)};
+    L2<LzL> ld[3], la[3];
+    for (int s = 0; s < steps; ++s) {
+      lz_dbl_line(t, e1, ld);
+      lz_add_line(t, qx, qy, e1, la);
+    }
+    for (int j = 0; j < 3; ++j) {
+      wr_fp2(l2_to_fp2(ld[j]), out + 96 * j);
+      wr_fp2(l2_to_fp2(la[j]), out + 288 + 96 * j);
+    }
+    wr_fp2(l2_to_fp2(t.x), out + 576);
+    wr_fp2(l2_to_fp2(t.y), out + 672);
+    wr_fp2(l2_to_fp2(t.z), out + 768);
+  }
+  // reference
+  {
+    G2Proj T{q.x, q.y, fp2_one()};
+    Fp2 d[3], a[3];
+    for (int s = 0; s < steps; ++s) {
+      miller_dbl_step(T, d[0], d[1], d[2]);
+      miller_add_step(T, q, a[0], a[1], a[2]);
+    }
+    const Fp* ev[3] = {&P.z3, &P.xz, &P.y};
+    for (int j = 0; j < 3; ++j) {
+      wr_fp2(fp2_mul_fp(d[j], *ev[j]), out + 864 + 96 * j);
+      wr_fp2(fp2_mul_fp(a[j], *ev[j]), out + 864 + 288 + 96 * j);
+    }
+    wr_fp2(T.x, out + 864 + 576);
+    wr_fp2(T.y, out + 864 + 672);
+    wr_fp2(T.z, out + 864 + 768);
+  }
+}

@@ -72,13 +72,13 @@ def test_lazy28_raw_product_bounds(hostsim):
 def test_lazy28_fp_ops(hostsim):
     """lz_from_fp -> lazy formulas -> lz_to_fp equals the field arithmetic."""
     rng = random.Random(28)
-    out = ctypes.create_string_buffer(9 * 48)
+    out = ctypes.create_string_buffer(10 * 48)
     vals = [0, 1, 2, P - 1, P - 2, (P - 1) // 2, 2 ** 380, 2 ** 381 - 1 if 2 ** 381 - 1 < P else P - 3]
     vals += [rng.randrange(P) for _ in range(200)]
     for k, a in enumerate(vals):
         b = vals[(7 * k + 3) % len(vals)]
         hostsim.hs_lz_fp_ops(b48(a), b48(b), out)
-        r = [fp(out.raw[48 * i: 48 * i + 48]) for i in range(9)]
+        r = [fp(out.raw[48 * i: 48 * i + 48]) for i in range(10)]
         ab = a * b % P
         assert r[0] == ab
         assert r[1] == a * a % P
@@ -89,6 +89,7 @@ def test_lazy28_fp_ops(hostsim):
         assert r[6] == (-ab) % P
         assert r[7] == (2 * ab - b * b) * (b - a) % P
         assert r[8] == a
+        assert r[9] == 4 * (2 * ab - 7 * b * b - 7 * a) % P
 
 
 def test_lazy28_fp2_ops(hostsim):
@@ -130,7 +131,21 @@ def test_lazy28_fp12_ops(hostsim):
         assert r[0] == r[4]
         assert r[1] == r[5]
         assert r[2] == r[6]
-        conj = [fp(f[48 * i: 48 * i + 48]) for i in range(12)]
-        # w^1, w^3, w^5 coefficients (the c1 half) negate
-        want = b"".join(b48((-v) % P if (i // 2) % 2 == 1 else v) for i, v in enumerate(conj))
+        sq = [fp(r[4][48 * i: 48 * i + 48]) for i in range(12)]
+        # conj(reduce(sqr f)): the w^1, w^3, w^5 coefficients (the c1 half) negate
+        want = b"".join(b48((-v) % P if (i // 2) % 2 == 1 else v) for i, v in enumerate(sq))
         assert r[3] == want
+
+
+def test_lazy28_line_steps(hostsim, oracle):
+    """lazy12.hpp lz_dbl_line / lz_add_line (k_mlq's line side) equal pairing.hpp's
+    miller_dbl_step / miller_add_step and their evaluation at P, bit for bit, after 1, 5
+    and 20 rounds of both steps from T = Q (Q, P: multiples of the generators)."""
+    from tests._codec import g1b, g2b
+
+    out = ctypes.create_string_buffer(2 * 864)
+    for k, steps in ((3, 1), (11, 5), (29, 20)):
+        q = oracle.E2.mul(oracle.G2, k)
+        p = oracle.E1.mul(oracle.G1, 7 * k + 1)
+        hostsim.hs_lz_line_steps(g2b(q), g1b(p), steps, out)
+        assert out.raw[:864] == out.raw[864:]

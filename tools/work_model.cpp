@@ -15,6 +15,7 @@
 #include "bls/pipeline.hpp"
 
 unsigned long long bls_fpm_counter = 0;
+unsigned long long bls_lz_norm_counter = 0;
 
 using namespace bls;
 
