@@ -39,17 +39,10 @@ namespace {
 // out-of-line isogeny (bls/hash_to_curve.hpp iso_map_jac), called twice per set
 __device__ __noinline__ void iso_jac_nl(G2J* out, const Fp* q) { *out = iso_map_jac(Fp2{q[0], q[1]}, Fp2{q[2], q[3]}); }
 
-__device__ G2J iso_jac(const Fp* q) {
-  G2J r;
-  iso_jac_nl(&r, q);
-  return r;
-}
-
-// One out-of-line copy of each chain (A and U on a Jacobian G2 base, C and RS on the
-// affine signature, RP on G1):
-// the double-and-add body is large, so the kernel keeps a single instance of it.
-__device__ __noinline__ void g2_mul_u64(G2J* out, const G2J* in, uint64_t k) { *out = jac_mul_u64(*in, k); }
-// affine base (the signature): mixed additions
+// One out-of-line copy of each chain (the two [x] chains of H and the subgroup test on
+// affine bases, RS on the affine signature, RP on G1): the double-and-add body is large,
+// so the kernel keeps a single instance of it.
+// affine base: mixed additions
 __device__ __noinline__ void g2_mul_aff(G2J* out, const G2A* in, uint64_t k) { *out = aff_mul_u64(*in, k); }
 // [r] sig and [r] pk for the per-set batch scalar r: GLV/GLS (curve.hpp jac_mul_glv):
 // the set's scalar is a + b mu with a, b its two 32-bit halves and mu = -x^2, applied as
@@ -71,16 +64,29 @@ __device__ __noinline__ void g1_mul_r(G1J* out, const G1J* in, uint64_t k, G1J* 
 // out-of-line general addition for the handful of additions outside the chains
 __device__ __noinline__ void g2_add(G2J* out, const G2J* a, const G2J* b) { *out = jac_add(*a, *b); }
 
-__device__ G2J g2_add_v(const G2J& a, const G2J& b) {
-  G2J r;
-  g2_add(&r, &a, &b);
-  return r;
+// affine form of a Jacobian G2 point by one Fp inversion of N(Z) (binary GCD)
+__device__ __noinline__ void g2_to_aff(G2A* out, const G2J* in) {
+  if (jac_is_inf(*in)) {
+    out->x = fp2_zero();
+    out->y = fp2_zero();
+    out->inf = true;
+    return;
+  }
+  const Fp ni = fp_inv_gcd(fp_add(fp_sqr(in->z.c0), fp_sqr(in->z.c1)));
+  const Fp2 zi = Fp2{fp_mul(in->z.c0, ni), fp_neg(fp_mul(in->z.c1, ni))};
+  const Fp2 zi2 = fp2_sqr(zi);
+  out->x = fp2_mul(in->x, zi2);
+  out->y = fp2_mul(in->y, fp2_mul(zi2, zi));
+  out->inf = false;
 }
 
-__device__ G2J g2_mul_x(const G2J& p) {  // [x]P = -[|x|]P
-  G2J r;
-  g2_mul_u64(&r, &p, (uint64_t)BLS_X_ABS);
-  return jac_neg(r);
+// [x]P = -[|x|]P over the affine form of P: the chain's five additions are mixed
+// (madd-2007-bl, 29 Fp products instead of add-2007-bl's 43) for one inversion
+__device__ __noinline__ void g2_mul_x_aff(G2J* out, const G2J* p) {
+  G2A a;
+  g2_to_aff(&a, p);
+  g2_mul_aff(out, &a, (uint64_t)BLS_X_ABS);
+  out->y = fp2_neg(out->y);
 }
 
 __device__ void store_one(Fp12* f) {
@@ -108,44 +114,60 @@ __device__ bool chain_skip(const PipeBufs& b, uint32_t i) {
 // frame, not the kernel frame holding role 0's points plus the deepest callee (the
 // runtime reserves scratch per queue for a full device of wavefronts,
 // lodestar_amd/build.py SCRATCH_BUDGET).
-__device__ __noinline__ void chain_role_h(const PipeBufs& b, uint32_t i) {
-  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
-  // H = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P), P = iso(q0) + iso(q1)
-  const Fp* q = b.q + 8ull * i;
-  const G2J P = g2_add_v(iso_jac(q), iso_jac(q + 4));
-  const G2J t1 = g2_mul_x(P);
-  const G2J t2 = g2_psi(P);
-  G2J t3 = g2_psi(g2_psi(jac_dbl(P)));
-  t3 = g2_add_v(t3, jac_neg(t2));
-  t3 = g2_add_v(t3, g2_mul_x(g2_add_v(t1, t2)));
-  t3 = g2_add_v(t3, jac_neg(t1));
-  const G2J Hj = g2_add_v(t3, jac_neg(P));
-  b.chain_st[4 * i + 0] = jac_is_inf(Hj) ? 1 : 0;
-  if (jac_is_inf(Hj)) return;
-  // HQ = affine H: one Fp inversion of N(Z)
-  const Fp ni = fp_inv_gcd(fp_add(fp_sqr(Hj.z.c0), fp_sqr(Hj.z.c1)));
-  const Fp2 zi = Fp2{fp_mul(Hj.z.c0, ni), fp_neg(fp_mul(Hj.z.c1, ni))};
+// The role functions take the buffers they use as plain pointers: a `const PipeBufs&`
+// made the kernel copy its whole argument block into private memory (a 480-byte frame
+// under every role).
+__device__ __noinline__ void chain_role_h(Fp* chain, const Fp* qs, uint8_t* chain_st, uint32_t i) {
+  Fp* o = chain + (size_t)CHAIN_WORDS * i;
+  // H = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P), P = iso(q0) + iso(q1) (RFC 9380
+  // G.3), regrouped so one point stays live across each [x] chain and four additions
+  // remain instead of five:
+  //   s = [x]P + psi(P),   u = psi^2(2P) - (s + P),   H = [x]s + u
+  // (the same group element by the complete formulas, so the same affine H)
+  // Three point slots in private memory, reused in place (the out-of-line helpers take
+  // pointers; a fresh temporary per step made a 2.6 KB frame)
+  const Fp* q = qs + 8ull * i;
+  G2J A, B, C;
+  iso_jac_nl(&A, q);
+  iso_jac_nl(&B, q + 4);
+  g2_add(&A, &A, &B);             // A = P
+  g2_mul_x_aff(&B, &A);           // B = [x]P
+  C = g2_psi(A);
+  g2_add(&B, &B, &C);             // B = s
+  C = g2_psi(g2_psi(jac_dbl(A)));
+  g2_add(&A, &B, &A);
+  A.y = fp2_neg(A.y);
+  g2_add(&C, &C, &A);             // C = u
+  g2_mul_x_aff(&A, &B);           // A = [x]s
+  g2_add(&A, &A, &C);             // A = H
+  chain_st[4 * i + 0] = jac_is_inf(A) ? 1 : 0;
+  if (jac_is_inf(A)) return;
+  // HQ = affine H: one Fp inversion of N(Z) (inline here: through g2_to_aff the frame
+  // grows by the affine point's slot)
+  const Fp ni = fp_inv_gcd(fp_add(fp_sqr(A.z.c0), fp_sqr(A.z.c1)));
+  const Fp2 zi = Fp2{fp_mul(A.z.c0, ni), fp_neg(fp_mul(A.z.c1, ni))};
   const Fp2 zi2 = fp2_sqr(zi);
-  const Fp2 hx = fp2_mul(Hj.x, zi2);
-  const Fp2 hy = fp2_mul(Hj.y, fp2_mul(zi2, zi));
+  const Fp2 hx = fp2_mul(A.x, zi2);
+  const Fp2 hy = fp2_mul(A.y, fp2_mul(zi2, zi));
   o[CH_HQ + 0] = hx.c0;
   o[CH_HQ + 1] = hx.c1;
   o[CH_HQ + 2] = hy.c0;
   o[CH_HQ + 3] = hy.c1;
 }
 
-__device__ __noinline__ void chain_role_sub(const PipeBufs& b, uint32_t i) {
-  const G2A sig = b.sig[i];
+__device__ __noinline__ void chain_role_sub(const G2A* sigs, uint8_t* chain_st, uint32_t i) {
+  const G2A sig = sigs[i];
   G2J xs;
   g2_mul_aff(&xs, &sig, (uint64_t)BLS_X_ABS);
-  b.chain_st[4 * i + 1] = jac_eq(g2_psi(jac_from_aff(sig)), jac_neg(xs)) ? 0 : 1;
+  chain_st[4 * i + 1] = jac_eq(g2_psi(jac_from_aff(sig)), jac_neg(xs)) ? 0 : 1;
 }
 
-__device__ __noinline__ void chain_role_rs(const PipeBufs& b, uint32_t i) {
-  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
-  const G2A sig = b.sig[i];
+__device__ __noinline__ void chain_role_rs(Fp* chain, const G2A* sigs, const uint32_t* seed, uint32_t scalar_base,
+                                           G2J* rtab2, uint32_t i) {
+  Fp* o = chain + (size_t)CHAIN_WORDS * i;
+  const G2A sig = sigs[i];
   G2J RS;
-  g2_mul_r(&RS, &sig, set_scalar(b.seed, b.scalar_base + i), b.rtab2 + 15ull * i);
+  g2_mul_r(&RS, &sig, set_scalar(seed, scalar_base + i), rtab2 + 15ull * i);
   o[CH_RS + 0] = RS.x.c0;
   o[CH_RS + 1] = RS.x.c1;
   o[CH_RS + 2] = RS.y.c0;
@@ -154,12 +176,13 @@ __device__ __noinline__ void chain_role_rs(const PipeBufs& b, uint32_t i) {
   o[CH_RS + 5] = RS.z.c1;
 }
 
-__device__ __noinline__ void chain_role_rp(const PipeBufs& b, uint32_t i) {
-  Fp* o = b.chain + (size_t)CHAIN_WORDS * i;
+__device__ __noinline__ void chain_role_rp(Fp* chain, const G1J* pks, uint8_t* chain_st, const uint32_t* seed,
+                                           uint32_t scalar_base, G1J* rtab1, uint32_t i) {
+  Fp* o = chain + (size_t)CHAIN_WORDS * i;
   G1J RP;
-  const G1J pk = b.pk[i];
-  g1_mul_r(&RP, &pk, set_scalar(b.seed, b.scalar_base + i), b.rtab1 + 15ull * i);
-  b.chain_st[4 * i + 3] = jac_is_inf(RP) ? 1 : 0;
+  const G1J pk = pks[i];
+  g1_mul_r(&RP, &pk, set_scalar(seed, scalar_base + i), rtab1 + 15ull * i);
+  chain_st[4 * i + 3] = jac_is_inf(RP) ? 1 : 0;
   if (jac_is_inf(RP)) return;
   o[CH_RP + 0] = RP.x;
   o[CH_RP + 1] = RP.y;
@@ -198,10 +221,10 @@ __global__ __launch_bounds__(BLS_BLOCK) BLS_CHAIN_ATTR void k_chain(PipeBufs b, 
   // (plan_msg_dedup) runs role 0, whatever its own pubkey / signature status, unless
   // its SSWU points went to the exact path; k_chain_done shares the result
   if (role == 0 ? ((b.msg_rep && b.msg_rep[i] != i) || b.set_flag[i]) : chain_skip(b, i)) return;
-  if (role == 0) chain_role_h(b, i);
-  else if (role == 1) chain_role_sub(b, i);
-  else if (role == 2) chain_role_rs(b, i);
-  else chain_role_rp(b, i);
+  if (role == 0) chain_role_h(b.chain, b.q, b.chain_st, i);
+  else if (role == 1) chain_role_sub(b.sig, b.chain_st, i);
+  else if (role == 2) chain_role_rs(b.chain, b.sig, b.seed, b.scalar_base, b.rtab2, i);
+  else chain_role_rp(b.chain, b.pk, b.chain_st, b.seed, b.scalar_base, b.rtab1, i);
 }
 
 // One lane per set after the four roles: the set's fate.

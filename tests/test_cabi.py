@@ -40,8 +40,11 @@ def test_default_hw_queues_set_on_load():
     import subprocess
     import sys
 
-    code = ("import os, sys; sys.path.insert(0, %r); from lodestar_amd._abi import load_library; load_library(); "
-            "print(os.environ.get('GPU_MAX_HW_QUEUES'))" % str(ROOT))
+    # the C environment (os.environ is Python's snapshot from start-up; the library's
+    # constructor calls setenv)
+    code = ("import ctypes, sys; sys.path.insert(0, %r); from lodestar_amd._abi import load_library; load_library(); "
+            "libc = ctypes.CDLL(None); libc.getenv.restype = ctypes.c_char_p; "
+            "v = libc.getenv(b'GPU_MAX_HW_QUEUES'); print(v.decode() if v else None)" % str(ROOT))
     env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "BLS_KEEP_HW_QUEUES")}
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.stdout.strip() == "24", out.stderr[-500:]
