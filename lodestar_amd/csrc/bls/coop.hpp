@@ -25,6 +25,11 @@ namespace bls {
 #define COOP_OUT_NONE 0xFFFEu   // lane idle (kind 0, never written)
 #define COOP_OUT_ZSET 0xFFF0u   // zero-check of packed set s >= 1: 0xFFF0 + s
 #define COOP_MAX_CONSTS 40  // constants staged per block (tools/gen_coop.py asserts the bank fits)
+// op kinds (tools/gen_coop.py emit): 0 idle, 1 product of two combinations, 2 combination,
+// 3 / 4 one product on a lane pair (even lane: operand a and the write, odd lane: operand b)
+#define COOP_MUL 1u
+#define COOP_PAIR_A 3u
+#define COOP_PAIR_B 4u
 
 struct CoopOp {  // 80 bytes, one per lane per step (tools/gen_coop.py:emit)
   uint16_t out;
@@ -324,16 +329,26 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
   if (op.kind != 0) {
     r = coop_lin(op.a, op.ca, op.na, slots);
     if (TIMED && mark == 2 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
-    if (op.kind == 1) {
+    if (op.kind == COOP_MUL) {
       const Fp rb = coop_lin(op.b, op.cb, op.nb, slots);
       if (TIMED && mark == 3 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
       r = fp_mul_lazy(r, rb);
       if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
     }
   }
+  // a product on a lane pair (tools/gen_coop.py lane_entries): each lane gathered one
+  // operand; swap them with the neighbour (DPP quad_perm [1,0,3,2], every lane of the
+  // wave takes part) and both multiply -- the product is symmetric
+  if (__any(op.kind >= COOP_PAIR_A)) {
+    Fp o;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) o.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)r.l[i], 0xB1, 0xF, 0xF, false);
+    if (op.kind >= COOP_PAIR_A) r = fp_mul_lazy(r, o);
+    if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+  }
   if (TIMED && mark == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   coop_wave_sync();
-  if (op.kind != 0) {
+  if (op.kind != 0 && op.kind != COOP_PAIR_B) {
     if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
       if (fp_is_zero_lazy(r)) atomicOr(flag, op.out == COOP_OUT_ZCHECK ? 1u : 1u << (op.out - COOP_OUT_ZSET));
     } else {

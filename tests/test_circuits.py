@@ -69,3 +69,69 @@ def test_fin_final_exponentiation(progs, oracle):
     fr[GC.INV_OUT] = pow(fr[GC.INV_IN], P - 2, P)
     simulate(pg["fin_fe2"], fr, consts)
     assert get12(fr, GC.F) == oracle.final_exponentiation(f0, hard_multiple=3)
+
+
+def _run_binary(path, name, frame, n_consts):
+    """The emitted op table (gen_coop.emit) interpreted with coop.hpp coop_step's
+    semantics, lane by lane: kinds 1 (product), 2 (combination), 3 / 4 (a product on a
+    lane pair: each lane sums one operand, the pair swaps, the even lane writes)."""
+    import struct
+
+    raw = Path(path).read_bytes()
+    _, _, nc, nprog, _ = struct.unpack_from("<4sIIII", raw, 0)
+    off = 20
+    consts = [int.from_bytes(raw[off + 48 * k: off + 48 * (k + 1)], "little") for k in range(nc)]
+    off += 48 * nc
+    table = {}
+    for _ in range(nprog):
+        nm = raw[off: off + 32].rstrip(b"\0").decode()
+        table[nm] = struct.unpack_from("<IIII", raw, off + 32)
+        off += 48
+    first, n, n_slots, _ = table[name]
+    R_INV = pow(1 << 384, -1, P)
+    cvals = [c * R_INV % P for c in consts]  # the bank is in Montgomery form
+    flag = 0
+    for s in range(first, first + n):
+        lanes = [struct.unpack_from("<HBBB3x8H8H8h8h8x", raw, off + 80 * (64 * s + ln)) for ln in range(64)]
+
+        def lin(refs, cfs, k):
+            return sum(cf * (frame[r] if r < n_slots else cvals[r - n_slots]) for r, cf in zip(refs[:k], cfs[:k])) % P
+
+        vals = []
+        for out, kind, na, nb, *rest in lanes:
+            ra, rb, ca, cb = rest[0:8], rest[8:16], rest[16:24], rest[24:32]
+            v = lin(ra, ca, na) if kind else 0
+            if kind == 1:
+                v = v * lin(rb, cb, nb) % P
+            vals.append(v)
+        res = list(vals)
+        for ln, (out, kind, *_r) in enumerate(lanes):
+            if kind in (3, 4):
+                res[ln] = vals[ln] * vals[ln ^ 1] % P
+        for ln, (out, kind, *_r) in enumerate(lanes):
+            if kind in (0, 4):
+                continue
+            if out >= 0xFFF0:
+                if res[ln] == 0:
+                    flag |= 1 if out == 0xFFFF else 1 << (out - 0xFFF0)
+            else:
+                frame[out] = res[ln]
+    return flag
+
+
+def test_emitted_lane_pairs_match_program(progs, tmp_path):
+    """Product steps with room for two lanes per product are emitted as lane pairs
+    (gen_coop.lane_entries); the table the device runs computes what the program does."""
+    pg, consts = progs
+    path = tmp_path / "t.bin"
+    names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul"]
+    GC.emit([pg[nm] for nm in names], consts, path)
+    paired = sum(1 for nm in names for st in pg[nm].steps if any(e[1] == GC.PAIR_A for e in GC.lane_entries(st)))
+    assert paired >= 10
+    rng = random.Random(7)
+    for nm in names:
+        fr = [rng.randrange(P) for _ in range(pg[nm].n_slots)]
+        fr2 = list(fr)
+        f1 = simulate(pg[nm], fr, consts)
+        f2 = _run_binary(path, nm, fr2, len(consts.vals))
+        assert (fr, f1) == (fr2, f2), nm

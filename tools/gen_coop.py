@@ -422,6 +422,29 @@ def _le_limbs(v: int) -> bytes:
     return v.to_bytes(48, "little")
 
 
+PAIR_A, PAIR_B = 3, 4  # a product on a lane pair (lodestar_amd/csrc/bls/coop.hpp coop_step)
+
+
+def lane_entries(step) -> list:
+    """A step's lane entries (out, kind, a, b); out None = the lane writes nothing.
+
+    The interpreter runs one wavefront per task, so a step's time is one lane's
+    instruction stream, and in a product step the two operand gathers are more than half
+    of it.  A product step with room for two lanes per product (2 x products + linear
+    combinations <= 64) therefore runs each product on an adjacent lane pair: the even
+    lane (PAIR_A) gathers operand a, the odd lane (PAIR_B) operand b, the pair swaps the
+    sums (DPP) and both multiply; the even lane writes.  Other steps: one lane per op."""
+    muls = [op for op in step if op.kind == OP_MUL]
+    lins = [op for op in step if op.kind != OP_MUL]
+    if muls and 2 * len(muls) + len(lins) <= LANES:
+        out = []
+        for op in muls:
+            out.append((op.out, PAIR_A, op.a, []))
+            out.append((None, PAIR_B, op.b, []))
+        return out + [(op.out, op.kind, op.a, []) for op in lins]
+    return [(op.out, op.kind, op.a, op.b if op.kind == OP_MUL else []) for op in step]
+
+
 def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
     steps_bin = bytearray()
     table = bytearray()
@@ -431,18 +454,17 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
         table += name + struct.pack("<IIII", first, len(pg.steps), pg.n_slots, pg.n_mul_steps)
         for step in pg.steps:
             assert len(step) <= LANES
+            entries = lane_entries(step)
             for lane in range(LANES):
-                if lane < len(step):
-                    op = step[lane]
+                if lane < len(entries):
+                    out, kind, a, b = entries[lane]
                     # zero-checks: 0xFFFF for set 0, 0xFFF0 + s for packed set s >= 1
-                    if op.out == ZCHECK:
+                    if out is None:
+                        out = 0xFFFE
+                    elif out == ZCHECK:
                         out = 0xFFFF
-                    elif op.out < ZCHECK:
-                        out = 0xFFF0 + (ZCHECK - op.out)
-                    else:
-                        out = op.out
-                    kind = op.kind
-                    a, b = op.a, op.b if op.kind == OP_MUL else []
+                    elif out < ZCHECK:
+                        out = 0xFFF0 + (ZCHECK - out)
                 else:
                     out, kind, a, b = 0xFFFE, 0, [], []
                 assert len(a) <= 8 and len(b) <= 8
@@ -461,7 +483,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                                          *refs(a), *refs(b), *cfs(a), *cfs(b))
         first += len(pg.steps)
     assert len(consts.vals) <= 40, "constant bank exceeds COOP_MAX_CONSTS"
-    header = struct.pack("<4sIIII", b"BLSC", 1, len(consts.vals), len(progs), first)
+    header = struct.pack("<4sIIII", b"BLSC", 2, len(consts.vals), len(progs), first)
     cbin = b"".join(_le_limbs(v * MONT_R % P) for v in consts.vals)
     path.write_bytes(header + cbin + bytes(table) + bytes(steps_bin))
 
