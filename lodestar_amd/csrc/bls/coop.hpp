@@ -26,10 +26,12 @@ namespace bls {
 #define COOP_OUT_ZSET 0xFFF0u   // zero-check of packed set s >= 1: 0xFFF0 + s
 #define COOP_MAX_CONSTS 40  // constants staged per block (tools/gen_coop.py asserts the bank fits)
 // op kinds (tools/gen_coop.py emit): 0 idle, 1 product of two combinations, 2 combination,
-// 3 / 4 one product on a lane pair (even lane: operand a and the write, odd lane: operand b)
+// 3 / 4 one product on a lane pair (even lane: operand a and the write, odd lane: operand b),
 #define COOP_MUL 1u
 #define COOP_PAIR_A 3u
 #define COOP_PAIR_B 4u
+#define COOP_LPAIR_A 5u  // 5 / 6: one combination on a lane pair (even lane: the first half of the
+#define COOP_LPAIR_B 6u  // terms and the write, odd lane: the rest)
 
 struct CoopOp {  // 80 bytes, one per lane per step (tools/gen_coop.py:emit)
   uint16_t out;
@@ -225,8 +227,10 @@ __device__ __forceinline__ int coop_wave_max_terms(int n) {
 // leaves limb 12, the -|c| goes to the reduction bias.  (Round 3 formed every product
 // x |c| as a 13-limb number and added it with a carry chain: ~62 instructions per term
 // against ~26 here.)
-__device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n, const LdsU4* slots) {
-  if (__all(n == 1 && cf[0] == 1)) return lds_load_fp(slots, refs[0]);
+// The unreduced sum as a 13-limb two's-complement accumulator; returns the sum of |c|
+// over the negated terms (acc_reduce's bias)
+__device__ __forceinline__ uint32_t coop_lin_acc(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n,
+                                                 const LdsU4* slots, Acc13& acc) {
   const int nmax = coop_wave_max_terms(n);
   uint64_t col[12];
 #pragma unroll
@@ -243,7 +247,6 @@ __device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t 
 #pragma unroll
     for (int i = 0; i < 12; ++i) col[i] += (uint64_t)(x.l[i] ^ mask) * m;
   }
-  Acc13 acc;
 #pragma unroll
   for (int i = 0; i < 11; ++i) {
     acc.l[i] = (uint32_t)col[i];
@@ -251,7 +254,19 @@ __device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t 
   }
   acc.l[11] = (uint32_t)col[11];
   acc.l[12] = (uint32_t)(col[11] >> 32) - negs;  // two's complement: the -|c| 2^384 of the negated terms
+  return negs;
+}
+
+__device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n, const LdsU4* slots) {
+  if (__all(n == 1 && cf[0] == 1)) return lds_load_fp(slots, refs[0]);
+  Acc13 acc;
+  const uint32_t negs = coop_lin_acc(refs, cf, n, slots, acc);
   return acc_reduce(acc, negs);
+}
+
+// the value of lane ^ 1 (DPP quad_perm [1,0,3,2]; every lane of the wave must take part)
+__device__ __forceinline__ uint32_t coop_pair_swap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
 }
 
 // One lane's op of one step as fetched: the 80-byte CoopOp as 20 raw dwords, loaded
@@ -326,7 +341,17 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
   const CoopOpView op = coop_decode(raw);
   if (TIMED && mark == 1 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   Fp r = fp_zero();
-  if (op.kind != 0) {
+  if (__any(op.kind >= COOP_LPAIR_A)) {
+    // a combination on a lane pair: each lane sums its half of the terms, the pair adds
+    // the two unreduced sums (13 limbs and the negation bias), one reduction
+    Acc13 acc, oth;
+    uint32_t negs = coop_lin_acc(op.a, op.ca, op.kind ? (int)op.na : 0, slots, acc);
+#pragma unroll
+    for (int i = 0; i < 13; ++i) oth.l[i] = coop_pair_swap(acc.l[i]);
+    negs += coop_pair_swap(negs);
+    asm_acc_add13(acc.l, oth.l);
+    r = acc_reduce(acc, negs);
+  } else if (op.kind != 0) {
     r = coop_lin(op.a, op.ca, op.na, slots);
     if (TIMED && mark == 2 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
     if (op.kind == COOP_MUL) {
@@ -339,16 +364,17 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
   // a product on a lane pair (tools/gen_coop.py lane_entries): each lane gathered one
   // operand; swap them with the neighbour (DPP quad_perm [1,0,3,2], every lane of the
   // wave takes part) and both multiply -- the product is symmetric
-  if (__any(op.kind >= COOP_PAIR_A)) {
+  const bool pair = op.kind == COOP_PAIR_A || op.kind == COOP_PAIR_B;
+  if (__any(pair)) {
     Fp o;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) o.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)r.l[i], 0xB1, 0xF, 0xF, false);
-    if (op.kind >= COOP_PAIR_A) r = fp_mul_lazy(r, o);
+    for (int i = 0; i < 12; ++i) o.l[i] = coop_pair_swap(r.l[i]);
+    if (pair) r = fp_mul_lazy(r, o);
     if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   }
   if (TIMED && mark == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   coop_wave_sync();
-  if (op.kind != 0 && op.kind != COOP_PAIR_B) {
+  if (op.kind != 0 && op.kind != COOP_PAIR_B && op.kind != COOP_LPAIR_B) {
     if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
       if (fp_is_zero_lazy(r)) atomicOr(flag, op.out == COOP_OUT_ZCHECK ? 1u : 1u << (op.out - COOP_OUT_ZSET));
     } else {

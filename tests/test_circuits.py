@@ -74,7 +74,8 @@ def test_fin_final_exponentiation(progs, oracle):
 def _run_binary(path, name, frame, n_consts):
     """The emitted op table (gen_coop.emit) interpreted with coop.hpp coop_step's
     semantics, lane by lane: kinds 1 (product), 2 (combination), 3 / 4 (a product on a
-    lane pair: each lane sums one operand, the pair swaps, the even lane writes)."""
+    lane pair: each lane sums one operand, the pair swaps, the even lane writes), 5 / 6 (a
+    combination on a lane pair: each lane sums half of the terms)."""
     import struct
 
     raw = Path(path).read_bytes()
@@ -108,8 +109,10 @@ def _run_binary(path, name, frame, n_consts):
         for ln, (out, kind, *_r) in enumerate(lanes):
             if kind in (3, 4):
                 res[ln] = vals[ln] * vals[ln ^ 1] % P
+            elif kind in (5, 6):
+                res[ln] = (vals[ln] + vals[ln ^ 1]) % P
         for ln, (out, kind, *_r) in enumerate(lanes):
-            if kind in (0, 4):
+            if kind in (0, 4, 6):
                 continue
             if out >= 0xFFF0:
                 if res[ln] == 0:
@@ -120,14 +123,15 @@ def _run_binary(path, name, frame, n_consts):
 
 
 def test_emitted_lane_pairs_match_program(progs, tmp_path):
-    """Product steps with room for two lanes per product are emitted as lane pairs
-    (gen_coop.lane_entries); the table the device runs computes what the program does."""
+    """Product steps with room for two lanes per product, and combination steps with room
+    for two lanes per combination, are emitted as lane pairs (gen_coop.lane_entries); the
+    table the device runs computes what the program does."""
     pg, consts = progs
     path = tmp_path / "t.bin"
     names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul"]
     GC.emit([pg[nm] for nm in names], consts, path)
-    paired = sum(1 for nm in names for st in pg[nm].steps if any(e[1] == GC.PAIR_A for e in GC.lane_entries(st)))
-    assert paired >= 10
+    kinds = [e[1] for nm in names for st in pg[nm].steps for e in GC.lane_entries(st)]
+    assert kinds.count(GC.PAIR_A) >= 10 and kinds.count(GC.LPAIR_A) >= 1
     rng = random.Random(7)
     for nm in names:
         fr = [rng.randrange(P) for _ in range(pg[nm].n_slots)]

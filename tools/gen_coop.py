@@ -422,7 +422,8 @@ def _le_limbs(v: int) -> bytes:
     return v.to_bytes(48, "little")
 
 
-PAIR_A, PAIR_B = 3, 4  # a product on a lane pair (lodestar_amd/csrc/bls/coop.hpp coop_step)
+PAIR_A, PAIR_B = 3, 4    # a product on a lane pair (lodestar_amd/csrc/bls/coop.hpp coop_step)
+LPAIR_A, LPAIR_B = 5, 6  # a linear combination on a lane pair (half of the terms each)
 
 
 def lane_entries(step) -> list:
@@ -433,7 +434,10 @@ def lane_entries(step) -> list:
     of it.  A product step with room for two lanes per product (2 x products + linear
     combinations <= 64) therefore runs each product on an adjacent lane pair: the even
     lane (PAIR_A) gathers operand a, the odd lane (PAIR_B) operand b, the pair swaps the
-    sums (DPP) and both multiply; the even lane writes.  Other steps: one lane per op."""
+    sums (DPP) and both multiply; the even lane writes.
+    A step of combinations only, with room, likewise splits each combination's terms over
+    a lane pair (LPAIR_A: the first half and the write, LPAIR_B: the rest); the pair adds
+    its two unreduced sums before the one reduction."""
     muls = [op for op in step if op.kind == OP_MUL]
     lins = [op for op in step if op.kind != OP_MUL]
     if muls and 2 * len(muls) + len(lins) <= LANES:
@@ -442,6 +446,13 @@ def lane_entries(step) -> list:
             out.append((op.out, PAIR_A, op.a, []))
             out.append((None, PAIR_B, op.b, []))
         return out + [(op.out, op.kind, op.a, []) for op in lins]
+    if not muls and 2 * len(lins) <= LANES and max(len(op.a) for op in lins) > 2:
+        out = []
+        for op in lins:
+            h = (len(op.a) + 1) // 2
+            out.append((op.out, LPAIR_A, op.a[:h], []))
+            out.append((None, LPAIR_B, op.a[h:], []))
+        return out
     return [(op.out, op.kind, op.a, op.b if op.kind == OP_MUL else []) for op in step]
 
 
