@@ -35,7 +35,10 @@ namespace bls {
 
 struct CoopOp {  // 80 bytes, one per lane per step (tools/gen_coop.py:emit)
   uint16_t out;
-  uint8_t kind, na, nb, pad0, pad1, pad2;
+  uint8_t kind, na, nb;
+  uint8_t ma, mb, flags;  // the same on every lane of a step: largest na over the lanes that
+                          // gather a, largest nb over the unpaired products; bit 0 / 1: a / b
+                          // is one +1 term on every one of them
   uint16_t a[8];
   uint16_t b[8];
   int16_t ca[8];
@@ -210,14 +213,6 @@ __device__ __forceinline__ Fp fp_canon3(const Fp& x) {
 
 __device__ __forceinline__ bool fp_is_zero_lazy(const Fp& x) { return fp_is_zero(fp_canon3(x)); }
 
-// Wave-uniform max of n over the active lanes (n <= 8)
-__device__ __forceinline__ int coop_wave_max_terms(int n) {
-  int m = 0;
-#pragma unroll
-  for (int k = 1; k <= 8; ++k) m += __any(n >= k) ? 1 : 0;
-  return m;
-}
-
 // sum_k cf[k] * slot[refs[k]] mod p over n <= 8 terms.  refs index the block's LDS
 // slot array (frame, then the constant bank at COOP_FRAME).  Branch-free up to the
 // wave's largest n (loop bound wave-uniform; a lane's unused term has coefficient 0):
@@ -230,8 +225,7 @@ __device__ __forceinline__ int coop_wave_max_terms(int n) {
 // The unreduced sum as a 13-limb two's-complement accumulator; returns the sum of |c|
 // over the negated terms (acc_reduce's bias)
 __device__ __forceinline__ uint32_t coop_lin_acc(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n,
-                                                 const LdsU4* slots, Acc13& acc) {
-  const int nmax = coop_wave_max_terms(n);
+                                                 int nmax, const LdsU4* slots, Acc13& acc) {
   uint64_t col[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) col[i] = 0;
@@ -257,10 +251,13 @@ __device__ __forceinline__ uint32_t coop_lin_acc(const uint16_t (&refs)[8], cons
   return negs;
 }
 
-__device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n, const LdsU4* slots) {
-  if (__all(n == 1 && cf[0] == 1)) return lds_load_fp(slots, refs[0]);
+// nmax / single: the step's wave-uniform largest term count and "one +1 term on every
+// lane" (CoopOp ma / mb / flags, scalar registers)
+__device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t (&cf)[8], int n, int nmax,
+                                       bool single, const LdsU4* slots) {
+  if (single) return lds_load_fp(slots, refs[0]);
   Acc13 acc;
-  const uint32_t negs = coop_lin_acc(refs, cf, n, slots, acc);
+  const uint32_t negs = coop_lin_acc(refs, cf, n, nmax, slots, acc);
   return acc_reduce(acc, negs);
 }
 
@@ -296,6 +293,8 @@ __device__ __forceinline__ uint32_t op_word(const CoopOpRaw& u, int k) { return 
 // a[8] u16 @8 | b[8] u16 @24 | ca[8] i16 @40 | cb[8] i16 @56)
 struct CoopOpView {
   uint32_t out, kind, na, nb;
+  int ma, mb;        // wave-uniform (readfirstlane)
+  bool sa, sb;
   uint16_t a[8], b[8];
   int16_t ca[8], cb[8];
 };
@@ -307,6 +306,11 @@ __device__ __forceinline__ CoopOpView coop_decode(const CoopOpRaw& u) {
   v.kind = (w0 >> 16) & 0xffu;
   v.na = w0 >> 24;
   v.nb = w1 & 0xffu;
+  const uint32_t s1 = __builtin_amdgcn_readfirstlane(w1);  // every lane carries the same bytes 1-3
+  v.ma = (int)((s1 >> 8) & 0xffu);
+  v.mb = (int)((s1 >> 16) & 0xffu);
+  v.sa = (s1 >> 24) & 1u;
+  v.sb = (s1 >> 25) & 1u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t wa = op_word(u, 2 + k), wb = op_word(u, 6 + k), wca = op_word(u, 10 + k), wcb = op_word(u, 14 + k);
@@ -345,17 +349,17 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
     // a combination on a lane pair: each lane sums its half of the terms, the pair adds
     // the two unreduced sums (13 limbs and the negation bias), one reduction
     Acc13 acc, oth;
-    uint32_t negs = coop_lin_acc(op.a, op.ca, op.kind ? (int)op.na : 0, slots, acc);
+    uint32_t negs = coop_lin_acc(op.a, op.ca, op.kind ? (int)op.na : 0, op.ma, slots, acc);
 #pragma unroll
     for (int i = 0; i < 13; ++i) oth.l[i] = coop_pair_swap(acc.l[i]);
     negs += coop_pair_swap(negs);
     asm_acc_add13(acc.l, oth.l);
     r = acc_reduce(acc, negs);
   } else if (op.kind != 0) {
-    r = coop_lin(op.a, op.ca, op.na, slots);
+    r = coop_lin(op.a, op.ca, op.na, op.ma, op.sa, slots);
     if (TIMED && mark == 2 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
     if (op.kind == COOP_MUL) {
-      const Fp rb = coop_lin(op.b, op.cb, op.nb, slots);
+      const Fp rb = coop_lin(op.b, op.cb, op.nb, op.mb, op.sb, slots);
       if (TIMED && mark == 3 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
       r = fp_mul_lazy(r, rb);
       if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();

@@ -211,8 +211,8 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
   size_t consts_off = sizeof(h), progs_off = consts_off + (size_t)h.n_consts * sizeof(Fp);
   size_t steps_off = progs_off + (size_t)h.n_progs * sizeof(CoopProgEntry);
   size_t steps_bytes = (size_t)h.n_steps * COOP_LANES * sizeof(CoopOp);
-  // version 2: op kinds 3 / 4 (products on lane pairs, coop.hpp coop_step)
-  if (memcmp(h.magic, "BLSC", 4) != 0 || h.version != 2 || steps_off + steps_bytes != (size_t)sz) {
+  // version 3: op kinds 3-6 (lane pairs) and the per-step term bounds (coop.hpp CoopOp)
+  if (memcmp(h.magic, "BLSC", 4) != 0 || h.version != 3 || steps_off + steps_bytes != (size_t)sz) {
     snprintf(ctx->err, sizeof(ctx->err), "%s: bad coop table format", path.c_str());
     return -1;
   }

@@ -93,7 +93,13 @@ def _run_binary(path, name, frame, n_consts):
     cvals = [c * R_INV % P for c in consts]  # the bank is in Montgomery form
     flag = 0
     for s in range(first, first + n):
-        lanes = [struct.unpack_from("<HBBB3x8H8H8h8h8x", raw, off + 80 * (64 * s + ln)) for ln in range(64)]
+        lanes = [struct.unpack_from("<HBBBBBB8H8H8h8h8x", raw, off + 80 * (64 * s + ln)) for ln in range(64)]
+        # the per-step fields (max term counts, single-term flags) are what every lane says
+        ma, mb, fl = lanes[0][4:7]
+        assert all(x[4:7] == (ma, mb, fl) for x in lanes)
+        assert ma == max((x[2] for x in lanes if x[1]), default=0)
+        assert mb == max((x[3] for x in lanes if x[1] == 1), default=0)
+        lanes = [x[:4] + x[7:] for x in lanes]
 
         def lin(refs, cfs, k):
             return sum(cf * (frame[r] if r < n_slots else cvals[r - n_slots]) for r, cf in zip(refs[:k], cfs[:k])) % P

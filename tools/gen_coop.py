@@ -466,6 +466,17 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
         for step in pg.steps:
             assert len(step) <= LANES
             entries = lane_entries(step)
+            # per-step (wave-uniform) fields every lane carries: the largest term count of
+            # operand a over the lanes that gather it (every op) and of operand b (the
+            # unpaired products), and whether each is a single +1 term on all of them --
+            # the interpreter's loop bounds and fast paths without a ballot per step
+            act = [e for e in entries if e[1] != 0]
+            muls = [e for e in entries if e[1] == OP_MUL]
+            ma = max((len(e[2]) for e in act), default=0)
+            mb = max((len(e[3]) for e in muls), default=0)
+            sa = bool(act) and all(len(e[2]) == 1 and e[2][0][1] == 1 for e in act)
+            sb = bool(muls) and all(len(e[3]) == 1 and e[3][0][1] == 1 for e in muls)
+            flags = int(sa) | int(sb) << 1
             for lane in range(LANES):
                 if lane < len(entries):
                     out, kind, a, b = entries[lane]
@@ -490,11 +501,11 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                 def cfs(lst):
                     r = [cf for _, cf in lst]
                     return r + [0] * (8 - len(r))
-                steps_bin += struct.pack("<HBBB3x8H8H8h8h8x", out, kind, len(a), len(b),
+                steps_bin += struct.pack("<HBBBBBB8H8H8h8h8x", out, kind, len(a), len(b), ma, mb, flags,
                                          *refs(a), *refs(b), *cfs(a), *cfs(b))
         first += len(pg.steps)
     assert len(consts.vals) <= 40, "constant bank exceeds COOP_MAX_CONSTS"
-    header = struct.pack("<4sIIII", b"BLSC", 2, len(consts.vals), len(progs), first)
+    header = struct.pack("<4sIIII", b"BLSC", 3, len(consts.vals), len(progs), first)
     cbin = b"".join(_le_limbs(v * MONT_R % P) for v in consts.vals)
     path.write_bytes(header + cbin + bytes(table) + bytes(steps_bin))
 
