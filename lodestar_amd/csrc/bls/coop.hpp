@@ -86,6 +86,7 @@ struct CoopEnv {
   CoopProg fin_fmul, fin_fe1, fin_fe2;
   // per-set frame (tools/gen_pset.py, kernels/k_pset.hip; the r chains run beside them)
   CoopProg pset_prep, pset_dbl_all, pset_add_x, pset_phase2, pset_norm2, pset_affine2, pset_ml2;
+  CoopProg pset_ml2_w2;  // pset_ml2 laid out for two wavefronts (k_pset: every product on a lane pair)
   CoopPsetN packed[2];  // [0]: 2 sets per wavefront, [1]: 3 sets
   // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln, the
   // cooperative packings tests force): 1 or 2 sets per wavefront (COOP_FRAME)
@@ -230,10 +231,13 @@ __device__ __forceinline__ uint32_t coop_lin_acc(const uint16_t (&refs)[8], cons
 #pragma unroll
   for (int i = 0; i < 12; ++i) col[i] = 0;
   uint32_t negs = 0;  // sum of |c| over the negated terms
+  // (terms past a lane's n have coefficient 0 and slot 0 in the table: no masking; the
+  // next term's LDS reads issued before this term's multiply-adds measured slower,
+  // profiles/r05_ab_coop_prefetch.json)
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     if (k >= nmax) break;
-    const int c = k < n ? cf[k] : 0;
+    const int c = cf[k];
     const uint32_t mask = c < 0 ? 0xffffffffu : 0u;
     const uint32_t m = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
     negs += mask & m;
@@ -339,7 +343,15 @@ __device__ __forceinline__ void coop_wave_sync() {
 // TIMED (the probe, bls_gpu_coop_probe): lane 0 stamps s_memtime at the point `mark`
 // names -- 0: compute done (before the fence), 1: op decoded, 2: operand a summed,
 // 3: operand b summed (product steps), 4: product done.
-template <bool TIMED>
+// W wavefronts per task (a block of 64 W lanes, program steps of 64 W ops): the step
+// boundaries are block barriers then
+template <int W>
+__device__ __forceinline__ void coop_task_sync() {
+  if (W == 1) coop_wave_sync();
+  else __syncthreads();
+}
+
+template <bool TIMED, int W = 1>
 __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, uint32_t* flag, uint64_t* stamp,
                                           uint32_t mark = 0) {
   const CoopOpView op = coop_decode(raw);
@@ -377,7 +389,7 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
     if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   }
   if (TIMED && mark == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
-  coop_wave_sync();
+  coop_task_sync<W>();
   if (op.kind != 0 && op.kind != COOP_PAIR_B && op.kind != COOP_LPAIR_B) {
     if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
       if (fp_is_zero_lazy(r)) atomicOr(flag, op.out == COOP_OUT_ZCHECK ? 1u : 1u << (op.out - COOP_OUT_ZSET));
@@ -385,14 +397,16 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
       lds_store_fp(slots, op.out, r);
     }
   }
-  coop_wave_sync();
+  coop_task_sync<W>();
 }
 
 // Run one program on this block's frame.  cbank: the constant bank staged in LDS
 // (coop_stage_consts).  *flag (LDS) is set when a zero-check op sees zero.  Two op
 // buffers alternate: step s computes from one while step s + 1's ops load into the
 // other.
-template <bool TIMED>
+// W: wavefronts per task; a W-wavefront program's step is W consecutive 64-op records
+// (tools/gen_coop.py emit, programs named *_w2), lane threadIdx.x reads op threadIdx.x
+template <bool TIMED, int W = 1>
 __device__ __forceinline__ void coop_run_body(const CoopEnv& env, CoopProg pg, Fp* frame, uint32_t* flag,
                                               uint64_t* stamps) {
   const int lane = threadIdx.x;
@@ -401,17 +415,17 @@ __device__ __forceinline__ void coop_run_body(const CoopEnv& env, CoopProg pg, F
   LdsU4* slots = (LdsU4*)frame;
   CoopOpRaw A, B;
   const uint32_t mark = TIMED && stamps ? (uint32_t)stamps[0] : 0u;  // the probe's stamp point
-  const uint32_t last = pg.first + pg.n - 1;
+  const uint32_t last = pg.first + W * (pg.n - 1);
   coop_fetch(A, base, pg.first, lane);
   for (uint32_t s = 0; s < pg.n; s += 2) {
-    const uint32_t g = pg.first + s;
+    const uint32_t g = pg.first + W * s;
     if (TIMED && lane == 0) stamps[2 * s] = __builtin_amdgcn_s_memtime();
-    coop_fetch(B, base, g + 1 <= last ? g + 1 : last, lane);
-    coop_step<TIMED>(A, slots, flag, stamps ? stamps + 2 * s + 1 : nullptr, mark);
+    coop_fetch(B, base, g + W <= last ? g + W : last, lane);
+    coop_step<TIMED, W>(A, slots, flag, stamps ? stamps + 2 * s + 1 : nullptr, mark);
     if (s + 1 >= pg.n) break;
     if (TIMED && lane == 0) stamps[2 * s + 2] = __builtin_amdgcn_s_memtime();
-    coop_fetch(A, base, g + 2 <= last ? g + 2 : last, lane);
-    coop_step<TIMED>(B, slots, flag, stamps ? stamps + 2 * s + 3 : nullptr, mark);
+    coop_fetch(A, base, g + 2 * W <= last ? g + 2 * W : last, lane);
+    coop_step<TIMED, W>(B, slots, flag, stamps ? stamps + 2 * s + 3 : nullptr, mark);
   }
   if (TIMED && lane == 0) stamps[2 * pg.n] = __builtin_amdgcn_s_memtime();
 }
@@ -427,6 +441,11 @@ __device__ __noinline__ void coop_run_t(const CoopEnv& env, CoopProg pg, Fp* fra
 __device__ __forceinline__ void coop_run(const CoopEnv& env, CoopProg pg, Fp* frame, const Fp* cbank,
                                          uint32_t* flag) {
   coop_run_t<false>(env, pg, frame, cbank, flag, nullptr);
+}
+
+// a two-wavefront program (both wavefronts of the block call it)
+__device__ __noinline__ void coop_run2_t(const CoopEnv& env, CoopProg pg, Fp* frame, uint32_t* flag) {
+  coop_run_body<false, 2>(env, pg, frame, flag, nullptr);
 }
 
 // copy the constant bank into LDS (once per block)

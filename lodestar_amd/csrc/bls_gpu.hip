@@ -239,7 +239,8 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
               {"pset_dbl_all", &ctx->coop.pset_dbl_all}, {"pset_add_x", &ctx->coop.pset_add_x},
               {"pset_phase2", &ctx->coop.pset_phase2},
               {"pset_norm2", &ctx->coop.pset_norm2},     {"pset_affine2", &ctx->coop.pset_affine2},
-              {"pset_ml2", &ctx->coop.pset_ml2},         {"ml1_1", &ctx->coop.ml1_1},
+              {"pset_ml2", &ctx->coop.pset_ml2},         {"pset_ml2_w2", &ctx->coop.pset_ml2_w2},
+              {"ml1_1", &ctx->coop.ml1_1},
               {"ml1_2", &ctx->coop.ml1_2}};
   ctx->coop_progs = new std::vector<std::pair<std::string, CoopProg>>();
   for (uint32_t k = 0; k < h.n_progs; ++k) {

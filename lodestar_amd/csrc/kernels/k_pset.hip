@@ -54,11 +54,19 @@ __device__ __forceinline__ void pset_flag(const PipeBufs& b, uint32_t i) {
   atomicAdd(b.flag_count, 1u);
 }
 
-__global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, const CoopEnv* __restrict__ envp) {
+// Two wavefronts per set: wavefront 0 runs every program up to the Miller loop (their
+// steps fit one wavefront with each product and combination on a lane pair, coop.hpp
+// coop_step); both run the Miller loop, whose steps carry ~48 products -- 96 lanes as
+// pairs (pset_ml2_w2, tools/gen_coop.py).  Every branch between the block barriers below
+// reads block-uniform values (the set's status in global memory, the LDS flag and frame
+// after a barrier), so both wavefronts take it.
+#define PSET_WAVES 2
+__global__ __launch_bounds__(PSET_WAVES * COOP_LANES) void k_pset(PipeBufs b, const CoopEnv* __restrict__ envp) {
   const CoopEnv& env = *envp;
   __shared__ PsetShared sh;
   const uint32_t i = blockIdx.x;
   const int lane = threadIdx.x;
+  const bool w0 = lane < COOP_LANES;
   if (b.pk_status[i] != BLS_OK || b.sig_status[i] != BLS_OK || jac_is_inf(b.pk[i])) {
     pset_store_one(&b.f[i]);  // the request errors on its status; f_i is unused
     return;
@@ -77,12 +85,15 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, const CoopEnv* 
   if (lane == 0) sh.flag = 0;
   __syncthreads();
 
-  coop_run(env, env.pset_prep, sh.frame, sh.cbank, &sh.flag);
-  for (int k = 62; k >= 0; --k) {
-    coop_run(env, env.pset_dbl_all, sh.frame, sh.cbank, &sh.flag);
-    if ((PS_X_ABS >> k) & 1ull) coop_run(env, env.pset_add_x, sh.frame, sh.cbank, &sh.flag);
+  if (w0) {
+    coop_run(env, env.pset_prep, sh.frame, sh.cbank, &sh.flag);
+    for (int k = 62; k >= 0; --k) {
+      coop_run(env, env.pset_dbl_all, sh.frame, sh.cbank, &sh.flag);
+      if ((PS_X_ABS >> k) & 1ull) coop_run(env, env.pset_add_x, sh.frame, sh.cbank, &sh.flag);
+    }
+    coop_run(env, env.pset_phase2, sh.frame, sh.cbank, &sh.flag);
   }
-  coop_run(env, env.pset_phase2, sh.frame, sh.cbank, &sh.flag);
+  __syncthreads();
   if (sh.flag) {
     if (lane == 0) pset_flag(b, i);
     return;
@@ -92,14 +103,18 @@ __global__ __launch_bounds__(COOP_LANES) void k_pset(PipeBufs b, const CoopEnv* 
     pset_store_one(&b.f[i]);
     return;
   }
-  coop_run(env, env.pset_norm2, sh.frame, sh.cbank, &sh.flag);
+  if (w0) coop_run(env, env.pset_norm2, sh.frame, sh.cbank, &sh.flag);
+  __syncthreads();
   if (sh.flag) {
     if (lane == 0) pset_flag(b, i);
     return;
   }
-  coop_invert(sh.frame, PS_INV_IN, PS_INV_OUT);
-  coop_run(env, env.pset_affine2, sh.frame, sh.cbank, &sh.flag);
-  coop_run(env, env.pset_ml2, sh.frame, sh.cbank, &sh.flag);
+  if (w0) {
+    coop_invert(sh.frame, PS_INV_IN, PS_INV_OUT);
+    coop_run(env, env.pset_affine2, sh.frame, sh.cbank, &sh.flag);
+  }
+  __syncthreads();
+  coop_run2_t(env, env.pset_ml2_w2, sh.frame, &sh.flag);
   if (lane < 12) reinterpret_cast<Fp*>(&b.f[i])[lane] = coop_get(sh.frame, PS_F + lane);
 }
 
@@ -310,7 +325,7 @@ hipError_t launch_k_pset(const PipeBufs& b, const CoopEnv& env, hipStream_t s) {
   } else if (S == 2 && env.packed[0].ml2.n > 0) {
     k_psetn<2, COOP_FRAME2><<<(b.n_sets + 1) / 2, COOP_LANES, 0, s>>>(b, env.dev);
   } else {
-    k_pset<<<b.n_sets, COOP_LANES, 0, s>>>(b, env.dev);
+    k_pset<<<b.n_sets, PSET_WAVES * COOP_LANES, 0, s>>>(b, env.dev);
   }
   return hipGetLastError();
 }

@@ -89,11 +89,13 @@ def _run_binary(path, name, frame, n_consts):
         table[nm] = struct.unpack_from("<IIII", raw, off + 32)
         off += 48
     first, n, n_slots, _ = table[name]
+    L = 128 if name.endswith("_w2") else 64  # two-wavefront programs: steps of 128 ops
     R_INV = pow(1 << 384, -1, P)
     cvals = [c * R_INV % P for c in consts]  # the bank is in Montgomery form
     flag = 0
-    for s in range(first, first + n):
-        lanes = [struct.unpack_from("<HBBBBBB8H8H8h8h8x", raw, off + 80 * (64 * s + ln)) for ln in range(64)]
+    for s in range(n):
+        rec = first + s * (L // 64)
+        lanes = [struct.unpack_from("<HBBBBBB8H8H8h8h8x", raw, off + 80 * (64 * rec + ln)) for ln in range(L)]
         # the per-step fields (max term counts, single-term flags) are what every lane says
         ma, mb, fl = lanes[0][4:7]
         assert all(x[4:7] == (ma, mb, fl) for x in lanes)
@@ -134,9 +136,9 @@ def test_emitted_lane_pairs_match_program(progs, tmp_path):
     table the device runs computes what the program does."""
     pg, consts = progs
     path = tmp_path / "t.bin"
-    names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul"]
+    names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul", "pset_ml2_w2"]
     GC.emit([pg[nm] for nm in names], consts, path)
-    kinds = [e[1] for nm in names for st in pg[nm].steps for e in GC.lane_entries(st)]
+    kinds = [e[1] for nm in names for st in pg[nm].steps for e in GC.lane_entries(st, getattr(pg[nm], "lanes", 64))]
     assert kinds.count(GC.PAIR_A) >= 10 and kinds.count(GC.LPAIR_A) >= 1
     rng = random.Random(7)
     for nm in names:

@@ -426,7 +426,7 @@ PAIR_A, PAIR_B = 3, 4    # a product on a lane pair (lodestar_amd/csrc/bls/coop.
 LPAIR_A, LPAIR_B = 5, 6  # a linear combination on a lane pair (half of the terms each)
 
 
-def lane_entries(step) -> list:
+def lane_entries(step, lanes: int = LANES) -> list:
     """A step's lane entries (out, kind, a, b); out None = the lane writes nothing.
 
     The interpreter runs one wavefront per task, so a step's time is one lane's
@@ -440,13 +440,13 @@ def lane_entries(step) -> list:
     its two unreduced sums before the one reduction."""
     muls = [op for op in step if op.kind == OP_MUL]
     lins = [op for op in step if op.kind != OP_MUL]
-    if muls and 2 * len(muls) + len(lins) <= LANES:
+    if muls and 2 * len(muls) + len(lins) <= lanes:
         out = []
         for op in muls:
             out.append((op.out, PAIR_A, op.a, []))
             out.append((None, PAIR_B, op.b, []))
         return out + [(op.out, op.kind, op.a, []) for op in lins]
-    if not muls and 2 * len(lins) <= LANES and max(len(op.a) for op in lins) > 2:
+    if not muls and 2 * len(lins) <= lanes and max(len(op.a) for op in lins) > 2:
         out = []
         for op in lins:
             h = (len(op.a) + 1) // 2
@@ -463,9 +463,10 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
     for pg in progs:
         name = pg.name.encode()[:31].ljust(32, b"\0")
         table += name + struct.pack("<IIII", first, len(pg.steps), pg.n_slots, pg.n_mul_steps)
+        L = getattr(pg, "lanes", LANES)  # 64 per wavefront the program runs on
         for step in pg.steps:
-            assert len(step) <= LANES
-            entries = lane_entries(step)
+            assert len(step) <= L
+            entries = lane_entries(step, L)
             # per-step (wave-uniform) fields every lane carries: the largest term count of
             # operand a over the lanes that gather it (every op) and of operand b (the
             # unpaired products), and whether each is a single +1 term on all of them --
@@ -477,7 +478,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
             sa = bool(act) and all(len(e[2]) == 1 and e[2][0][1] == 1 for e in act)
             sb = bool(muls) and all(len(e[3]) == 1 and e[3][0][1] == 1 for e in muls)
             flags = int(sa) | int(sb) << 1
-            for lane in range(LANES):
+            for lane in range(L):
                 if lane < len(entries):
                     out, kind, a, b = entries[lane]
                     # zero-checks: 0xFFFF for set 0, 0xFFF0 + s for packed set s >= 1
@@ -503,7 +504,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                     return r + [0] * (8 - len(r))
                 steps_bin += struct.pack("<HBBBBBB8H8H8h8h8x", out, kind, len(a), len(b), ma, mb, flags,
                                          *refs(a), *refs(b), *cfs(a), *cfs(b))
-        first += len(pg.steps)
+        first += len(pg.steps) * (L // LANES)
     assert len(consts.vals) <= 40, "constant bank exceeds COOP_MAX_CONSTS"
     header = struct.pack("<4sIIII", b"BLSC", 3, len(consts.vals), len(progs), first)
     cbin = b"".join(_le_limbs(v * MONT_R % P) for v in consts.vals)
@@ -534,6 +535,13 @@ def build_all():
     # per wavefront in the 256-slot frame
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=2))
+    # the one-set Miller loop laid out for two wavefronts (kernels/k_pset.hip): the same
+    # steps, 128 lanes each, so every product finds a lane pair
+    import copy
+    ml2 = next(p for p in progs if p.name == "pset_ml2")
+    w2 = copy.copy(ml2)
+    w2.name, w2.lanes = "pset_ml2_w2", 2 * LANES
+    progs.append(w2)
     return progs, consts
 
 
