@@ -546,25 +546,29 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
         # committee roots), calls of 1024 batchable single-set requests on the headline's
         # contexts, invalid sets included (their passes fail the merged check and run the
         # chunk and per-request fallback inside the timed region)
-        w5 = W.cfg5_slice(ctxs[0], n_keys, cfg5_sets, cfg5_roots, invalid=max(1, cfg5_sets // 2048))
-        pbs = W.packed_calls(w5)
-        cpp5 = (len(pbs) + n_ctx - 1) // n_ctx
-        run_calls(ctxs, pbs[: n_ctx], 1)  # warm-up
-        best, out, tot = None, None, None
-        for _ in range(reps):
-            el, out, tot = run_calls(ctxs, pbs, cpp5)
-            best = el if best is None else min(best, el)
-        bad = [k for k in range(len(pbs)) if not W.verdicts_ok(w5, k, out[k])]
-        assert not bad, f"cfg5_slice: {len(bad)} calls with wrong verdicts (first {bad[0]})"
-        res["cfg5_slice"] = {"workload": w5.note, "sets": w5.n_sets, "calls": len(pbs),
-                             "invalid_sets": sum(not x for v in w5.valid for x in v),
-                             "false_requests": sum(int((o == 0).sum()) for o in out),
-                             "elapsed_s": round(best, 4), "sets_per_s": round(w5.n_sets / best, 1),
-                             "contexts": n_ctx, "calls_per_pass": cpp5, "runs": reps,
-                             "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
-                             "passes_merged_check_failed": tot["merged_fail"],
-                             "verdicts": "every call matches the sets' validity by construction",
-                             **steady_state(ctxs, w5, pbs, cpp5, jobs)}
+        # and the same epoch slice with every set valid (cfg5_slice_valid): the shape's own
+        # rate -- with 1 invalid set in 2,048 about half of the 1024-set calls fail their
+        # merged check and re-verify a chunk's 16 requests alone
+        for key, n_invalid in (("cfg5_slice", max(1, cfg5_sets // 2048)), ("cfg5_slice_valid", 0)):
+            w5 = W.cfg5_slice(ctxs[0], n_keys, cfg5_sets, cfg5_roots, invalid=n_invalid)
+            pbs = W.packed_calls(w5)
+            cpp5 = (len(pbs) + n_ctx - 1) // n_ctx
+            run_calls(ctxs, pbs[: n_ctx], 1)  # warm-up
+            best, out, tot = None, None, None
+            for _ in range(reps):
+                el, out, tot = run_calls(ctxs, pbs, cpp5)
+                best = el if best is None else min(best, el)
+            bad = [k for k in range(len(pbs)) if not W.verdicts_ok(w5, k, out[k])]
+            assert not bad, f"{key}: {len(bad)} calls with wrong verdicts (first {bad[0]})"
+            res[key] = {"workload": w5.note, "sets": w5.n_sets, "calls": len(pbs),
+                        "invalid_sets": sum(not x for v in w5.valid for x in v),
+                        "false_requests": sum(int((o == 0).sum()) for o in out),
+                        "elapsed_s": round(best, 4), "sets_per_s": round(w5.n_sets / best, 1),
+                        "contexts": n_ctx, "calls_per_pass": cpp5, "runs": reps,
+                        "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
+                        "passes_merged_check_failed": tot["merged_fail"],
+                        "verdicts": "every call matches the sets' validity by construction",
+                        **steady_state(ctxs, w5, pbs, cpp5, jobs)}
     finally:
         for c in ctxs:
             c.close()
