@@ -25,20 +25,21 @@ namespace bls {
 #define COOP_OUT_NONE 0xFFFEu   // lane idle (kind 0, never written)
 #define COOP_OUT_ZSET 0xFFF0u   // zero-check of packed set s >= 1: 0xFFF0 + s
 #define COOP_MAX_CONSTS 40  // constants staged per block (tools/gen_coop.py asserts the bank fits)
-// op kinds (tools/gen_coop.py emit): 0 idle, 1 product of two combinations, 2 combination,
-// 3 / 4 one product on a lane pair (even lane: operand a and the write, odd lane: operand b),
+// op kinds (tools/gen_coop.py emit, lane_entries): 0 idle, 1 product of two combinations,
+// 2 combination (or its part in a lane group), 3 / 4 part of a product's operand a / b in
+// a lane group
 #define COOP_MUL 1u
-#define COOP_PAIR_A 3u
-#define COOP_PAIR_B 4u
-#define COOP_LPAIR_A 5u  // 5 / 6: one combination on a lane pair (even lane: the first half of the
-#define COOP_LPAIR_B 6u  // terms and the write, odd lane: the rest)
+#define COOP_LIN 2u
+#define COOP_GRP_A 3u
+#define COOP_GRP_B 4u
 
 struct CoopOp {  // 80 bytes, one per lane per step (tools/gen_coop.py:emit)
   uint16_t out;
   uint8_t kind, na, nb;
   uint8_t ma, mb, flags;  // the same on every lane of a step: largest na over the lanes that
-                          // gather a, largest nb over the unpaired products; bit 0 / 1: a / b
-                          // is one +1 term on every one of them
+                          // gather a, largest nb over the ungrouped products; bit 0 / 1: a / b
+                          // is one +1 term on every one of them; bits 2-3 / 4-5: log2 of the
+                          // lane-group size of the step's products / combinations
   uint16_t a[8];
   uint16_t b[8];
   int16_t ca[8];
@@ -265,9 +266,13 @@ __device__ __forceinline__ Fp coop_lin(const uint16_t (&refs)[8], const int16_t 
   return acc_reduce(acc, negs);
 }
 
-// the value of lane ^ 1 (DPP quad_perm [1,0,3,2]; every lane of the wave must take part)
+// the value of lane ^ 1 / lane ^ 2 (DPP quad_perm [1,0,3,2] / [2,3,0,1]; every lane of the
+// wave must take part)
 __device__ __forceinline__ uint32_t coop_pair_swap(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t coop_half_swap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
 }
 
 // One lane's op of one step as fetched: the 80-byte CoopOp as 20 raw dwords, loaded
@@ -299,6 +304,7 @@ struct CoopOpView {
   uint32_t out, kind, na, nb;
   int ma, mb;        // wave-uniform (readfirstlane)
   bool sa, sb;
+  int lgp, lgl;      // log2 of the product / combination lane-group sizes (wave-uniform)
   uint16_t a[8], b[8];
   int16_t ca[8], cb[8];
 };
@@ -315,6 +321,8 @@ __device__ __forceinline__ CoopOpView coop_decode(const CoopOpRaw& u) {
   v.mb = (int)((s1 >> 16) & 0xffu);
   v.sa = (s1 >> 24) & 1u;
   v.sb = (s1 >> 25) & 1u;
+  v.lgp = (int)((s1 >> 26) & 3u);
+  v.lgl = (int)((s1 >> 28) & 3u);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t wa = op_word(u, 2 + k), wb = op_word(u, 6 + k), wca = op_word(u, 10 + k), wcb = op_word(u, 14 + k);
@@ -357,40 +365,65 @@ __device__ __forceinline__ void coop_step(const CoopOpRaw& raw, LdsU4* slots, ui
   const CoopOpView op = coop_decode(raw);
   if (TIMED && mark == 1 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   Fp r = fp_zero();
-  if (__any(op.kind >= COOP_LPAIR_A)) {
-    // a combination on a lane pair: each lane sums its half of the terms, the pair adds
-    // the two unreduced sums (13 limbs and the negation bias), one reduction
+  if (op.lgp == 0 && op.lgl == 0) {  // one lane per op
+    if (op.kind != 0) {
+      r = coop_lin(op.a, op.ca, op.na, op.ma, op.sa, slots);
+      if (TIMED && mark == 2 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+      if (op.kind == COOP_MUL) {
+        const Fp rb = coop_lin(op.b, op.cb, op.nb, op.mb, op.sb, slots);
+        if (TIMED && mark == 3 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+        r = fp_mul_lazy(r, rb);
+        if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+      }
+    }
+  } else {
+    // lane groups (tools/gen_coop.py lane_entries): every lane sums its part of its
+    // operand unreduced; the parts of one operand are added by DPP butterflies (lanes
+    // ^1, then ^2, within the aligned group: a combination's whole group, a product
+    // operand's half of its group); one reduction; a product group's halves then swap
+    // their operands and every lane of it multiplies (the product is symmetric)
+    const bool grp = op.kind == COOP_GRP_A || op.kind == COOP_GRP_B;
+    const int lv = grp ? op.lgp - 1 : (op.kind == COOP_LIN ? op.lgl : 0);
+    const int levels = op.lgp - 1 > op.lgl ? op.lgp - 1 : op.lgl;
     Acc13 acc, oth;
     uint32_t negs = coop_lin_acc(op.a, op.ca, op.kind ? (int)op.na : 0, op.ma, slots, acc);
+    if (levels > 0) {
 #pragma unroll
-    for (int i = 0; i < 13; ++i) oth.l[i] = coop_pair_swap(acc.l[i]);
-    negs += coop_pair_swap(negs);
-    asm_acc_add13(acc.l, oth.l);
-    r = acc_reduce(acc, negs);
-  } else if (op.kind != 0) {
-    r = coop_lin(op.a, op.ca, op.na, op.ma, op.sa, slots);
-    if (TIMED && mark == 2 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
-    if (op.kind == COOP_MUL) {
-      const Fp rb = coop_lin(op.b, op.cb, op.nb, op.mb, op.sb, slots);
-      if (TIMED && mark == 3 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
-      r = fp_mul_lazy(r, rb);
-      if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+      for (int i = 0; i < 13; ++i) oth.l[i] = coop_pair_swap(acc.l[i]);
+      const uint32_t on = coop_pair_swap(negs);
+      if (lv > 0) {
+        asm_acc_add13(acc.l, oth.l);
+        negs += on;
+      }
     }
-  }
-  // a product on a lane pair (tools/gen_coop.py lane_entries): each lane gathered one
-  // operand; swap them with the neighbour (DPP quad_perm [1,0,3,2], every lane of the
-  // wave takes part) and both multiply -- the product is symmetric
-  const bool pair = op.kind == COOP_PAIR_A || op.kind == COOP_PAIR_B;
-  if (__any(pair)) {
-    Fp o;
+    if (levels > 1) {
 #pragma unroll
-    for (int i = 0; i < 12; ++i) o.l[i] = coop_pair_swap(r.l[i]);
-    if (pair) r = fp_mul_lazy(r, o);
+      for (int i = 0; i < 13; ++i) oth.l[i] = coop_half_swap(acc.l[i]);
+      const uint32_t on = coop_half_swap(negs);
+      if (lv > 1) {
+        asm_acc_add13(acc.l, oth.l);
+        negs += on;
+      }
+    }
+    r = acc_reduce(acc, negs);
+    if (TIMED && mark == 2 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
+    if (op.kind == COOP_MUL) r = fp_mul_lazy(r, coop_lin(op.b, op.cb, op.nb, op.mb, op.sb, slots));
+    if (op.lgp > 0) {
+      Fp o;
+      if (op.lgp == 1) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) o.l[i] = coop_pair_swap(r.l[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) o.l[i] = coop_half_swap(r.l[i]);
+      }
+      if (grp) r = fp_mul_lazy(r, o);
+    }
     if (TIMED && mark == 4 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   }
   if (TIMED && mark == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memtime();
   coop_task_sync<W>();
-  if (op.kind != 0 && op.kind != COOP_PAIR_B && op.kind != COOP_LPAIR_B) {
+  if (op.kind != 0 && op.out != COOP_OUT_NONE) {  // (a group writes from its first lane)
     if (op.out >= COOP_OUT_ZSET) {  // zero-check: bit 0 (0xFFFF) or bit s of packed set s (0xFFF0 + s)
       if (fp_is_zero_lazy(r)) atomicOr(flag, op.out == COOP_OUT_ZCHECK ? 1u : 1u << (op.out - COOP_OUT_ZSET));
     } else {

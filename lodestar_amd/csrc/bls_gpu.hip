@@ -211,8 +211,9 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
   size_t consts_off = sizeof(h), progs_off = consts_off + (size_t)h.n_consts * sizeof(Fp);
   size_t steps_off = progs_off + (size_t)h.n_progs * sizeof(CoopProgEntry);
   size_t steps_bytes = (size_t)h.n_steps * COOP_LANES * sizeof(CoopOp);
-  // version 3: op kinds 3-6 (lane pairs) and the per-step term bounds (coop.hpp CoopOp)
-  if (memcmp(h.magic, "BLSC", 4) != 0 || h.version != 3 || steps_off + steps_bytes != (size_t)sz) {
+  // version 4: lane groups (op kinds 3 / 4, group sizes in the step flags) and the
+  // per-step term bounds (coop.hpp CoopOp)
+  if (memcmp(h.magic, "BLSC", 4) != 0 || h.version != 4 || steps_off + steps_bytes != (size_t)sz) {
     snprintf(ctx->err, sizeof(ctx->err), "%s: bad coop table format", path.c_str());
     return -1;
   }

@@ -73,9 +73,10 @@ def test_fin_final_exponentiation(progs, oracle):
 
 def _run_binary(path, name, frame, n_consts):
     """The emitted op table (gen_coop.emit) interpreted with coop.hpp coop_step's
-    semantics, lane by lane: kinds 1 (product), 2 (combination), 3 / 4 (a product on a
-    lane pair: each lane sums one operand, the pair swaps, the even lane writes), 5 / 6 (a
-    combination on a lane pair: each lane sums half of the terms)."""
+    semantics, lane by lane: kinds 1 (product), 2 (combination, or its part in a lane
+    group of the step's combination group size gl), 3 / 4 (part of a product's operand a
+    / b in a lane group of size gp: each half of the group sums one operand, every lane
+    multiplies), the group's first lane writes."""
     import struct
 
     raw = Path(path).read_bytes()
@@ -96,11 +97,12 @@ def _run_binary(path, name, frame, n_consts):
     for s in range(n):
         rec = first + s * (L // 64)
         lanes = [struct.unpack_from("<HBBBBBB8H8H8h8h8x", raw, off + 80 * (64 * rec + ln)) for ln in range(L)]
-        # the per-step fields (max term counts, single-term flags) are what every lane says
+        # the per-step fields (max term counts, flags) are what every lane says
         ma, mb, fl = lanes[0][4:7]
         assert all(x[4:7] == (ma, mb, fl) for x in lanes)
         assert ma == max((x[2] for x in lanes if x[1]), default=0)
         assert mb == max((x[3] for x in lanes if x[1] == 1), default=0)
+        gp, gl = 1 << ((fl >> 2) & 3), 1 << ((fl >> 4) & 3)
         lanes = [x[:4] + x[7:] for x in lanes]
 
         def lin(refs, cfs, k):
@@ -115,12 +117,16 @@ def _run_binary(path, name, frame, n_consts):
             vals.append(v)
         res = list(vals)
         for ln, (out, kind, *_r) in enumerate(lanes):
-            if kind in (3, 4):
-                res[ln] = vals[ln] * vals[ln ^ 1] % P
-            elif kind in (5, 6):
-                res[ln] = (vals[ln] + vals[ln ^ 1]) % P
+            if kind == 2 and gl > 1:
+                base = ln & ~(gl - 1)
+                assert all(lanes[base + k][1] == 2 for k in range(gl) if lanes[base + k][1])
+                res[ln] = sum(vals[base: base + gl]) % P
+            elif kind in (3, 4):
+                base, h = ln & ~(gp - 1), gp // 2
+                assert [lanes[base + k][1] for k in range(gp)] == [3] * h + [4] * h
+                res[ln] = sum(vals[base: base + h]) * sum(vals[base + h: base + gp]) % P
         for ln, (out, kind, *_r) in enumerate(lanes):
-            if kind in (0, 4, 6):
+            if kind == 0 or out == 0xFFFE:
                 continue
             if out >= 0xFFF0:
                 if res[ln] == 0:
@@ -130,16 +136,17 @@ def _run_binary(path, name, frame, n_consts):
     return flag
 
 
-def test_emitted_lane_pairs_match_program(progs, tmp_path):
-    """Product steps with room for two lanes per product, and combination steps with room
-    for two lanes per combination, are emitted as lane pairs (gen_coop.lane_entries); the
-    table the device runs computes what the program does."""
+def test_emitted_lane_groups_match_program(progs, tmp_path):
+    """Steps with spare lanes spread their products and combinations over lane groups of
+    2 or 4 (gen_coop.lane_entries); the table the device runs computes what the program
+    does."""
     pg, consts = progs
     path = tmp_path / "t.bin"
-    names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul", "pset_ml2_w2"]
+    names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul", "pset_norm2", "pset_ml2_w2"]
     GC.emit([pg[nm] for nm in names], consts, path)
-    kinds = [e[1] for nm in names for st in pg[nm].steps for e in GC.lane_entries(st, getattr(pg[nm], "lanes", 64))]
-    assert kinds.count(GC.PAIR_A) >= 10 and kinds.count(GC.LPAIR_A) >= 1
+    sizes = [GC.lane_entries(st, getattr(pg[nm], "lanes", 64))[1:] for nm in names for st in pg[nm].steps]
+    assert sum(gp == 2 for gp, _ in sizes) >= 10 and sum(gp == 4 for gp, _ in sizes) >= 3
+    assert sum(gl == 4 for _, gl in sizes) >= 5
     rng = random.Random(7)
     for nm in names:
         fr = [rng.randrange(P) for _ in range(pg[nm].n_slots)]

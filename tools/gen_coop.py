@@ -422,38 +422,56 @@ def _le_limbs(v: int) -> bytes:
     return v.to_bytes(48, "little")
 
 
-PAIR_A, PAIR_B = 3, 4    # a product on a lane pair (lodestar_amd/csrc/bls/coop.hpp coop_step)
-LPAIR_A, LPAIR_B = 5, 6  # a linear combination on a lane pair (half of the terms each)
+GRP_A, GRP_B = 3, 4  # lanes of a product spread over a group (coop.hpp coop_step)
 
 
-def lane_entries(step, lanes: int = LANES) -> list:
-    """A step's lane entries (out, kind, a, b); out None = the lane writes nothing.
+def _split(terms, k):
+    """terms in k consecutive parts (the first ones one longer)"""
+    q, r = divmod(len(terms), k)
+    out, at = [], 0
+    for i in range(k):
+        n = q + (1 if i < r else 0)
+        out.append(terms[at: at + n])
+        at += n
+    return out
 
-    The interpreter runs one wavefront per task, so a step's time is one lane's
-    instruction stream, and in a product step the two operand gathers are more than half
-    of it.  A product step with room for two lanes per product (2 x products + linear
-    combinations <= 64) therefore runs each product on an adjacent lane pair: the even
-    lane (PAIR_A) gathers operand a, the odd lane (PAIR_B) operand b, the pair swaps the
-    sums (DPP) and both multiply; the even lane writes.
-    A step of combinations only, with room, likewise splits each combination's terms over
-    a lane pair (LPAIR_A: the first half and the write, LPAIR_B: the rest); the pair adds
-    its two unreduced sums before the one reduction."""
+
+def lane_entries(step, lanes: int = LANES):
+    """A step's lane entries (out, kind, a, b) -- out None: the lane writes nothing -- and
+    the step's group sizes (gp, gl) for its products and its combinations.
+
+    The interpreter runs one wavefront per task (two for k_pset's Miller loop), alone on
+    its SIMD, so a step's time is one lane's instruction stream, and the operand gathers
+    are the larger part of it.  A step with spare lanes therefore spreads its ops over
+    aligned lane groups: a product over gp = 2 or 4 lanes (the first half gathers operand
+    a -- GRP_A, split over gp / 2 lanes --, the second half operand b -- GRP_B --; each half
+    adds its partial sums by DPP, the halves swap the reduced operands and every lane
+    multiplies; the group's first lane writes), a combination over gl = 2 or 4 lanes (its
+    terms split, the partial sums added by DPP, the first lane writes).  gp is the largest
+    of 4, 2, 1 with gp x products + combinations <= lanes, then gl the largest with
+    gp x products + gl x combinations <= lanes (one lane per op when neither fits)."""
     muls = [op for op in step if op.kind == OP_MUL]
     lins = [op for op in step if op.kind != OP_MUL]
-    if muls and 2 * len(muls) + len(lins) <= lanes:
-        out = []
-        for op in muls:
-            out.append((op.out, PAIR_A, op.a, []))
-            out.append((None, PAIR_B, op.b, []))
-        return out + [(op.out, op.kind, op.a, []) for op in lins]
-    if not muls and 2 * len(lins) <= lanes and max(len(op.a) for op in lins) > 2:
-        out = []
-        for op in lins:
-            h = (len(op.a) + 1) // 2
-            out.append((op.out, LPAIR_A, op.a[:h], []))
-            out.append((None, LPAIR_B, op.a[h:], []))
-        return out
-    return [(op.out, op.kind, op.a, op.b if op.kind == OP_MUL else []) for op in step]
+    gp = next((g for g in (4, 2) if muls and g * len(muls) + len(lins) <= lanes), 1)
+    longest = max((len(op.a) for op in lins), default=0)
+    def lin_start(g):  # combination groups start aligned to their size
+        return -(-gp * len(muls) // g) * g
+    gl = next((g for g in (4, 2) if lins and longest > g // 2 and lin_start(g) + g * len(lins) <= lanes), 1)
+    out = []
+    for op in muls:
+        if gp == 1:
+            out.append((op.out, OP_MUL, op.a, op.b))
+            continue
+        h = gp // 2
+        for k, part in enumerate(_split(op.a, h)):
+            out.append((op.out if k == 0 else None, GRP_A, part, []))
+        for part in _split(op.b, h):
+            out.append((None, GRP_B, part, []))
+    out += [(None, 0, [], [])] * (lin_start(gl) - len(out))
+    for op in lins:
+        for k, part in enumerate(_split(op.a, gl)):
+            out.append((op.out if k == 0 else None, OP_LIN, part, []))
+    return out, gp, gl
 
 
 def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
@@ -466,7 +484,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
         L = getattr(pg, "lanes", LANES)  # 64 per wavefront the program runs on
         for step in pg.steps:
             assert len(step) <= L
-            entries = lane_entries(step, L)
+            entries, gp, gl = lane_entries(step, L)
             # per-step (wave-uniform) fields every lane carries: the largest term count of
             # operand a over the lanes that gather it (every op) and of operand b (the
             # unpaired products), and whether each is a single +1 term on all of them --
@@ -477,7 +495,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
             mb = max((len(e[3]) for e in muls), default=0)
             sa = bool(act) and all(len(e[2]) == 1 and e[2][0][1] == 1 for e in act)
             sb = bool(muls) and all(len(e[3]) == 1 and e[3][0][1] == 1 for e in muls)
-            flags = int(sa) | int(sb) << 1
+            flags = int(sa) | int(sb) << 1 | (gp.bit_length() - 1) << 2 | (gl.bit_length() - 1) << 4
             for lane in range(L):
                 if lane < len(entries):
                     out, kind, a, b = entries[lane]
@@ -506,7 +524,7 @@ def emit(progs: list[Program], consts: ConstBank, path: Path) -> None:
                                          *refs(a), *refs(b), *cfs(a), *cfs(b))
         first += len(pg.steps) * (L // LANES)
     assert len(consts.vals) <= 40, "constant bank exceeds COOP_MAX_CONSTS"
-    header = struct.pack("<4sIIII", b"BLSC", 3, len(consts.vals), len(progs), first)
+    header = struct.pack("<4sIIII", b"BLSC", 4, len(consts.vals), len(progs), first)
     cbin = b"".join(_le_limbs(v * MONT_R % P) for v in consts.vals)
     path.write_bytes(header + cbin + bytes(table) + bytes(steps_bin))
 
