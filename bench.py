@@ -214,10 +214,10 @@ def latency_curve(ctxs, works, points, sets_per_call: int, steps: int = 5) -> di
     return res
 
 
-PMC_FILE = "r04_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
+PMC_FILE = "r05_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
 # the committed rocprofv3 --kernel-trace --stats summary of the timed 12 x 22 shape (the
 # dominant kernels' average launch time with ~12 passes sharing the device)
-KSTATS_FILE = "r04_kernel_stats_timed_12x22_final.csv"
+KSTATS_FILE = "r05_kernel_stats_timed_12x22.csv"
 KSTATS_SETS = 22528                      # sets per pass of that run (22 calls x 1024)
 PEAK_FILE = "peak_fixed.json"            # the fixed v_mad_u64_u32 peak (median of the committed measurements)
 
@@ -269,9 +269,19 @@ def committed_pmc():
                          "valu_insts_per_wave": round(v["SQ_INSTS_VALU"] / max(1.0, v["SQ_WAVES"])),
                          "valu_wave_insts_per_set": round(v["SQ_INSTS_VALU"] / sets) if sets else None,
                          "hbm_bytes_per_launch": v.get("hbm_bytes_per_launch")}
+    # the timed shape proper (Pippenger signature sum, four items per k_mlf lane): counter
+    # collection serialises the probe's kernels, so some passes start with fewer sets in
+    # flight and take the group-sum shape (k_chain with role 2) or two items per k_mlf
+    # lane; the timed shape is the one with the fewest instructions in both, so per kernel
+    # the lowest per-dispatch figure
+    per = d.get("per_dispatch_valu_wave_insts_per_set", {})
+    mode = {n: min(v) for n, v in per.items() if v}
     return {"source": f"profiles/{PMC_FILE} (copied, not measured by this run)", "shape": d.get("shape"),
             "kernels": out, "hbm_bytes_per_pass": total, "sets_per_pass": sets,
-            "valu_wave_insts_per_set": round(vset) if sets else None}
+            "valu_wave_insts_per_set": round(vset) if sets else None,
+            "valu_wave_insts_per_set_note": "average over every dispatch of the probe, mixed pass shapes",
+            "valu_wave_insts_per_set_timed_shape": sum(mode.values()) if mode else None,
+            "valu_wave_insts_per_set_timed_shape_by_kernel": mode or None}
 
 
 def interop_sk(i: int) -> bytes:
