@@ -42,9 +42,20 @@ def sources() -> list[Path]:
 # A/B build variants: extra defines -> lodestar_amd/_native/liblodestar_bls_<name>.so
 # (the round-3 variants that lost were removed from the sources; their A/B records stay
 # under profiles/r03_ab_*.json)
-VARIANTS: dict[str, list[str]] = {
+VARIANTS: dict[str, list[str] | dict[str, list[str]]] = {
     "mlflz": ["-DBLS_LAZY_MLF=1"],   # both Miller-loop kernels in the lazy 28-bit-digit form (slower, k_mlq.hip)
+    # (a variant may also give flags per translation unit, {file stem: flags}; LLVM's
+    # iterative-ilp / iterative-minreg schedulers on k_mlq.hip alone measured slower /
+    # level, profiles/r05_ab_sched_strategy.json)
 }
+
+
+def _variant_flags(variant: str | None, tu: str) -> list[str] | None:
+    """extra compiler flags of a build variant for one translation unit (by file stem)"""
+    if not variant:
+        return None
+    v = VARIANTS[variant]
+    return v if isinstance(v, list) else v.get(tu) or None
 
 
 # Scratch: the HIP runtime backs each hardware queue with scratch for a full device of the
@@ -183,16 +194,16 @@ def build(jobs: int | None = None, verbose: bool = True, variant: str | None = N
     build_work_model(verbose)
     hdr = _headers_digest()
     srcs = sources()
-    extra = VARIANTS[variant] if variant else None
     lib = OUT_DIR / f"liblodestar_bls_{variant}.so" if variant else LIB
     jobs = jobs or min(len(srcs), os.cpu_count() or 4)
     # the kernels first: their resource usage sets the host TU's admission figure
     kern_srcs, host_src = srcs[1:], srcs[0]
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        kobjs = list(ex.map(lambda s: _compile(s, hdr, verbose, extra), kern_srcs))
+        kobjs = list(ex.map(lambda s: _compile(s, hdr, verbose, _variant_flags(variant, s.stem)), kern_srcs))
     table = [dict(k, tu=o.stem.split(".")[0]) for o in kobjs for k in json.loads(o.with_suffix(".res.json").read_text())]
     per_queue, worst = scratch_per_queue(table)
-    host_extra = (extra or []) + [f"-DBLS_SCRATCH_PER_QUEUE={per_queue}ull", f'-DBLS_SCRATCH_WORST_KERNEL="{worst}"']
+    host_extra = (_variant_flags(variant, host_src.stem) or []) + [f"-DBLS_SCRATCH_PER_QUEUE={per_queue}ull",
+                                                                  f'-DBLS_SCRATCH_WORST_KERNEL="{worst}"']
     objs = [_compile(host_src, hdr, verbose, host_extra)] + kobjs
     if not variant:  # every kernel's registers, occupancy and scratch reservation, for the record
         (OUT_DIR / "kernel_resources.json").write_text(json.dumps(
