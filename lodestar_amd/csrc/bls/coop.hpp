@@ -88,6 +88,7 @@ struct CoopEnv {
   // per-set frame (tools/gen_pset.py, kernels/k_pset.hip; the r chains run beside them)
   CoopProg pset_prep, pset_dbl_all, pset_add_x, pset_phase2, pset_norm2, pset_affine2, pset_ml2;
   CoopProg pset_ml2_w2;  // pset_ml2 laid out for two wavefronts (k_pset: every product on a lane pair)
+  CoopProg pset_xchain;  // the |x| chains as one program (pset_dbl_all / pset_add_x by the bits of |x|)
   CoopPsetN packed[2];  // [0]: 2 sets per wavefront, [1]: 3 sets
   // single-pair Miller loops (tools/gen_pset.py build_ml1, kernels/k_pset.hip k_mln, the
   // cooperative packings tests force): 1 or 2 sets per wavefront (COOP_FRAME)

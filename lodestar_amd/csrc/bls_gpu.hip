@@ -241,6 +241,7 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
               {"pset_phase2", &ctx->coop.pset_phase2},
               {"pset_norm2", &ctx->coop.pset_norm2},     {"pset_affine2", &ctx->coop.pset_affine2},
               {"pset_ml2", &ctx->coop.pset_ml2},         {"pset_ml2_w2", &ctx->coop.pset_ml2_w2},
+              {"pset_xchain", &ctx->coop.pset_xchain},
               {"ml1_1", &ctx->coop.ml1_1},
               {"ml1_2", &ctx->coop.ml1_2}};
   ctx->coop_progs = new std::vector<std::pair<std::string, CoopProg>>();

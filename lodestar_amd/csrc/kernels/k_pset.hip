@@ -2,7 +2,8 @@
 // programs of tools/gen_pset.py (interpreter: bls/coop.hpp):
 //
 //   P = iso(q0) + iso(q1)                               pset_prep
-//   A = [|x|]P, C = [|x|]sig (fixed bits of |x|)        pset_dbl_all / pset_add_x
+//   A = [|x|]P, C = [|x|]sig (fixed bits of |x|)        pset_xchain (pset_dbl_all / pset_add_x
+//                                                       in the order of |x|'s bits)
 //   H = clear_cofactor(P), psi(sig) ?= [x]sig           pset_phase2
 //   affine H with one lane-0 inversion                  pset_norm2, pset_affine2
 //   f_i = ML(RP, H) * ML(-RG, sig)                      pset_ml2
@@ -87,10 +88,7 @@ __global__ __launch_bounds__(PSET_WAVES * COOP_LANES) void k_pset(PipeBufs b, co
 
   if (w0) {
     coop_run(env, env.pset_prep, sh.frame, sh.cbank, &sh.flag);
-    for (int k = 62; k >= 0; --k) {
-      coop_run(env, env.pset_dbl_all, sh.frame, sh.cbank, &sh.flag);
-      if ((PS_X_ABS >> k) & 1ull) coop_run(env, env.pset_add_x, sh.frame, sh.cbank, &sh.flag);
-    }
+    coop_run(env, env.pset_xchain, sh.frame, sh.cbank, &sh.flag);  // 63 doublings, 5 additions
     coop_run(env, env.pset_phase2, sh.frame, sh.cbank, &sh.flag);
   }
   __syncthreads();

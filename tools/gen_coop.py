@@ -553,9 +553,22 @@ def build_all():
     # per wavefront in the 256-slot frame
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=1))
     progs.append(gen_pset.build_ml1(consts, T, miller_dbl, miller_add, X_ABS, FRAME, S=2))
+    # the one-set |x| chains as one straight program (kernels/k_pset.hip): the doubling /
+    # addition programs in the order of |x|'s bits, so the interpreter's op fetch stays
+    # ahead across the 68 chain steps instead of restarting at every program call
+    import copy
+    dbl = next(p for p in progs if p.name == "pset_dbl_all")
+    addx = next(p for p in progs if p.name == "pset_add_x")
+    assert dbl.n_slots == addx.n_slots
+    steps = []
+    for k in range(62, -1, -1):
+        steps += dbl.steps
+        if (X_ABS >> k) & 1:
+            steps += addx.steps
+    progs.append(Program("pset_xchain", steps, dbl.n_slots, [], sum(
+        1 for st in steps if any(op.kind == OP_MUL for op in st))))
     # the one-set Miller loop laid out for two wavefronts (kernels/k_pset.hip): the same
     # steps, 128 lanes each, so every product finds a lane pair
-    import copy
     ml2 = next(p for p in progs if p.name == "pset_ml2")
     w2 = copy.copy(ml2)
     w2.name, w2.lanes = "pset_ml2_w2", 2 * LANES
