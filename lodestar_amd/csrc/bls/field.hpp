@@ -180,6 +180,14 @@ BLS_HD Fp fp_sub_nr(const Fp& a, const Fp& b) {
   asm_add12(r.l, a.l, t.l);
   return r;
 }
+
+// a < 4p -> [0, 2p): one conditional subtraction of 2p (fp2_mul_s)
+BLS_HD Fp fp_reduce_2p(const Fp& a) {
+  const uint32_t pl2[12] = {BLS_2P_LIMBS};
+  Fp r;
+  asm_reduce12(r.l, a.l, pl2);
+  return r;
+}
 #else
 // Host build (CPU test harness and the CPU baseline under oracle/): the 12 x 32-bit
 // little-endian limbs are the bytes of 6 x 64-bit little-endian words, so the CPU
@@ -279,6 +287,20 @@ BLS_HD Fp fp_sub_nr(const Fp& a, const Fp& b) {
     c >>= 64;
   }
   return fp_w_store(x);
+}
+
+BLS_HD Fp fp_reduce_2p(const Fp& a) {
+  static const uint64_t P2[6] = {0x73fdffffffff5556ull, 0x3d57fffd62a7ffffull, 0xce61a541ed61ec48ull,
+                                 0xc8ee9709e70a257eull, 0x96374f6c869759aeull, 0x340223d472ffcd34ull};
+  uint64_t x[6], d[6];
+  fp_w_load(a, x);
+  unsigned __int128 br = 0;
+  for (int i = 0; i < 6; ++i) {
+    const unsigned __int128 t = (unsigned __int128)x[i] - P2[i] - (uint64_t)br;
+    d[i] = (uint64_t)t;
+    br = (t >> 64) & 1;
+  }
+  return fp_w_store(br ? x : d);
 }
 #endif
 
@@ -1115,6 +1137,19 @@ BLS_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
+// the same product for operands whose coefficients are unreduced sums (< 2p each,
+// fp2_add_nr of canonical values): a0 b0 and a1 b1 < 4p^2, and (a0 + a1) brought back
+// under 2p times (b0 + b1) < 4p is < 8p^2 < 2^384 p, inside the Montgomery product's
+// input bound (its output < 2p, then canonical); output canonical.  Saves the four
+// reductions of the pre-additions for one here (tests: test_hostsim.py::test_fp2_mul_s)
+BLS_HD Fp2 fp2_mul_s(const Fp2& a, const Fp2& b) {
+  Fp t0 = fp_mul(a.c0, b.c0);
+  Fp t1 = fp_mul(a.c1, b.c1);
+  Fp t2 = fp_mul(fp_reduce_2p(fp_add_nr(a.c0, a.c1)), fp_add_nr(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+BLS_HD Fp2 fp2_add_nr(const Fp2& a, const Fp2& b) { return Fp2{fp_add_nr(a.c0, b.c0), fp_add_nr(a.c1, b.c1)}; }
+
 BLS_HD Fp2 fp2_sqr(const Fp2& a) {
   Fp t0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub_nr(a.c0, a.c1));  // operands < 2p
   Fp t1 = fp_mul(fp_add_nr(a.c0, a.c0), a.c1);                   // 2 a0 a1
@@ -1202,11 +1237,12 @@ BLS_HD Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
   Fp2 t0 = fp2_mul(a.c0, b.c0);
   Fp2 t1 = fp2_mul(a.c1, b.c1);
   Fp2 t2 = fp2_mul(a.c2, b.c2);
-  Fp2 c0 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2);
+  // (the Karatsuba pre-additions stay unreduced: fp2_mul_s)
+  Fp2 c0 = fp2_sub(fp2_sub(fp2_mul_s(fp2_add_nr(a.c1, a.c2), fp2_add_nr(b.c1, b.c2)), t1), t2);
   c0 = fp2_add(fp2_mul_xi(c0), t0);
-  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1);
+  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul_s(fp2_add_nr(a.c0, a.c1), fp2_add_nr(b.c0, b.c1)), t0), t1);
   c1 = fp2_add(c1, fp2_mul_xi(t2));
-  Fp2 c2 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2);
+  Fp2 c2 = fp2_sub(fp2_sub(fp2_mul_s(fp2_add_nr(a.c0, a.c2), fp2_add_nr(b.c0, b.c2)), t0), t2);
   c2 = fp2_add(c2, t1);
   return Fp6{c0, c1, c2};
 }
@@ -1218,7 +1254,7 @@ BLS_HD Fp6 fp6_mul_01(const Fp6& a, const Fp2& d0, const Fp2& d1) {
   Fp2 a0d0 = fp2_mul(a.c0, d0);
   Fp2 a1d1 = fp2_mul(a.c1, d1);
   Fp2 c0 = fp2_add(a0d0, fp2_mul_xi(fp2_mul(a.c2, d1)));
-  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(d0, d1)), a0d0), a1d1);
+  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul_s(fp2_add_nr(a.c0, a.c1), fp2_add_nr(d0, d1)), a0d0), a1d1);
   Fp2 c2 = fp2_add(a1d1, fp2_mul(a.c2, d0));
   return Fp6{c0, c1, c2};
 }
@@ -1280,9 +1316,9 @@ BLS_HD Fp12 fp12_mul_line2(const Fp12& f, const Fp2& l0, const Fp2& l2, const Fp
                            const Fp2& m2, const Fp2& m3) {
   const Fp2 m00 = fp2_mul(l0, m0), m22 = fp2_mul(l2, m2), m33 = fp2_mul(l3, m3);
   const Fp2 a0 = fp2_add(m00, fp2_mul_xi(m33));
-  const Fp2 a2 = fp2_sub(fp2_sub(fp2_mul(fp2_add(l0, l2), fp2_add(m0, m2)), m00), m22);
-  const Fp2 a3 = fp2_sub(fp2_sub(fp2_mul(fp2_add(l0, l3), fp2_add(m0, m3)), m00), m33);
-  const Fp2 a5 = fp2_sub(fp2_sub(fp2_mul(fp2_add(l2, l3), fp2_add(m2, m3)), m22), m33);
+  const Fp2 a2 = fp2_sub(fp2_sub(fp2_mul_s(fp2_add_nr(l0, l2), fp2_add_nr(m0, m2)), m00), m22);
+  const Fp2 a3 = fp2_sub(fp2_sub(fp2_mul_s(fp2_add_nr(l0, l3), fp2_add_nr(m0, m3)), m00), m33);
+  const Fp2 a5 = fp2_sub(fp2_sub(fp2_mul_s(fp2_add_nr(l2, l3), fp2_add_nr(m2, m3)), m22), m33);
   const Fp6 p0 = Fp6{a0, a2, m22};
   const Fp6 t0 = fp6_mul(f.c0, p0);
   const Fp6 t1 = fp6_mul_v(fp6_mul_01(f.c1, a3, a5));  // f.c1 * (a3 v + a5 v^2)

@@ -147,6 +147,17 @@ int hs_fp_sqrt(const uint8_t* a, uint8_t* out) {
 }
 
 void hs_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr_fp2(fp2_mul(rd_fp2(a), rd_fp2(b)), out); }
+// field.hpp fp2_mul_s on raw limbs: coefficients < 2p (unreduced sums), canonical out
+void hs_fp2_mul_s_raw(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  Fp2 x, y;
+  memcpy(x.c0.l, a, 48);
+  memcpy(x.c1.l, a + 48, 48);
+  memcpy(y.c0.l, b, 48);
+  memcpy(y.c1.l, b + 48, 48);
+  const Fp2 r = fp2_mul_s(x, y);
+  memcpy(out, r.c0.l, 48);
+  memcpy(out + 48, r.c1.l, 48);
+}
 // the device's lazy Fp2 product (field.hpp fp2_mul_d28) on raw limbs (Montgomery form in, out)
 void hs_fp2_mul_d28_raw(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   Fp a0, a1, b0, b1;

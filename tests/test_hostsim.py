@@ -48,6 +48,39 @@ def test_fp_mul_d28_lazy(hostsim):
             assert r % P == (a * (a if sqr else b) * rinv) % P
 
 
+def test_fp_mul_d28_input_bound(hostsim):
+    """The Montgomery product's inputs may reach a b < 2^384 p (output < a b / R + p < 2p):
+    fp2_mul_s multiplies a value < 2p by one < 4p (8 p^2)."""
+    rng = random.Random(29)
+    o = _buf(48)
+    rinv = pow(2, -384, P)
+    pairs = [(2 * P - 1, 4 * P - 1), (2 * P - 1, 4 * P - 2 ** 100), (P, 4 * P - 1), (0, 4 * P - 1)]
+    pairs += [(rng.randrange(2 * P), rng.randrange(4 * P)) for _ in range(300)]
+    for a, b in pairs:
+        hostsim.hs_fp_mul_d28_raw(a.to_bytes(48, "little"), b.to_bytes(48, "little"), o, 0)
+        r = int.from_bytes(o.raw, "little")
+        assert r < 2 * P and r % P == (a * b * rinv) % P
+
+
+def test_fp2_mul_s(hostsim):
+    """field.hpp fp2_mul_s: the Fp2 product for operands whose coefficients are unreduced
+    sums (< 2p each); canonical output equal to the product of the reduced operands."""
+    rng = random.Random(30)
+    o = _buf(96)
+    rinv = pow(2, -384, P)
+    edge = [0, 1, P - 1, P, P + 1, 2 * P - 1, 2 * P - 2, 2 ** 381]
+    vals = edge + [rng.randrange(2 * P) for _ in range(200)]
+    for k in range(len(vals)):
+        a0, a1 = vals[k], vals[(k * 5 + 1) % len(vals)]
+        b0, b1 = vals[(k * 11 + 2) % len(vals)], vals[(k * 3 + 4) % len(vals)]
+        le = [v.to_bytes(48, "little") for v in (a0, a1, b0, b1)]
+        hostsim.hs_fp2_mul_s_raw(le[0] + le[1], le[2] + le[3], o)
+        c0, c1 = int.from_bytes(o.raw[:48], "little"), int.from_bytes(o.raw[48:], "little")
+        assert c0 < P and c1 < P
+        assert c0 == (a0 * b0 - a1 * b1) * rinv % P
+        assert c1 == (a0 * b1 + a1 * b0) * rinv % P
+
+
 def test_fp2_mul_lazy(hostsim):
     """The device Fp2 product with one reduction per coefficient (field.hpp fp2_mul_d28):
     canonical inputs -> canonical (a0 b0 - a1 b1) / R, (a0 b1 + a1 b0) / R, including the
