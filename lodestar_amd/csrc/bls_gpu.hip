@@ -1128,7 +1128,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   uint32_t* tseg_dev = nullptr;          // the merged signature sum's plan
   G2J* gtmp[2] = {nullptr, nullptr};
   uint32_t *unit_rep_dev = nullptr, *ugsets_dev = nullptr, *useg_dev = nullptr;  // Miller-loop units
-  uint32_t* own_sets_dev = nullptr;      // the individually verified sets' own Miller loops (one launch)
+  uint32_t* own_sets_dev = nullptr;      // the individually verified sets' own Miller loops + the requests' sums (one launch)
   MsmBufs msm;
   memset(&msm, 0, sizeof(msm));
   G1J* utmp[2] = {nullptr, nullptr};
@@ -1163,7 +1163,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.indiv_reqs = c.take<uint32_t>(R);
     gbufs.off = c.take<uint32_t>(gt_possible ? grp_cap + 1 : 0);
     gbufs.members = c.take<uint32_t>(grp_mem_cap);
-    own_sets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
+    own_sets_dev = sigagg ? c.take<uint32_t>((size_t)n + R) : nullptr;
     b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
     b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
     gsets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
@@ -1337,7 +1337,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       }
       HIPC(ctx, hipEventRecord(ctx->ev[4], s));
       // the f-side shape is chosen once per call (other contexts change the sets in flight
-      // meanwhile): every Miller-loop launch of the call and stats->pass_shape use it
+      // meanwhile): the first pass's Miller-loop launch and stats->pass_shape use it
       if (!b.mlf_pl && k_mln_list_ok(b)) b.mlf_pl = mlf_per_lane();
       HIPC(ctx, launch_k_mln(b, ctx->coop, 0, indiv_vbase, s)); dbg_sync(s, "k_mln");
     } else {
@@ -1380,6 +1380,14 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     }
     return 0;
   };
+  // the Miller-loop launches after the first pass take their own items-per-lane
+  // (mlf_per_lane_alone: their items never share f) unless a test forces one
+  const uint32_t pass_pl = b.mlf_pl;
+  const bool pl_forced = (ctx->debug_flags & BLS_DEBUG_MLF_PL_MASK) != 0;
+  auto alone_pl = [&](uint32_t count) {
+    const uint32_t pl = mlf_per_lane_alone(count);
+    if (pl && !pl_forced && k_mln_list_ok(b)) b.mlf_pl = pl;
+  };
   std::vector<int32_t> chunk_ok(n_chunks + 1, 0);
   std::vector<int32_t> merged_status(merged ? R : 0, 0);
   int32_t merged_verdict = 0;
@@ -1412,6 +1420,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     if (use_total) {
       // the chunks' own signature sums and their Miller loops (virtual sets n + c)
       if (launch_gsum(ctx, b, chunk_gsum, gseg_dev, gsets_dev, gtmp, n, s)) return -1;
+      alone_pl(n_chunks);
       HIPC(ctx, launch_k_mln(b, ctx->coop, n, n_chunks, s)); dbg_sync(s, "k_mln chunk sums");
     }
     HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s)); dbg_sync(s, "k_chunk_coop");
@@ -1421,7 +1430,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   if (stats) {
     stats->merged_check = merged ? (merged_pass ? 1 : 2) : 0;
     stats->pass_shape =
-        sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? b.mlf_pl << 8 : 0u)) : 0u;
+        sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? pass_pl << 8 : 0u)) : 0u;
   }
   if (stats) {
     stats->n_flagged = flagged;
@@ -1510,14 +1519,14 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       // each individually verified request pairs the sum of its own r sig:
       // virtual sets indiv_vbase + t; a request whose sets were paired in their
       // chunk's units or shared loops (its chunk failed) now runs their own Miller loops
-      std::vector<uint32_t> own;  // outlives the staged copy (the stream is synchronised below)
-      if ((use_units || ml_shared) && k_mln_list_ok(b)) {
-        // one launch over every set of the failed chunks' requests
+      std::vector<uint32_t> own;
+      const bool own_list = (use_units || ml_shared) && k_mln_list_ok(b);
+      if (own_list) {
+        // every set of the failed chunks' requests, in ONE launch with the requests'
+        // signature sums below (one Miller-loop latency instead of two on the failing
+        // call's path, profiles/r05_cfg5_fallback.json)
         for (size_t t = plan.nonbatch_reqs.size(); t < indiv.size(); ++t)
           for (uint32_t i = in->req_set_offsets[indiv[t]]; i < in->req_set_offsets[indiv[t] + 1]; ++i) own.push_back(i);
-        stage_copy(ctx, own_sets_dev, own.data(), sizeof(uint32_t) * own.size());
-        HIPC(ctx, launch_k_mln_list(b, own_sets_dev, (uint32_t)own.size(), s));
-        dbg_sync(s, "k_mln own (list)");
       } else if (use_units || ml_shared) {
         // one launch per run of consecutive sets (a failed chunk's requests are adjacent)
         uint32_t run_beg = 0, run_end = 0;
@@ -1529,6 +1538,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
             continue;
           }
           if (run_end > run_beg) {
+            alone_pl(run_end - run_beg);
             HIPC(ctx, launch_k_mln(b, ctx->coop, run_beg, run_end - run_beg, s, true));
             dbg_sync(s, "k_mln own");
           }
@@ -1547,7 +1557,16 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       stage_copy(ctx, gsets_dev, indiv_gsum.gsets.data(), sizeof(uint32_t) * indiv_gsum.gsets.size());
       stage_copy(ctx, gseg_dev, indiv_gsum.seg.data(), sizeof(uint32_t) * indiv_gsum.seg.size());
       if (launch_gsum(ctx, b, indiv_gsum, gseg_dev, gsets_dev, gtmp, indiv_vbase, s)) return -1;
-      HIPC(ctx, launch_k_mln(b, ctx->coop, indiv_vbase, (uint32_t)indiv.size(), s)); dbg_sync(s, "k_mln indiv");
+      if (own_list) {
+        for (size_t t = 0; t < indiv.size(); ++t) own.push_back(indiv_vbase + (uint32_t)t);
+        stage_copy(ctx, own_sets_dev, own.data(), sizeof(uint32_t) * own.size());
+        alone_pl((uint32_t)own.size());
+        HIPC(ctx, launch_k_mln_list(b, own_sets_dev, (uint32_t)own.size(), s));
+        dbg_sync(s, "k_mln own + indiv (list)");
+      } else {
+        alone_pl((uint32_t)indiv.size());
+        HIPC(ctx, launch_k_mln(b, ctx->coop, indiv_vbase, (uint32_t)indiv.size(), s)); dbg_sync(s, "k_mln indiv");
+      }
     }
     // groups of BLS_FOLD consecutive sets per request, multiplied in parallel first
     bool any_fold = false;

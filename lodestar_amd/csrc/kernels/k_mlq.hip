@@ -481,16 +481,44 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   return hipGetLastError();
 }
 
-uint32_t mlf_per_lane() {
+uint32_t mlf_per_lane_fixed() {
   static const uint32_t fixed = [] {
     const char* e = getenv("BLS_MLF_PER_LANE");
     const int v = e ? atoi(e) : 0;
     return (v == 1 || v == 2 || v == 4 || v == (int)MLF_PAIR) ? (uint32_t)v : 0u;
   }();
+  return fixed;
+}
+
+uint64_t mlf_pair_max() {
   static const uint64_t pair_max = [] {
     const char* e = getenv("BLS_MLF_PAIR_MAX");
     return e ? (uint64_t)strtoull(e, nullptr, 10) : 16384ull;
   }();
+  return pair_max;
+}
+
+// Items per k_mlf lane for the launches after the first pass (a failed merged check's
+// chunk signature sums, the individually verified requests' own loops and sums): their
+// items never share f, so more than one per lane only lengthens the chain that the failing
+// call waits on (4 per lane ran each such launch for the whole 14 ms of a plateau pass's f
+// side, profiles/r05_cfg5_fallback.json).  Two lanes per item up to $BLS_MLF_PAIR_MAX
+// items, else one; $BLS_MLF_PER_LANE still fixes it; $BLS_MLF_ALONE=0 returns 0 (the
+// launches keep the first pass's shape, as before round 5's change).
+uint32_t mlf_per_lane_alone(uint32_t count) {
+  static const bool off = [] {
+    const char* e = getenv("BLS_MLF_ALONE");
+    return e && atoi(e) == 0;
+  }();
+  if (off) return 0u;
+  const uint32_t fixed = mlf_per_lane_fixed();
+  if (fixed) return fixed;
+  return count <= mlf_pair_max() ? MLF_PAIR : 1u;
+}
+
+uint32_t mlf_per_lane() {
+  const uint32_t fixed = mlf_per_lane_fixed();
+  const uint64_t pair_max = mlf_pair_max();
   static const uint64_t pl2_min = [] {
     const char* e = getenv("BLS_MLF_PL2_MIN");
     return e ? (uint64_t)strtoull(e, nullptr, 10) : 98304ull;

@@ -99,5 +99,9 @@ size_t mlq_line_words(uint32_t count);
 uint64_t bls_sets_in_flight();
 // items per lane of k_mlf (1, 2 or 4) for a launch now (kernels/k_mlq.hip)
 uint32_t mlf_per_lane();
+// ... and for a launch after the first pass (items that never share f), by its item count
+uint32_t mlf_per_lane_alone(uint32_t count);
+uint32_t mlf_per_lane_fixed();
+uint64_t mlf_pair_max();
 hipError_t launch_k_mlqf(const bls::PipeBufs& b, uint32_t first, uint32_t count, bool own_only, uint32_t* lines,
                          hipStream_t s, const uint32_t* items = nullptr);
