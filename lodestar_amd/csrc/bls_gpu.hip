@@ -1388,6 +1388,17 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     const uint32_t pl = mlf_per_lane_alone(count);
     if (pl && !pl_forced && k_mln_list_ok(b)) b.mlf_pl = pl;
   };
+  // ... and up to coop_ml_max() items they are cooperative single-pair loops, one
+  // wavefront per item (launch_k_mln_coop), else the SIMT pair at that shape
+  auto launch_ml_alone = [&](uint32_t first, uint32_t count, const uint32_t* items) -> hipError_t {
+    if (count == 0) return hipSuccess;
+    if (!pl_forced && k_mln_list_ok(b)) {
+      const hipError_t e = launch_k_mln_coop(b, ctx->coop, first, count, items, s);
+      if (e != hipErrorNotSupported) return e;
+    }
+    alone_pl(count);
+    return items ? launch_k_mln_list(b, items, count, s) : launch_k_mln(b, ctx->coop, first, count, s);
+  };
   std::vector<int32_t> chunk_ok(n_chunks + 1, 0);
   std::vector<int32_t> merged_status(merged ? R : 0, 0);
   int32_t merged_verdict = 0;
@@ -1420,8 +1431,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     if (use_total) {
       // the chunks' own signature sums and their Miller loops (virtual sets n + c)
       if (launch_gsum(ctx, b, chunk_gsum, gseg_dev, gsets_dev, gtmp, n, s)) return -1;
-      alone_pl(n_chunks);
-      HIPC(ctx, launch_k_mln(b, ctx->coop, n, n_chunks, s)); dbg_sync(s, "k_mln chunk sums");
+      HIPC(ctx, launch_ml_alone(n, n_chunks, nullptr)); dbg_sync(s, "k_mln chunk sums");
     }
     HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s)); dbg_sync(s, "k_chunk_coop");
     HIPC(ctx, hipStreamSynchronize(s));
@@ -1560,12 +1570,10 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       if (own_list) {
         for (size_t t = 0; t < indiv.size(); ++t) own.push_back(indiv_vbase + (uint32_t)t);
         stage_copy(ctx, own_sets_dev, own.data(), sizeof(uint32_t) * own.size());
-        alone_pl((uint32_t)own.size());
-        HIPC(ctx, launch_k_mln_list(b, own_sets_dev, (uint32_t)own.size(), s));
+        HIPC(ctx, launch_ml_alone(0, (uint32_t)own.size(), own_sets_dev));
         dbg_sync(s, "k_mln own + indiv (list)");
       } else {
-        alone_pl((uint32_t)indiv.size());
-        HIPC(ctx, launch_k_mln(b, ctx->coop, indiv_vbase, (uint32_t)indiv.size(), s)); dbg_sync(s, "k_mln indiv");
+        HIPC(ctx, launch_ml_alone(indiv_vbase, (uint32_t)indiv.size(), nullptr)); dbg_sync(s, "k_mln indiv");
       }
     }
     // groups of BLS_FOLD consecutive sets per request, multiplied in parallel first

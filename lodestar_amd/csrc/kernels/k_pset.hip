@@ -271,6 +271,16 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln(PipeBufs b, const CoopEnv* _
                first + count, units_paired);
 }
 
+// The listed items' own single-pair loops, one wavefront each (a failing pass's later
+// Miller loops, launch_k_mln_coop).
+template <class Lds>
+__global__ __launch_bounds__(COOP_LANES) void k_mln_items(PipeBufs b, const CoopEnv* __restrict__ envp,
+                                                          const uint32_t* __restrict__ items) {
+  __shared__ Lds sh;
+  const uint32_t i = items[blockIdx.x];
+  mln_items<1>(b, *envp, sh.frame, &sh.flag, (int)(sizeof(sh.frame) / sizeof(Fp)), i, i + 1, 0u);
+}
+
 // Sets per wavefront for a batch: 1 for small batches (latency: one wave per set
 // spreads a small call over more SIMDs), 2 from BLS_PACK_MIN_SETS sets on
 // (throughput: the 2-set frame fits 20 KB of LDS, so two wavefronts share each SIMD;
@@ -313,6 +323,29 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
   } else {
     k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env.dev, first, count, up);
   }
+  return hipGetLastError();
+}
+
+// A failing pass's later Miller loops (chunk signature sums, the failed chunks' own loops,
+// the individually verified requests' sums: items that never share f) as cooperative
+// single-pair loops, one wavefront per item: ~1 ms of latency where the SIMT pair
+// k_mlq + k_mlf2 takes ~7 ms (2.6 + 4.6, profiles/r05_cfg5_fallback_coop.json), and the
+// items are few.  Up to $BLS_COOP_ML_MAX items (default 8192; 0 turns it off); 0 items
+// or no ml1_1 program: hipErrorNotSupported (the caller takes the SIMT pair).
+uint32_t coop_ml_max() {
+  static const uint32_t v = [] {
+    const char* e = getenv("BLS_COOP_ML_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 8192u;
+  }();
+  return v;
+}
+
+hipError_t launch_k_mln_coop(const PipeBufs& b, const CoopEnv& env, uint32_t first, uint32_t count,
+                             const uint32_t* items, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  if (env.ml1_1.n == 0 || count > coop_ml_max()) return hipErrorNotSupported;
+  if (items) k_mln_items<CoopLds><<<count, COOP_LANES, 0, s>>>(b, env.dev, items);
+  else k_mln<1, CoopLds><<<count, COOP_LANES, 0, s>>>(b, env.dev, first, count, 0u);
   return hipGetLastError();
 }
 

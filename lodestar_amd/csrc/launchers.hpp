@@ -94,6 +94,12 @@ hipError_t launch_k_mln(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_
 // the failed chunks at once
 bool k_mln_list_ok(const bls::PipeBufs& b);
 hipError_t launch_k_mln_list(const bls::PipeBufs& b, const uint32_t* items, uint32_t count, hipStream_t s);
+// cooperative single-pair loops of [first, first + count) or of items[0, count), one
+// wavefront each, for a failing pass's later launches; hipErrorNotSupported above
+// coop_ml_max() items (kernels/k_pset.hip)
+hipError_t launch_k_mln_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, uint32_t first, uint32_t count,
+                             const uint32_t* items, hipStream_t s);
+uint32_t coop_ml_max();
 size_t mlq_line_words(uint32_t count);
 // sets in the verify calls currently running in this process (every context)
 uint64_t bls_sets_in_flight();
