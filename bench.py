@@ -214,10 +214,10 @@ def latency_curve(ctxs, works, points, sets_per_call: int, steps: int = 5) -> di
     return res
 
 
-PMC_FILE = "r05_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
+PMC_FILE = "r05f_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
 # the committed rocprofv3 --kernel-trace --stats summary of the timed 12 x 22 shape (the
 # dominant kernels' average launch time with ~12 passes sharing the device)
-KSTATS_FILE = "r05_kernel_stats_timed_12x22.csv"
+KSTATS_FILE = "r05f_kernel_stats_timed_12x22.csv"
 KSTATS_SETS = 22528                      # sets per pass of that run (22 calls x 1024)
 PEAK_FILE = "peak_fixed.json"            # the fixed v_mad_u64_u32 peak (median of the committed measurements)
 
@@ -275,7 +275,7 @@ def committed_pmc():
     # lane; the timed shape is the one with the fewest instructions in both, so per kernel
     # the lowest per-dispatch figure
     per = d.get("per_dispatch_valu_wave_insts_per_set", {})
-    mode = {n: min(v) for n, v in per.items() if v}
+    mode = {n: min(v) for n, v in per.items() if v and n.startswith(VERIFY_KERNELS)}
     return {"source": f"profiles/{PMC_FILE} (copied, not measured by this run)", "shape": d.get("shape"),
             "kernels": out, "hbm_bytes_per_pass": total, "sets_per_pass": sets,
             "valu_wave_insts_per_set": round(vset) if sets else None,

@@ -66,6 +66,10 @@ def main():
     ap.add_argument("--table-keys", type=int, default=1 << 20)
     ap.add_argument("--runs", default="invalid,valid", help="which of the two jobs to run")
     ap.add_argument("--jobs", type=int, default=5, help="the job back to back in one timed region (steady state)")
+    ap.add_argument("--shape", choices=("cfg5", "cfg4", "cfg4b"), default="cfg5",
+                    help="cfg4 / cfg4b: bench.py's cfg4 slice (125,000 range-sync sets, 1 %% invalid) as "
+                         "non-batchable or per-set batchable 128-set calls; --contexts / --cpp as its sub-record")
+    ap.add_argument("--cpp", type=int, default=0, help="calls per pass (0: the slice's calls over the contexts)")
     args = ap.parse_args()
     from lodestar_amd import workloads as W
     from lodestar_amd.native import GpuContext
@@ -78,14 +82,18 @@ def main():
         for key, inv in (("invalid", args.invalid), ("valid", 0)):
             if key not in args.runs.split(","):
                 continue
-            w = W.cfg5_slice(ctxs[0], args.table_keys, args.sets, args.roots, invalid=inv)
+            if args.shape == "cfg5":
+                w = W.cfg5_slice(ctxs[0], args.table_keys, args.sets, args.roots, invalid=inv)
+            else:
+                w = W.cfg4_slice(ctxs[0], args.table_keys, args.sets, invalid_frac=0.01 if inv else 0.0,
+                                 batchable_calls=args.shape == "cfg4b")
             pbs = W.packed_calls(w)
-            cpp = (len(pbs) + len(ctxs) - 1) // len(ctxs)
+            cpp = args.cpp or (len(pbs) + len(ctxs) - 1) // len(ctxs)
             run(ctxs, pbs[:len(ctxs)], 1)  # warm-up
             el, out, tot, stage = run(ctxs, pbs * args.jobs, cpp)
             bad = [k for k in range(len(out)) if not W.verdicts_ok(w, k % len(pbs), out[k])]
             assert not bad, f"{key}: {len(bad)} calls with wrong verdicts"
-            res[key] = {"invalid_sets": inv, "calls": len(pbs), "calls_per_pass": cpp, "elapsed_s": round(el, 4),
+            res[key] = {"shape": args.shape, "invalid_sets": sum(not x for v in w.valid for x in v), "calls": len(pbs), "calls_per_pass": cpp, "elapsed_s": round(el, 4),
                         "jobs": args.jobs, "sets_per_s": round(args.jobs * w.n_sets / el, 1), **tot,
                         "stage_ms_sum": [round(float(x), 2) for x in stage]}
             print(key, json.dumps(res[key]), file=sys.stderr, flush=True)

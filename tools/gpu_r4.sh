@@ -95,6 +95,6 @@ if [ -n "$PMC" ]; then
   done
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o run --output-format csv -- $PB > $R/$O/trace.log 2>&1 || { tail -20 $R/$O/trace.log; exit 1; }
   cd $R
-  python3 tools/pmc_summary.py $O/pmc_summary.json "the timed region's shape: ${PMC_CTX:-12} contexts x ${PMC_CPP:-22} calls of 1024 cfg2 sets, one pass each (bench.py --probe-only --inflight ${PMC_CTX:-12} --calls-per-pass ${PMC_CPP:-22} --steps 1 --warmup 0; the pass shape chosen by the sets in flight as in the timed region); counter collection serialises the kernels, so per-dispatch figures, not the overlap; setup kernels (k_sign, k_sk_to_pk, k_load_pubkeys, k_aggregate) are input synthesis" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5 > $O/pmc_summary.txt
+  python3 tools/pmc_summary.py --sets-per-pass $(( ${PMC_CPP:-22} * 1024 )) $O/pmc_summary.json "the timed region's shape: ${PMC_CTX:-12} contexts x ${PMC_CPP:-22} calls of 1024 cfg2 sets, one pass each (bench.py --probe-only --inflight ${PMC_CTX:-12} --calls-per-pass ${PMC_CPP:-22} --steps 1 --warmup 0; the pass shape chosen by the sets in flight as in the timed region); counter collection serialises the kernels, so per-dispatch figures, not the overlap; setup kernels (k_sign, k_sk_to_pk, k_load_pubkeys, k_aggregate) are input synthesis" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5 > $O/pmc_summary.txt
 fi
 echo done
