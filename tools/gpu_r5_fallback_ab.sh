@@ -10,7 +10,7 @@ if [ -z "$NOTESTS" ]; then
   tail -1 $O/pytest.log
 fi
 for ab in off on off2 on2; do
-  case $ab in off*) export ${OFF_VAR:-BLS_MLF_ALONE}=0;; *) unset ${OFF_VAR:-BLS_MLF_ALONE};; esac
+  case $ab in off*) export ${OFF_VAR:-BLS_MLF_ALONE}=${OFF_VAL:-0};; *) unset ${OFF_VAR:-BLS_MLF_ALONE};; esac
   timeout -k 10 300 python -u tools/cfg5_probe.py ${ARGS} > $O/probe_$ab.json 2> $O/probe_$ab.err || { echo "probe $ab failed"; tail -20 $O/probe_$ab.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/probe_$ab.json'));print('$ab',{k:(d[k]['sets_per_s'],d[k]['merged_fail'],d[k]['stage_ms_sum']) for k in ('invalid','valid')})"
 done
