@@ -47,6 +47,10 @@ struct bls_gpu_ctx {
   G1A* table;
   uint32_t table_n, table_cap;
   uint32_t debug_flags;  // bls_gpu_set_debug_flags
+  // the context's last pass failed its merged check: its next pass keeps the per-set
+  // [r] sig chains rather than the Pippenger sum (verify_body use_msm), so a failure
+  // there does not relaunch them (profiles/r05_ab_msm_min.json)
+  bool last_merged_failed;
   // grow-only device workspace and pinned staging
   uint32_t* msm_state;  // MSM bucket counters + tickets (MSM_STATE_WORDS), zero between passes
   uint8_t* dev_ws;
@@ -759,8 +763,12 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
 // set, but its serial stages (segments, buckets, the windows' dependent additions) make
 // the pass ~5 ms longer.  So it pays only when the device is VALU-bound with many sets in
 // flight: 3.46M vs 3.21M sets/s at 16 x 16, level at 12 x 16, 1.89M vs 2.25M at 4 x 16
-// (profiles/r03_ab_msm.json).  By default on while the process has more than
-// $BLS_MSM_MIN (200,000) sets in flight; $BLS_MSM=1 / 0 forces it on / off.
+// (profiles/r03_ab_msm.json, round 3).  On the round-5 build it is level at 4 x 16 and
+// ahead from 6 x 16 on (8 x 16: 3.24M / 3.30M vs 3.00M, profiles/r05_ab_msm_min.json), so
+// by default on while the process has more than $BLS_MSM_MIN (60,000) sets in flight and
+// the context's last pass passed its merged check (a failing pass needs the per-set chains
+// after all: relaunching them cost the epoch slice with invalid sets 2.42M -> 2.1M sets/s);
+// $BLS_MSM=1 / 0 forces it on / off.
 static bool msm_on() {
   static const int forced = [] {
     const char* e = getenv("BLS_MSM");
@@ -768,7 +776,7 @@ static bool msm_on() {
   }();
   static const uint64_t min_sets = [] {
     const char* e = getenv("BLS_MSM_MIN");
-    return e ? (uint64_t)strtoull(e, nullptr, 10) : 200000ull;
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 60000ull;
   }();
   if (forced >= 0) return forced == 1;
   return bls_sets_in_flight() > min_sets;
@@ -1069,7 +1077,8 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // role 2 alone) only when the merged check fails and the chunks' own sums are needed
   // (an MSM entry packs its bucket slot in 22 bits and a bucket takes up to 2 entries per
   // set: passes above MSM_MAX_SETS keep the group sums)
-  const bool use_msm = use_total && n <= MSM_MAX_SETS && (msm_on() || (ctx->debug_flags & BLS_DEBUG_MSM));
+  const bool use_msm = use_total && n <= MSM_MAX_SETS &&
+                       ((msm_on() && !ctx->last_merged_failed) || (ctx->debug_flags & BLS_DEBUG_MSM));
   GsumPlan total_gsum;
   if (use_total) {
     std::vector<uint32_t> goff(n_chunks + 1, (uint32_t)chunk_gsum.gsets.size());
@@ -1423,6 +1432,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   }
   bool merged_pass = merged && merged_verdict == 1;
   for (uint32_t r = 0; merged_pass && r < R; ++r) merged_pass = merged_status[r] == BLS_OK;
+  if (merged) ctx->last_merged_failed = !merged_pass;
   if (merged_pass) {
     for (uint32_t ch = 0; ch < n_chunks; ++ch) chunk_ok[ch] = 1;
   } else if (n_chunks > 0 && !partial) {
