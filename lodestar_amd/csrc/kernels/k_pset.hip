@@ -281,11 +281,15 @@ __global__ __launch_bounds__(COOP_LANES) void k_mln_items(PipeBufs b, const Coop
   mln_items<1>(b, *envp, sh.frame, &sh.flag, (int)(sizeof(sh.frame) / sizeof(Fp)), i, i + 1, 0u);
 }
 
-// Sets per wavefront for a batch: 1 for small batches (latency: one wave per set
-// spreads a small call over more SIMDs), 2 from BLS_PACK_MIN_SETS sets on
-// (throughput: the 2-set frame fits 20 KB of LDS, so two wavefronts share each SIMD;
-// the 3-set frame holds one).  $BLS_PACK (1, 2 or 3) forces a packing; $BLS_PACK_MIN
-// overrides the threshold.
+// Sets per wavefront for a batch: 1 for small batches (latency: one set per two
+// wavefronts spreads a small call over more SIMDs); from BLS_PACK_MIN_SETS sets on, 2
+// while the process has at most $BLS_PACK3_INFLIGHT (2,048) sets in flight, else 3
+// (three sets' steps share one wavefront's lanes: on the round-5 interpreter 1024-set
+// calls at 4 x 1 / 8 x 1 / 12 x 1 contexts run 0.58M / 0.70M / 0.79M sets/s packed 3
+// against 0.49-0.53M / 0.63-0.66M / 0.68-0.70M packed 2 and ~0.26M unpacked, but at
+// 2 x 1 0.32M against 0.35M; profiles/r05_ab_perset_pack.json; round 4 had 2 ahead of 3
+// everywhere).  $BLS_PACK (1, 2 or 3) forces a packing; $BLS_PACK_MIN overrides the
+// threshold.
 #define BLS_PACK_MIN_SETS 512u
 static uint32_t pack_for(uint32_t n_sets) {
   static const int forced = [] {
@@ -297,7 +301,12 @@ static uint32_t pack_for(uint32_t n_sets) {
     return e ? (uint32_t)strtoul(e, nullptr, 10) : BLS_PACK_MIN_SETS;
   }();
   if (forced >= 1 && forced <= 3) return (uint32_t)forced;
-  return n_sets >= min_sets ? 2u : 1u;
+  static const uint64_t pack3_inflight = [] {
+    const char* e = getenv("BLS_PACK3_INFLIGHT");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : 2048ull;
+  }();
+  if (n_sets < min_sets) return 1u;
+  return bls_sets_in_flight() > pack3_inflight ? 3u : 2u;
 }
 
 // The aggregated path's Miller loops are the SIMT pair k_mlq / k_mlf
