@@ -85,6 +85,7 @@ struct CoopEnv {
   const Fp* consts;
   uint32_t n_consts;
   CoopProg fin_fmul, fin_fe1, fin_fe2;
+  CoopProg fin_fe2_w2;  // fin_fe2 laid out for two wavefronts (k_indiv_coop2)
   // per-set frame (tools/gen_pset.py, kernels/k_pset.hip; the r chains run beside them)
   CoopProg pset_prep, pset_dbl_all, pset_add_x, pset_phase2, pset_norm2, pset_affine2, pset_ml2;
   CoopProg pset_ml2_w2;  // pset_ml2 laid out for two wavefronts (k_pset: every product on a lane pair)

@@ -241,6 +241,7 @@ static int load_coop_tables(bls_gpu_ctx* ctx) {
     CoopProg* dst;
   } want[] = {{"fin_fmul", &ctx->coop.fin_fmul},         {"fin_fe1", &ctx->coop.fin_fe1},
               {"fin_fe2", &ctx->coop.fin_fe2},           {"pset_prep", &ctx->coop.pset_prep},
+              {"fin_fe2_w2", &ctx->coop.fin_fe2_w2},
               {"pset_dbl_all", &ctx->coop.pset_dbl_all}, {"pset_add_x", &ctx->coop.pset_add_x},
               {"pset_phase2", &ctx->coop.pset_phase2},
               {"pset_norm2", &ctx->coop.pset_norm2},     {"pset_affine2", &ctx->coop.pset_affine2},

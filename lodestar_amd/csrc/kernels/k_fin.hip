@@ -194,8 +194,67 @@ hipError_t launch_k_chunk_coop(const PipeBufs& b, const CoopEnv& env, hipStream_
   k_chunk_coop<<<b.n_chunks, COOP_LANES, 0, s>>>(b, env.dev);
   return hipGetLastError();
 }
+// k_indiv_coop on two wavefronts per request: products, the easy part and the inversion
+// on wavefront 0 (single-wavefront programs, block barriers between), the hard part
+// (fin_fe2_w2) on both, so every product of its steps finds a lane pair -- for calls with
+// few requests verified alone (a small non-batchable call's one request), where the
+// final exponentiation is on the call's critical path.  Every branch reads block-uniform
+// values.
+__device__ void fin_accumulate_set2(const PipeBufs& b, const CoopEnv& env, FinShared& sh, uint32_t i, bool& first,
+                                    bool w0) {
+  if (first) {
+    coop_load(sh.frame, FIN_F, reinterpret_cast<const Fp*>(&b.f[i]), 12);
+    first = false;
+    return;
+  }
+  coop_load(sh.frame, FIN_G, reinterpret_cast<const Fp*>(&b.f[i]), 12);
+  if (w0) coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(2 * COOP_LANES) void k_indiv_coop2(PipeBufs b, const CoopEnv* __restrict__ envp,
+                                                                GroupBufs gb) {
+  const CoopEnv& env = *envp;
+  BLS_TAIL_PRIO();
+  __shared__ FinShared sh;
+  const uint32_t t = blockIdx.x;
+  const uint32_t r = b.indiv_reqs[t];
+  const int32_t code = b.req_status[r];
+  if (code != BLS_OK) {
+    if (threadIdx.x == 0) b.indiv_verdict[t] = -code;
+    return;
+  }
+  const bool w0 = threadIdx.x < COOP_LANES;
+  fin_init(env, sh);
+  bool first = true;
+  const uint32_t stride = b.fold > 1 ? b.fold : 1u;
+  for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set2(b, env, sh, i, first, w0);
+  if (b.sigagg) fin_accumulate_set2(b, env, sh, b.indiv_vbase + t, first, w0);
+  if (t >= gb.n_direct) {
+    if (threadIdx.x < 12) reinterpret_cast<Fp*>(&gb.f[t])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
+    if (threadIdx.x == 0) b.indiv_verdict[t] = 2;
+    return;
+  }
+  if (w0) {
+    coop_run(env, env.fin_fe1, sh.frame, sh.cbank, &sh.flag);
+    coop_invert(sh.frame, FIN_INV_IN, FIN_INV_OUT);
+  }
+  __syncthreads();
+  coop_run2_t(env, env.fin_fe2_w2, sh.frame, &sh.flag);
+  bool one = fp_eq(coop_get(sh.frame, FIN_F), c_one());
+  for (int k = 1; k < 12; ++k) one = one && fp_is_zero(coop_get(sh.frame, FIN_F + k));
+  if (threadIdx.x == 0) b.indiv_verdict[t] = one ? 1 : 0;
+}
+
+// Up to $BLS_INDIV2_MAX (64) requests verified alone: two wavefronts each (k_indiv_coop2);
+// more: one (the rate of a failing pass's many requests)
 hipError_t launch_k_indiv_coop(const PipeBufs& b, const CoopEnv& env, const GroupBufs& g, hipStream_t s) {
-  k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env.dev, g);
+  static const uint32_t w2_max = [] {
+    const char* e = getenv("BLS_INDIV2_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 64u;
+  }();
+  if (b.n_indiv <= w2_max && env.fin_fe2_w2.n > 0) k_indiv_coop2<<<b.n_indiv, 2 * COOP_LANES, 0, s>>>(b, env.dev, g);
+  else k_indiv_coop<<<b.n_indiv, COOP_LANES, 0, s>>>(b, env.dev, g);
   return hipGetLastError();
 }
 

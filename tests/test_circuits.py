@@ -142,7 +142,8 @@ def test_emitted_lane_groups_match_program(progs, tmp_path):
     does."""
     pg, consts = progs
     path = tmp_path / "t.bin"
-    names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul", "pset_norm2", "pset_ml2_w2", "pset_xchain"]
+    names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul", "pset_norm2", "pset_ml2_w2", "pset_xchain",
+             "fin_fe2_w2"]
     GC.emit([pg[nm] for nm in names], consts, path)
     sizes = [GC.lane_entries(st, getattr(pg[nm], "lanes", 64))[1:] for nm in names for st in pg[nm].steps]
     assert sum(gp == 2 for gp, _ in sizes) >= 10 and sum(gp == 4 for gp, _ in sizes) >= 3

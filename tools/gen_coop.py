@@ -573,6 +573,12 @@ def build_all():
     w2 = copy.copy(ml2)
     w2.name, w2.lanes = "pset_ml2_w2", 2 * LANES
     progs.append(w2)
+    # the final exponentiation's hard part likewise (kernels/k_fin.hip k_indiv_coop2: a
+    # small call's requests verified alone)
+    fe2 = next(p for p in progs if p.name == "fin_fe2")
+    f2 = copy.copy(fe2)
+    f2.name, f2.lanes = "fin_fe2_w2", 2 * LANES
+    progs.append(f2)
     return progs, consts
 
 
