@@ -1,8 +1,9 @@
 // Single-lane pre-stage of the verify path (pipeline.hpp stage_pre): for every
 // distinct signing root the two SSWU points on E2' (expand_message_xmd + hash_to_field + SSWU, two Fp
-// exponentiations each) and the signature decompression.  Lanes [0, 2u) map,
-// lanes [2u, 2u + n) decode, so each wavefront runs one kind of work; k_qdup then
-// hands each set its root's points.
+// exponentiations each) and the signature decompression.  Lanes [0, 2u) map, lanes
+// [base, base + n) decode from the next wavefront boundary (pipeline.hpp
+// pre_decode_base), so each wavefront runs one kind of work; k_qdup then hands each set
+// its root's points.
 #define BLS_FP_D28 1  // 28-bit-digit Montgomery product (bls/field.hpp)
 #include "../launchers.hpp"
 
