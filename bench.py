@@ -700,7 +700,7 @@ def bench_job(args, ctxs, rank: int, world: int, dist, device, make_backend) -> 
             "data": "synthetic: interop keys, sha256 messages, GPU-made signatures, invalid sets by construction",
             "config": {"workload": workload, "parallelism": par, "table_keys": args.table_keys,
                        "contexts_per_gpu": len(ctxs),
-                       "runtime": {"hip_runtime": _mapped_hip(),
+                       "runtime": {"hip_runtime": _mapped_hip(), "library_hip_runtime": _library_hip(),
                                    "process_group": ({"backend": dist.get_backend(), "world": dist.get_world_size()}
                                                      if dist is not None and dist.is_initialized() else None)}},
             "job": {k: v for k, v in res.items() if k != "elapsed_s"}}
@@ -726,18 +726,20 @@ def run_sharded(be, sets, seed, steps, warmup, dist, device):
     return time.perf_counter() - t0, len(sets)
 
 
-def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int, per_call: int = 1, max_call: int = 1024) -> dict:
+def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int, per_call: int = 1, max_call: int = 1024,
+             devices: str = "0") -> dict:
     """--mode napi: integration/js/benchNapi.js in a child Node process (the GPU is not
     touched by this process meanwhile); per_call sets per verifySignatureSets call,
-    max_call sets per GPU call (the adapter's maxSetsPerCall)."""
+    max_call sets per GPU call (the adapter's maxSetsPerCall); `inflight` contexts per
+    device slot of `devices` (the adapter's `devices` option)."""
     node = shutil.which("node")
     if node is None:
         raise SystemExit("--mode napi needs node")
-    env = dict(os.environ, UV_THREADPOOL_SIZE=str(max(4, inflight + 2)))
+    n_slots = len(devices.split(","))
+    env = dict(os.environ, UV_THREADPOOL_SIZE=str(max(4, n_slots * inflight + 2)))
     out = subprocess.run([node, str(ROOT / "integration" / "js" / "benchNapi.js"), str(work_file), str(steps),
-                          str(inflight), str(n_sets), str(per_call), str(max_call)], capture_output=True, text=True,
-                         env=env,
-                         timeout=1200)
+                          str(inflight), str(n_sets), str(per_call), str(max_call), devices], capture_output=True,
+                         text=True, env=env, timeout=1200)
     if out.returncode != 0:
         raise SystemExit(f"benchNapi.js failed: {out.stderr[-2000:]}")
     return json.loads(out.stdout.strip().splitlines()[-1])
@@ -747,6 +749,16 @@ def _mapped_hip() -> list[str]:
     from lodestar_amd.native import mapped_hip_runtime
 
     return mapped_hip_runtime()
+
+
+def _library_hip() -> str | None:
+    """the libamdhip64 the library's HIP calls bind to (native.library_hip_runtime)"""
+    from lodestar_amd.native import library_hip_runtime
+
+    try:
+        return library_hip_runtime()
+    except Exception:  # noqa: BLE001 - a stand-in run without the library
+        return None
 
 
 def _free_port() -> int:
@@ -844,6 +856,9 @@ def main() -> None:
                     help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "
                          "its own chunks and verdicts)")
     ap.add_argument("--mode", choices=("cfg2", "sharded", "napi", "cfg4", "cfg5"), default="cfg2")
+    ap.add_argument("--devices", default="0",
+                    help="--mode napi: the JS adapter's device slots, comma-separated (one verifier per node; '0,0' "
+                         "= two slots on one GPU); --inflight contexts are spread over them")
     ap.add_argument("--shape", choices=("cfg2", "cfg4", "cfg5"), default="cfg2",
                     help="--mode sharded: the sets of the split call (cfg2 all-valid single sets; cfg4 the range-sync "
                          "mix with aggregates and invalid sets; cfg5 committee-shared roots with invalid sets)")
@@ -877,6 +892,10 @@ def main() -> None:
     ap.add_argument("--hwq-child", action="store_true",
                     help="internal: the deployable-configuration sub-record (hw_queues_N), started by the parent "
                          "before it touches the GPU; waits for a line on stdin, then runs the cfg2 timed region")
+    ap.add_argument("--torch-world1-child", action="store_true",
+                    help="internal: the runtime_torch_world1 sub-record (torch.cuda.set_device + a world-1 nccl group "
+                         "before the cfg2 timed region), started by the parent before it touches the GPU")
+    ap.add_argument("--no-torch-world1", action="store_true", help="skip the runtime_torch_world1 sub-record")
     ap.add_argument("--stand-in", default=None, metavar="MODULE:FACTORY",
                     help="dry run of --mode cfg4 / cfg5 without a device: ranks on gloo, contexts from this CPU "
                          "stand-in (tests only)")
@@ -898,23 +917,49 @@ def main() -> None:
     if share:
         local_rank = 0
     if world > 1:
+        # RCCL only where the path exchanges data: the split call (--mode sharded).  The
+        # shard-by-request / by-call modes (cfg2, cfg4, cfg5) have no data-path collective;
+        # their barrier and max-over-ranks reduction run on gloo, and the library is loaded
+        # BEFORE torch so it binds to /opt/rocm's HIP runtime exactly as the N = 1 line does
+        # (torch imported first would hand it torch's bundled libamdhip64 -- ROCm 7.0, the
+        # same soname -- and the scaling curve would mix a runtime change into its N = 1 ->
+        # N > 1 ratio; the line's config.runtime records which runtime ran, and the N = 1
+        # line's runtime_torch_world1 sub-record measures the cfg2 shape under torch's).
+        nccl = args.mode == "sharded" and not (args.stand_in or share)
+        if not nccl and not args.stand_in:
+            from lodestar_amd._abi import load_library
+
+            load_library()
         import torch.distributed as dist
 
-        if args.stand_in or share:
-            dist.init_process_group("gloo")
-        else:
+        if nccl:
             import torch
 
             torch.cuda.set_device(local_rank)
             device = f"cuda:{local_rank}"
             dist.init_process_group("nccl")
+        else:
+            dist.init_process_group("gloo")
+    elif args.torch_world1_child:
+        # the runtime_torch_world1 sub-record (started before the parent's first GPU call,
+        # released after it): torch's HIP runtime and a world-1 RCCL group, as a rank of the
+        # nccl modes has them, around the cfg2 timed region
+        if sys.stdin.readline().strip() != "go":
+            sys.exit(3)
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        device = "cuda:0"
+        dist.init_process_group("nccl", rank=0, world_size=1)
 
     def barrier_sync():
         if dist is not None:
-            import torch
-
             dist.barrier()
-            torch.cuda.synchronize()
+            if device is not None:
+                import torch
+
+                torch.cuda.synchronize()
 
     if args.stand_in:
         if args.mode not in ("cfg4", "cfg5"):
@@ -937,8 +982,20 @@ def main() -> None:
         args.probe_only = True
         if sys.stdin.readline().strip() != "go":  # the parent's go: its own GPU work is done
             sys.exit(3)  # the parent ended without releasing this child: touch nothing
+    elif args.torch_world1_child:
+        args.probe_only = True
     elif (world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records
-          and not args.probe_only and args.hw_queues):
+          and not args.probe_only):
+        if not args.no_torch_world1:
+            env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+            env.pop("WORLD_SIZE", None)
+            hwq_children["torch_world1"] = subprocess.Popen(
+                [sys.executable, str(Path(__file__).resolve()), "--torch-world1-child", "--inflight",
+                 str(args.inflight), "--calls-per-pass", str(args.calls_per_pass), "--steps",
+                 str(max(3, args.steps // 3)), "--warmup", "1", "--sets", str(args.sets)],
+                env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    if (world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records and not args.probe_only
+            and args.hw_queues and not args.hwq_child and not args.torch_world1_child):
         for q in args.hw_queues.split(","):
             env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
             if q != "unset":
@@ -957,11 +1014,36 @@ def main() -> None:
                 p.wait()
 
 
-def run_hwq_children(children: dict) -> dict:
+def run_hwq_children(children: dict, value: float | None = None) -> dict:
     """Release each deployable-configuration child in turn (this process's GPU work is
-    over) and collect its line: sets/s and ms per call at its hardware-queue count."""
+    over) and collect its line: sets/s and ms per call at its hardware-queue count, or
+    under torch's HIP runtime with a world-1 RCCL group (runtime_torch_world1)."""
     res = {}
     for q, p in children.items():
+        if q == "torch_world1":
+            try:
+                out, err = p.communicate("go\n", timeout=300)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+                res["runtime_torch_world1"] = {"error": "timed out"}
+                continue
+            lines = [ln for ln in out.splitlines() if ln.lstrip().startswith("{")]
+            if p.returncode != 0 or not lines:
+                res["runtime_torch_world1"] = {"error": f"exit {p.returncode}: {err[-400:]}"}
+                continue
+            d = json.loads(lines[-1])
+            res["runtime_torch_world1"] = {
+                "sets_per_s": d["value"], "ms_per_call": d["ms_per_step"], "steps": d["steps"],
+                "contexts": d["config"]["contexts_per_gpu"], "calls_per_pass": d["config"]["calls_per_pass"],
+                "runtime": d["config"].get("runtime"),
+                "ratio_to_value": round(d["value"] / value, 4) if value else None,
+                "note": "the headline's cfg2 shape in a child process that called torch.cuda.set_device(0) and "
+                        "started a world-1 nccl (RCCL) group first, so the library runs on torch's bundled HIP "
+                        "runtime, as a rank of the nccl modes does; the N > 1 cfg2 / cfg4 / cfg5 ranks instead "
+                        "load the library before torch and use gloo for their barrier (no data-path collective), "
+                        "so they run on the same runtime as the headline"}
+            continue
         try:
             out, err = p.communicate("go\n", timeout=300)
         except subprocess.TimeoutExpired:
@@ -1090,8 +1172,10 @@ def _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, 
                 c.close()
             ctxs = []
             max_call = len(sets)
-            batched = run_napi(wf, args.steps, args.inflight, len(sets), args.sets, max_call)
-            res = run_napi(wf, args.steps, args.inflight, len(sets), 1, max_call)
+            slots = len(args.devices.split(","))
+            per_slot = max(1, args.inflight // slots)  # the same contexts in total, spread over the slots
+            batched = run_napi(wf, args.steps, per_slot, len(sets), args.sets, max_call, args.devices)
+            res = run_napi(wf, args.steps, per_slot, len(sets), 1, max_call, args.devices)
         value, elapsed = res["sets_per_s"], res["elapsed_s"]
         stage_ms = np.zeros(8)
         extra["napi"] = {"per_set_calls": res, "calls_of_1024_sets": batched,
@@ -1100,14 +1184,15 @@ def _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, 
         config = {"workload": "cfg2 through the N-API addon + JS GpuBlsVerifier: one verifySignatureSets([set], "
                               f"{{batchable: true}}) per set, buffered and coalesced into GPU calls of up to {max_call} "
                               "sets", "sets_per_step_per_gpu": res.get("sets_per_step"), "contexts": args.inflight,
-                  "parallelism": "napi x1"}
+                  "devices": args.devices, "contexts_per_slot": per_slot,
+                  "parallelism": f"napi x1 ({slots} device slot(s): {args.devices})"}
         scaling = "weak"
 
     from lodestar_amd.native import mapped_hip_runtime
 
     # which HIP runtime the library runs under (torch's bundled copy once a rank has
     # initialised torch.cuda / RCCL, /opt/rocm's otherwise) and the process group
-    config["runtime"] = {"hip_runtime": mapped_hip_runtime(),
+    config["runtime"] = {"hip_runtime": mapped_hip_runtime(), "library_hip_runtime": _library_hip(),
                          "process_group": ({"backend": dist.get_backend(), "world": dist.get_world_size()}
                                            if dist is not None and dist.is_initialized() else None)}
     out = None
@@ -1269,7 +1354,7 @@ def _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, 
                                cfg4_cpp=args.cfg4_calls_per_pass, cfg5_sets=args.cfg5_sets,
                                cfg5_roots=args.cfg5_roots))
     if hwq_children:
-        out.update(run_hwq_children(hwq_children))
+        out.update(run_hwq_children(hwq_children, value))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

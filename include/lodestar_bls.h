@@ -121,9 +121,14 @@ const char* bls_gpu_init_error(void);
  * bls_gpu_set_scratch_budget). */
 typedef struct bls_admission {
   uint32_t contexts_normal, contexts_high; /* open contexts on the device */
-  uint32_t hw_queues;                      /* GPU_MAX_HW_QUEUES (4 when unset) */
+  uint32_t hw_queues;                      /* the runtime's hardware queues per priority (below) */
   uint32_t queues_in_use;
   uint64_t scratch_per_queue, scratch_reserved, scratch_budget; /* bytes */
+  uint32_t hw_queues_known;                /* 1: hw_queues is the runtime's count (the variable's value when the
+                                              runtime initialised under this library's first context, or the
+                                              caller's argument); 0: unknown -- HIP was initialised before that
+                                              context, hw_queues is the variable's value now (4 when unset);
+                                              2: no context yet, hw_queues is what the runtime will read */
 } bls_admission;
 
 /* The accounting alone (no device needed): 0 if n_normal + n_high contexts are
@@ -135,6 +140,17 @@ int bls_gpu_admission(int device, bls_admission* out);
 const char* bls_scratch_worst_kernel(void);
 /* Override the budget for this process (0 restores the default / environment). */
 void bls_gpu_set_scratch_budget(uint64_t bytes);
+
+/* Ask the HIP runtime for n hardware queues per priority (one per verifier context, so
+ * contexts do not serialise on HIP's default 4: 12 contexts x 22 calls run 2.27M sets/s
+ * on 4 queues, 3.65M on 24).  The runtime reads GPU_MAX_HW_QUEUES once, when it
+ * initialises; this sets the variable to n when it is unset and the runtime is not up
+ * yet.  The library never writes the environment on its own: call this before any HIP
+ * use in the process, from one thread (setenv).  Returns 0 applied, 1 left alone (the
+ * variable is already set: the host's choice stands), 2 too late (the runtime is up and
+ * keeps its count), -2 for n == 0.  The Python and JS wrappers call it (or set the
+ * variable) as they load the library unless $BLS_KEEP_HW_QUEUES=1. */
+int bls_gpu_request_hw_queues(uint32_t n);
 
 /* Release device memory and streams (IBlsVerifier.close, index.ts:176-197). */
 void bls_gpu_close(bls_gpu_ctx* ctx);

@@ -7,8 +7,10 @@
  * setsPerCall sets, sync/range/range.ts:191-214).  A step submits inflight x nSets
  * sets; two steps are kept outstanding so the contexts never wait for the JS side.
  *
- *   node benchNapi.js work.json steps contexts nSets [setsPerCall [maxSetsPerCall]]   -> one JSON line
- * (maxSetsPerCall: sets per GPU call the adapter coalesces queued jobs into)
+ *   node benchNapi.js work.json steps contexts nSets [setsPerCall [maxSetsPerCall [devices]]]   -> one JSON line
+ * (maxSetsPerCall: sets per GPU call the adapter coalesces queued jobs into; devices: the
+ * adapter's device slots, comma-separated -- "0,0" runs two slots on one GPU; `contexts`
+ * is per slot)
  */
 const fs = require("fs");
 const {GpuBlsVerifier} = require("./gpuBlsVerifier.js");
@@ -20,15 +22,16 @@ async function main() {
   const nSets = Number(nSetsS);
   const perCall = Number(process.argv[6] || 1);
   const maxSetsPerCall = Number(process.argv[7] || 1024);
+  const devices = String(process.argv[8] || "0").split(",").map(Number);
   const data = JSON.parse(fs.readFileSync(file, "utf8"));
   const sets = data.sets.map((s) => ({
     pubkeyIndices: [s.idx],
     signingRoot: Buffer.from(s.msg, "hex"),
     signature: Buffer.from(s.sig, "hex"),
   }));
-  const pool = new GpuBlsVerifier({contexts: inflight, maxSetsPerCall});
+  const pool = new GpuBlsVerifier({contexts: inflight, maxSetsPerCall, devices});
   pool.loadPubkeys(Buffer.from(data.pubkeys48, "hex"));
-  const per = inflight * nSets * Math.max(1, Math.round(maxSetsPerCall / nSets));
+  const per = devices.length * inflight * nSets * Math.max(1, Math.round(maxSetsPerCall / nSets));
   const calls = [];
   for (let k = 0; k < per; k += perCall) {
     const c = [];
@@ -52,7 +55,8 @@ async function main() {
   await pool.close();
   console.log(JSON.stringify({sets_per_s: (steps * per) / dt, elapsed_s: dt, steps, sets_per_step: per,
                               sets_per_call: perCall, max_sets_per_gpu_call: maxSetsPerCall, contexts: inflight,
-                              gpu_calls: st.jobGroupsStarted, jobs: st.jobsStarted}));
+                              gpu_calls: st.jobGroupsStarted, jobs: st.jobsStarted, devices,
+                              slot_sets: pool.slotStats.map((x) => x.sets)}));
 }
 
 main().catch((e) => {

@@ -10,6 +10,10 @@
  *                   setPkOffsets?, pkIndices?, pubkeys?, signatureLens?, seed?})
  *          -> Promise<Int32Array verdicts>   (1 valid, 0 invalid, -code error)
  *   verifySync(handle, request) -> Int32Array   (the same on the calling thread)
+ *   partial(handle, request, setIndexBase) -> Promise<{partial: Uint8Array(576) | null, status,
+ *          errClass, errIndex}>   (bls_gpu_partial: a shard of a call split across devices;
+ *          request.seed must hold the call's 32-byte seed)
+ *   finalCheck(handle, Uint8Array partials (576 B each)) -> Promise<boolean>   (bls_gpu_final_check)
  *   close(handle)
  *
  * The verdict array carries the worker's BlsWorkResult bookkeeping (types.ts:26-38) as
@@ -168,7 +172,10 @@ static napi_value js_load_pubkeys(napi_env env, napi_callback_info info) {
   return out;
 }
 
+enum { JOB_VERIFY = 0, JOB_PARTIAL = 1, JOB_FINAL = 2 };
+
 typedef struct {
+  int kind;
   bls_handle* h;
   bls_gpu_ctx* ctx;
   bls_batch batch;
@@ -178,6 +185,14 @@ typedef struct {
   bls_stats stats;
   double t_start_ns, t_end_ns;
   int rc;
+  /* JOB_PARTIAL / JOB_FINAL */
+  uint32_t base;
+  uint8_t part[576];
+  int32_t status;
+  uint32_t err_info[2];
+  const uint8_t* partials;
+  uint32_t n_partials;
+  int32_t verdict;
   napi_deferred deferred;
   napi_async_work work;
 } verify_job;
@@ -207,7 +222,12 @@ static void verify_execute(napi_env env, void* data) {
   (void)env;
   verify_job* j = (verify_job*)data;
   j->t_start_ns = mono_ns();
-  j->rc = bls_gpu_verify(j->ctx, &j->batch, j->verdicts, &j->stats);
+  if (j->kind == JOB_PARTIAL)
+    j->rc = bls_gpu_partial(j->ctx, &j->batch, j->base, j->part, &j->status, j->err_info, &j->stats);
+  else if (j->kind == JOB_FINAL)
+    j->rc = bls_gpu_final_check(j->ctx, j->partials, j->n_partials, &j->verdict);
+  else
+    j->rc = bls_gpu_verify(j->ctx, &j->batch, j->verdicts, &j->stats);
   j->t_end_ns = mono_ns();
 }
 
@@ -216,11 +236,41 @@ static void verify_complete(napi_env env, napi_status status, void* data) {
   if (status != napi_ok || j->rc != 0) {
     napi_value msg, err;
     char text[640];
-    snprintf(text, sizeof(text), "bls_gpu_verify failed (rc %d, status %d): %s", j->rc, (int)status,
+    snprintf(text, sizeof(text), "%s failed (rc %d, status %d): %s",
+             j->kind == JOB_PARTIAL ? "bls_gpu_partial" : (j->kind == JOB_FINAL ? "bls_gpu_final_check" : "bls_gpu_verify"),
+             j->rc, (int)status,
              j->rc ? bls_gpu_last_error(j->ctx) : "cancelled");
     napi_create_string_utf8(env, text, NAPI_AUTO_LENGTH, &msg);
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, j->deferred, err);
+  } else if (j->kind == JOB_PARTIAL) {
+    napi_value out, v;
+    napi_create_object(env, &out);
+    if (j->status == 0) {
+      napi_value ab;
+      void* dst;
+      napi_create_arraybuffer(env, 576, &dst, &ab);
+      memcpy(dst, j->part, 576);
+      napi_create_typedarray(env, napi_uint8_array, 576, ab, 0, &v);
+    } else {
+      napi_get_null(env, &v);
+    }
+    napi_set_named_property(env, out, "partial", v);
+    napi_create_int32(env, j->status, &v);
+    napi_set_named_property(env, out, "status", v);
+    napi_create_uint32(env, j->status ? j->err_info[0] : 3u, &v);
+    napi_set_named_property(env, out, "errClass", v);
+    napi_create_uint32(env, j->status ? j->err_info[1] : 0u, &v);
+    napi_set_named_property(env, out, "errIndex", v);
+    napi_create_double(env, j->t_start_ns, &v);
+    napi_set_named_property(env, out, "workerStartNs", v);
+    napi_create_double(env, j->t_end_ns, &v);
+    napi_set_named_property(env, out, "workerEndNs", v);
+    napi_resolve_deferred(env, j->deferred, out);
+  } else if (j->kind == JOB_FINAL) {
+    napi_value out;
+    napi_get_boolean(env, j->verdict == 1, &out);
+    napi_resolve_deferred(env, j->deferred, out);
   } else {
     napi_value ab, out;
     void* dst;
@@ -285,6 +335,21 @@ static int parse_request(napi_env env, napi_value req, bls_batch* b) {
   return 0;
 }
 
+/* queue j on a libuv worker: keep = the object holding the input buffers */
+static napi_value queue_job(napi_env env, bls_handle* h, verify_job* j, napi_value handle, napi_value keep) {
+  j->h = h;
+  j->ctx = h->ctx;
+  napi_value promise, name;
+  CHECK(env, napi_create_reference(env, keep, 1, &j->keep));
+  CHECK(env, napi_create_reference(env, handle, 1, &j->keep_handle));
+  CHECK(env, napi_create_promise(env, &j->deferred, &promise));
+  CHECK(env, napi_create_string_utf8(env, "lodestar_bls_verify", NAPI_AUTO_LENGTH, &name));
+  CHECK(env, napi_create_async_work(env, NULL, name, verify_execute, verify_complete, j, &j->work));
+  CHECK(env, napi_queue_async_work(env, j->work));
+  h->inflight += 1;
+  return promise;
+}
+
 static napi_value js_verify(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -297,19 +362,55 @@ static napi_value js_verify(napi_env env, napi_callback_info info) {
   bls_batch b;
   if (parse_request(env, argv[1], &b)) return NULL;
   verify_job* j = (verify_job*)calloc(1, sizeof(verify_job));
-  j->h = h;
-  j->ctx = h->ctx;
+  j->kind = JOB_VERIFY;
   j->batch = b;
   j->verdicts = (int32_t*)calloc(b.n_reqs ? b.n_reqs : 1, 4);
-  napi_value promise, name;
-  CHECK(env, napi_create_reference(env, argv[1], 1, &j->keep));
-  CHECK(env, napi_create_reference(env, argv[0], 1, &j->keep_handle));
-  CHECK(env, napi_create_promise(env, &j->deferred, &promise));
-  CHECK(env, napi_create_string_utf8(env, "lodestar_bls_verify", NAPI_AUTO_LENGTH, &name));
-  CHECK(env, napi_create_async_work(env, NULL, name, verify_execute, verify_complete, j, &j->work));
-  CHECK(env, napi_queue_async_work(env, j->work));
-  h->inflight += 1;
-  return promise;
+  return queue_job(env, h, j, argv[0], argv[1]);
+}
+
+/* partial(handle, request, setIndexBase) -> Promise<{partial, status, errClass, errIndex}>:
+ * bls_gpu_partial on a libuv worker -- one device's shard of a call split across the
+ * devices of the node (gpuBlsVerifier.js splitCall). */
+static napi_value js_partial(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_handle* h = argc >= 3 ? get_handle(env, argv[0]) : NULL;
+  uint32_t base = 0;
+  if (!h || napi_get_value_uint32(env, argv[2], &base) != napi_ok) {
+    napi_throw_type_error(env, NULL, "partial(handle, request, setIndexBase): no live handle (closed?)");
+    return NULL;
+  }
+  bls_batch b;
+  if (parse_request(env, argv[1], &b)) return NULL;
+  if (!b.seed || b.n_sets == 0) {
+    napi_throw_range_error(env, NULL, "partial: the request needs >= 1 set and the call's 32-byte seed");
+    return NULL;
+  }
+  verify_job* j = (verify_job*)calloc(1, sizeof(verify_job));
+  j->kind = JOB_PARTIAL;
+  j->batch = b;
+  j->base = base;
+  return queue_job(env, h, j, argv[0], argv[1]);
+}
+
+/* finalCheck(handle, partials) -> Promise<boolean>: FE(prod partials) == 1, bls_gpu_final_check. */
+static napi_value js_final_check(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bls_handle* h = argc >= 2 ? get_handle(env, argv[0]) : NULL;
+  void* p = NULL;
+  size_t bytes = 0;
+  if (!h || view_of(env, argv[1], &p, &bytes) || !p || bytes == 0 || bytes % 576) {
+    napi_throw_type_error(env, NULL, "finalCheck(handle, Uint8Array of 576-byte partials)");
+    return NULL;
+  }
+  verify_job* j = (verify_job*)calloc(1, sizeof(verify_job));
+  j->kind = JOB_FINAL;
+  j->partials = (const uint8_t*)p;
+  j->n_partials = (uint32_t)(bytes / 576);
+  return queue_job(env, h, j, argv[0], argv[1]);
 }
 
 /* verifySync(handle, request) -> Int32Array: the same call on the calling thread, for the
@@ -388,6 +489,8 @@ static napi_value module_init(napi_env env, napi_value exports) {
       {"verify", NULL, js_verify, NULL, NULL, NULL, napi_default, NULL},
       {"verifySync", NULL, js_verify_sync, NULL, NULL, NULL, napi_default, NULL},
       {"sszRoots", NULL, js_ssz_roots, NULL, NULL, NULL, napi_default, NULL},
+      {"partial", NULL, js_partial, NULL, NULL, NULL, napi_default, NULL},
+      {"finalCheck", NULL, js_final_check, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
   return exports;

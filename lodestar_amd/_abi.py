@@ -69,6 +69,7 @@ SYMBOLS = (
     "bls_gpu_admission",
     "bls_scratch_worst_kernel",
     "bls_gpu_set_scratch_budget",
+    "bls_gpu_request_hw_queues",
 )
 ERR_ADMISSION = -4  # BLS_ERR_ADMISSION: the context would push the runtime's scratch past the budget
 # SSZ kinds of bls_gpu_ssz_roots (low 8 bits: serialized size)
@@ -126,6 +127,7 @@ class BlsAdmission(ctypes.Structure):
         ("scratch_per_queue", ctypes.c_uint64),
         ("scratch_reserved", ctypes.c_uint64),
         ("scratch_budget", ctypes.c_uint64),
+        ("hw_queues_known", ctypes.c_uint32),
     ]
 
 
@@ -207,10 +209,14 @@ def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
         lib.bls_scratch_worst_kernel.restype = ctypes.c_char_p
         lib.bls_gpu_set_scratch_budget.argtypes = [ctypes.c_uint64]
         lib.bls_gpu_set_scratch_budget.restype = None
+        lib.bls_gpu_request_hw_queues.argtypes = [u32]
+        lib.bls_gpu_request_hw_queues.restype = i32
     return lib
 
 
 _LIB: ctypes.CDLL | None = None
+DEFAULT_HW_QUEUES = 24
+HW_QUEUES_REQUEST: int | None = None  # bls_gpu_request_hw_queues' code at load (None: not asked)
 
 
 def load_library() -> ctypes.CDLL:
@@ -222,5 +228,15 @@ def load_library() -> ctypes.CDLL:
                 f"{LIB_PATH} is missing: build it with `python -m lodestar_amd.build` "
                 "(or __graft_entry__.build()); there is no CPU fallback"
             )
-        _LIB = bind(ctypes.CDLL(str(LIB_PATH)))
+        lib = bind(ctypes.CDLL(str(LIB_PATH)))
+        # one hardware queue per context (the runtime reads the count once, when it
+        # initialises): the host's request, made here before this process's first HIP
+        # call through the library; $BLS_KEEP_HW_QUEUES=1 leaves HIP's default.  The
+        # returned code says whether it applied (bls_gpu_request_hw_queues).
+        global HW_QUEUES_REQUEST
+        if not os.environ.get("BLS_KEEP_HW_QUEUES"):
+            HW_QUEUES_REQUEST = int(lib.bls_gpu_request_hw_queues(DEFAULT_HW_QUEUES))
+            if HW_QUEUES_REQUEST == 0:
+                os.environ["GPU_MAX_HW_QUEUES"] = str(DEFAULT_HW_QUEUES)  # Python's view of the C environment
+        _LIB = lib
     return _LIB

@@ -43,7 +43,6 @@ def sources() -> list[Path]:
 # (the round-3 variants that lost were removed from the sources; their A/B records stay
 # under profiles/r03_ab_*.json)
 VARIANTS: dict[str, list[str] | dict[str, list[str]]] = {
-    "mlflz": ["-DBLS_LAZY_MLF=1"],   # both Miller-loop kernels in the lazy 28-bit-digit form (slower, k_mlq.hip)
     # (a variant may also give flags per translation unit, {file stem: flags}; LLVM's
     # iterative-ilp / iterative-minreg schedulers on k_mlq.hip alone measured slower /
     # level, profiles/r05_ab_sched_strategy.json)
@@ -123,6 +122,16 @@ def scratch_per_queue(table: list[dict]) -> tuple[int, str]:
     stream; the fixture and probe kernels, FIXTURE_TUS / FIXTURE_KERNELS, are left out)."""
     path = [k for k in table if k.get("tu") not in FIXTURE_TUS and _plain_name(k["name"]) not in FIXTURE_KERNELS]
     worst = max(path, key=lambda k: k["device_scratch_bytes"])
+    # the fixture kernels DO run on verifier contexts' streams (bench and tests sign and
+    # probe through them), so admission stays right only while none of them needs more
+    # than the verify path's deepest kernel (ADVICE r5): refuse the build otherwise
+    fixtures = [k for k in table if k not in path]
+    deepest = max(fixtures, key=lambda k: k["device_scratch_bytes"], default=None)
+    if deepest is not None and deepest["device_scratch_bytes"] > worst["device_scratch_bytes"]:
+        raise RuntimeError(
+            f"fixture kernel {_plain_name(deepest['name'])} reserves {deepest['device_scratch_bytes']} B of scratch per "
+            f"queue, more than the verify path's deepest ({_plain_name(worst['name'])}, "
+            f"{worst['device_scratch_bytes']} B): the admission figure would under-count; shrink it or count it")
     return worst["device_scratch_bytes"], _plain_name(worst["name"])
 
 

@@ -23,6 +23,7 @@
 #include <string.h>
 #include <sys/random.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <dlfcn.h>
 #include <stdlib.h>
@@ -343,26 +344,66 @@ std::atomic<uint64_t> g_adm_budget_override{0};
 thread_local char g_init_err[512];
 
 // The HIP runtime maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues per
-// priority (HIP's default 4), and streams sharing a queue serialise: 12 contexts x 22
-// calls give 2.27M sets/s on 4 queues against 3.42M on 16 and 3.65M on 24
-// (bench.py hw_queues_4 / hw_queues_16, profiles/r05_bench_first.json).  When the
-// variable is unset as the library loads, it is set to BLS_DEFAULT_HW_QUEUES here, before
-// the library's first HIP call, so a host that configures nothing (the beacon node
-// loading the N-API addon) gets a queue per context; an explicit value is kept, and
-// $BLS_KEEP_HW_QUEUES=1 leaves the runtime's default alone.  (A process whose HIP runtime
-// was initialised before this library loaded keeps the queues it started with; the
-// admission arithmetic then over-counts queues, the safe direction.)
-#define BLS_DEFAULT_HW_QUEUES "24"
-__attribute__((constructor)) void bls_default_hw_queues() {
-  const char* e = getenv("GPU_MAX_HW_QUEUES");
-  if ((e && *e) || getenv("BLS_KEEP_HW_QUEUES")) return;
-  setenv("GPU_MAX_HW_QUEUES", BLS_DEFAULT_HW_QUEUES, 0);
+// priority (HIP's default 4), read once when the runtime initialises, and streams
+// sharing a queue serialise: 12 contexts x 22 calls give 2.27M sets/s on 4 queues
+// against 3.42M on 16 and 3.65M on 24 (bench.py hw_queues_4 / hw_queues_16,
+// profiles/r05_bench_first.json).  The library never writes the environment by itself
+// (a load-time setenv would race getenv on a multithreaded host's other threads and leak
+// into every child process): the host asks with bls_gpu_request_hw_queues before any
+// HIP use (the Python and JS wrappers do as they load the library), and the library
+// records what the runtime really got -- the variable's value when the runtime
+// initialised, if that happened under this library's first context, or "unknown" when
+// another component of the process had initialised HIP first (hw_queues_known = 0 in
+// bls_admission, and one warning on stderr when the runtime then most likely kept
+// HIP's 4 queues).
+namespace {
+// the render / KFD device is open once the ROCm runtime initialised in this process
+bool hip_runtime_up() {
+  char path[64], target[64];
+  for (int fd = 0; fd < 4096; ++fd) {
+    snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
+    const ssize_t n = readlink(path, target, sizeof(target) - 1);
+    if (n <= 0) continue;
+    target[n] = 0;
+    if (strcmp(target, "/dev/kfd") == 0) return true;
+  }
+  return false;
 }
 
-uint32_t hw_queues_env() {
-  const char* e = getenv("GPU_MAX_HW_QUEUES");
+uint32_t parse_hwq(const char* e) {
   const long v = e && *e ? strtol(e, nullptr, 10) : 0;
   return v > 0 ? (uint32_t)v : 4u;
+}
+
+bool g_hip_up_at_load = false;  // HIP was initialised before this library loaded
+// the runtime's queue count: fixed at this library's first context (when the runtime
+// came up under it, hwq_known = 1) or guessed from the environment (hwq_known = 0)
+std::once_flag g_hwq_once;
+uint32_t g_hwq_effective = 0;
+bool g_hwq_known = false;
+
+__attribute__((constructor)) void bls_record_runtime_state() { g_hip_up_at_load = hip_runtime_up(); }
+
+// called by bls_gpu_init_priority before its first HIP call (g_adm_mu held)
+void note_runtime_queues() {
+  std::call_once(g_hwq_once, [] {
+    const bool up = g_hip_up_at_load || hip_runtime_up();
+    const char* e = getenv("GPU_MAX_HW_QUEUES");
+    g_hwq_effective = parse_hwq(e);
+    g_hwq_known = !up;
+    if (up && !(e && *e))
+      fprintf(stderr,
+              "lodestar_bls: warning: the HIP runtime was initialised before this library's first context, "
+              "with GPU_MAX_HW_QUEUES unset: its streams share HIP's default 4 hardware queues per priority, so "
+              "more than 4 verifier contexts serialise (set GPU_MAX_HW_QUEUES before the process's first HIP "
+              "call, or call bls_gpu_request_hw_queues first; INTEGRATION.md section 4)\n");
+  });
+}
+}  // namespace
+
+uint32_t hw_queues_env() {
+  if (g_hwq_effective) return g_hwq_effective;
+  return parse_hwq(getenv("GPU_MAX_HW_QUEUES"));
 }
 
 uint64_t scratch_budget() {
@@ -390,6 +431,7 @@ int bls_scratch_plan(uint32_t n_normal, uint32_t n_high, uint32_t hw_queues, bls
   a.contexts_normal = n_normal;
   a.contexts_high = n_high;
   a.hw_queues = hw_queues ? hw_queues : hw_queues_env();
+  a.hw_queues_known = hw_queues ? 1u : (g_hwq_effective ? (g_hwq_known ? 1u : 0u) : 2u);
   a.queues_in_use = (n_normal < a.hw_queues ? n_normal : a.hw_queues) + (n_high < a.hw_queues ? n_high : a.hw_queues);
   a.scratch_per_queue = BLS_SCRATCH_PER_QUEUE;
   a.scratch_reserved = (uint64_t)a.queues_in_use * a.scratch_per_queue;
@@ -399,6 +441,16 @@ int bls_scratch_plan(uint32_t n_normal, uint32_t n_high, uint32_t hw_queues, bls
 }
 
 const char* bls_scratch_worst_kernel(void) { return BLS_SCRATCH_WORST_KERNEL; }
+
+int bls_gpu_request_hw_queues(uint32_t n) {
+  if (n == 0) return -2;
+  const char* e = getenv("GPU_MAX_HW_QUEUES");
+  if (e && *e) return 1;  // the host's own choice stands
+  if (g_hip_up_at_load || g_hwq_effective || hip_runtime_up()) return 2;  // too late: the runtime has its count
+  char v[16];
+  snprintf(v, sizeof(v), "%u", n);
+  return setenv("GPU_MAX_HW_QUEUES", v, 0) == 0 ? 0 : -1;
+}
 
 int bls_gpu_admission(int device, bls_admission* out) {
   if (device < 0 || device >= ADM_MAX_DEV) return -2;
@@ -430,6 +482,7 @@ int bls_gpu_init_priority(int device, int priority, bls_gpu_ctx** out) {
   {
     // admit first: a refused context never creates its stream (no queue, no reservation)
     std::lock_guard<std::mutex> g(g_adm_mu);
+    note_runtime_queues();  // before this library's first HIP call
     bls_admission a;
     const uint32_t nn = g_adm_normal[device] + (high ? 0u : 1u), nh = g_adm_high[device] + (high ? 1u : 0u);
     if (bls_scratch_plan(nn, nh, 0, &a) != 0) {

@@ -22,32 +22,14 @@
 #include <stdlib.h>
 
 #include "../launchers.hpp"
-#include "bls/lazy12.hpp"
 #include "bls/pairing.hpp"
-
-// BLS_LAZY_MLF (build variant `mlflz`, default 0): both Miller-loop kernels in the lazy
-// 28-bit-digit form (bls/lazy12.hpp): k_mlq's T, Q, P and the stored lines as 14 signed
-// digits, k_mlf's f reduced once per step (lz_reduce), every product on digits, additions
-// digit by digit.  Bit-exact (GPU tests green), but SLOWER: 3.13M vs 3.59M sets/s at 12 x 22,
-// the Miller loops' stage 42.5 vs 29.2 ms, 2.22M vs 2.36M at 4 x 16 (profiles/r05_ab_lazy_ml.json)
-// -- 14-word elements and ~2 carry passes per product (lazy12.hpp: the signed 64-bit columns
-// admit operands of at most ~8.5 x (2^28)^2 digit products) outweigh the ~94 instructions each
-// product saves: k_mlf spills 2,032 B/lane (864 in the limb form).  The exponentiations,
-// pure product chains with one live element, keep the lazy form (field.hpp fp_pow_const).
-#ifndef BLS_LAZY_MLF
-#define BLS_LAZY_MLF 0
-#endif
 
 using namespace bls;
 
 namespace {
 
 constexpr int ML_EVENTS = 68;          // 63 doublings + 5 additions
-#if BLS_LAZY_MLF
-constexpr int LINE_WORDS = 6 * 14;     // l0, l2, l3 (Fp2 each) as lazy digits (lazy28.hpp, |value| < 2 p)
-#else
 constexpr int LINE_WORDS = 6 * 12;     // l0, l2, l3 (Fp2 each) as 32-bit words
-#endif
 
 __device__ __forceinline__ bool ml_live(const PipeBufs& b, uint32_t i, uint32_t units_paired) {
   if (!b.chain_live[i]) return false;
@@ -131,101 +113,6 @@ __device__ __forceinline__ Fp12 ml_f(const uint32_t* L, uint32_t stride, uint32_
   return fp12_conj(f);
 }
 
-#if BLS_LAZY_MLF
-typedef LzN<2> LzF;  // f's coefficients and the lines between steps: |value| < 2 p
-
-// one Fp2 of a line (words w0 .. w0 + 27 of line e: k_mlq's lazy digits)
-__device__ __forceinline__ L2<LzF> load_l2(const uint32_t* L, uint32_t stride, uint32_t k, int e, int w0) {
-  L2<LzF> r;
-#pragma unroll
-  for (int w = 0; w < 14; ++w) {
-    r.c0.d[w] = (int32_t)L[line_at(stride, k, e, w0 + w)];
-    r.c1.d[w] = (int32_t)L[line_at(stride, k, e, w0 + 14 + w)];
-  }
-  return r;
-}
-__device__ __forceinline__ void store_l2(uint32_t* L, uint32_t stride, uint32_t k, int e, int w0, const L2<LzF>& a) {
-#pragma unroll
-  for (int w = 0; w < 14; ++w) {
-    L[line_at(stride, k, e, w0 + w)] = (uint32_t)a.c0.d[w];
-    L[line_at(stride, k, e, w0 + 14 + w)] = (uint32_t)a.c1.d[w];
-  }
-}
-
-__device__ __forceinline__ Fp2 l2_out(const L2<LzF>& a) { return Fp2{lz_to_fp(a.c0), lz_to_fp(a.c1)}; }
-
-// ml_f in the lazy form: the same products and order (fp12_mul_line2 for two items'
-// lines, fp12_mul_line for one, one complex squaring per bit), f reduced after each step
-__device__ __forceinline__ L12<LzF> l12_one() {
-  const LzF z = lz_widen<LzF>(lz_zero()), o = lz_widen<LzF>(lz_one());
-  const L2<LzF> z2{z, z};
-  return L12<LzF>{L6<LzF>{L2<LzF>{o, z}, z2, z2}, L6<LzF>{z2, z2, z2}};
-}
-__device__ __forceinline__ Fp12 l12_out(const L12<LzF>& f) {
-  Fp12 r;
-  r.c0 = Fp6{l2_out(f.c0.c0), l2_out(f.c0.c1), l2_out(f.c0.c2)};
-  r.c1 = Fp6{l2_out(f.c1.c0), l2_out(f.c1.c1), l2_out(f.c1.c2)};
-  return r;
-}
-
-// the line side in the lazy form (lazy12.hpp lz_dbl_line / lz_add_line): T, Q and the
-// prepared P as digits, every line stored as normalised digits
-__device__ __forceinline__ LzF lz_in(const Fp& a) { return lz_reduce(lz_from_fp(a)); }
-__device__ __forceinline__ void mlq_lz(const Fp* ch, uint32_t* L, uint32_t stride, uint32_t k) {
-  const LzF x = lz_in(ch[CH_RP + 0]), z = lz_in(ch[CH_RP + 2]);
-  const LEval<LzF> P{lz_widen<LzF>(lz_mul(x, z)), lz_in(ch[CH_RP + 1]), lz_widen<LzF>(lz_mul(lz_sqr(z), z))};
-  const L2<LzF> qx{lz_in(ch[CH_HQ + 0]), lz_in(ch[CH_HQ + 1])}, qy{lz_in(ch[CH_HQ + 2]), lz_in(ch[CH_HQ + 3])};
-  typedef Lz<3 * LZ_M28, 8> TT;  // closed under both steps (lazy12.hpp LProj)
-  LProj<TT> T{l2_widen<TT>(qx), l2_widen<TT>(qy), l2_widen<TT>(l12_one().c0.c0)};
-  L2<LzL> l[3];
-  int e = 0;
-  const uint64_t X = BLS_X_ABS;
-  for (int bit = 62; bit >= 0; --bit) {
-    lz_dbl_line(T, P, l);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) store_l2(L, stride, k, e, 28 * j, l[j]);
-    ++e;
-    if ((X >> bit) & 1ull) {
-      lz_add_line(T, qx, qy, P, l);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) store_l2(L, stride, k, e, 28 * j, l[j]);
-      ++e;
-    }
-  }
-}
-
-__device__ __forceinline__ Fp12 ml_f_lz(const uint32_t* L, uint32_t stride, uint32_t k0, uint32_t n) {
-  L12<LzF> f = l12_one();
-  int e = 0;
-  const uint64_t X = BLS_X_ABS;
-  for (int bit = 62; bit >= 0; --bit) {
-    if (bit != 62) f = l12_reduce(l12_sqr(f));
-    const int adds = (int)((X >> bit) & 1ull);
-    for (int a = 0; a <= adds; ++a) {
-      uint32_t g = 0;
-#pragma unroll 1
-      for (; g + 1 < n; g += 2) {
-        const L2<LzF> l0 = load_l2(L, stride, k0 + g, e, 0), l2 = load_l2(L, stride, k0 + g, e, 28),
-                      l3 = load_l2(L, stride, k0 + g, e, 56);
-        const L2<LzF> m0 = load_l2(L, stride, k0 + g + 1, e, 0), m2 = load_l2(L, stride, k0 + g + 1, e, 28),
-                      m3 = load_l2(L, stride, k0 + g + 1, e, 56);
-        f = l12_reduce(l12_mul_line2(f, l0, l2, l3, m0, m2, m3));
-      }
-#pragma unroll 1
-      for (; g < n; ++g) {
-        const L2<LzF> l0 = load_l2(L, stride, k0 + g, e, 0), l2 = load_l2(L, stride, k0 + g, e, 28),
-                      l3 = load_l2(L, stride, k0 + g, e, 56);
-        f = l12_reduce(l12_mul_line(f, l0, l2, l3));
-      }
-      ++e;
-    }
-  }
-  return l12_out(l12_conj(f));
-}
-#define ML_F ml_f_lz
-#else
-#define ML_F ml_f
-#endif
 
 }  // namespace
 
@@ -238,10 +125,6 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
   const uint32_t i = items ? items[k] : first + k;
   if (!ml_live(b, i, units_paired)) return;
   const Fp* ch = b.chain + (size_t)CHAIN_WORDS * i;
-#if BLS_LAZY_MLF
-  mlq_lz(ch, L, stride, k);
-  return;
-#endif
   G1J rp;
   rp.x = ch[CH_RP + 0];
   rp.y = ch[CH_RP + 1];
@@ -288,13 +171,13 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
     share = ml_live(b, i, units_paired) && i < b.indiv_vbase && b.ml_dom[i] == b.ml_dom[i0];
   }
   if (share) {
-    b.f[i0] = ML_F(L, stride, k0, n);
+    b.f[i0] = ml_f(L, stride, k0, n);
     for (uint32_t g = 1; g < n; ++g) b.f[first + k0 + g] = fp12_one();
     return;
   }
   for (uint32_t g = 0; g < n; ++g) {
     const uint32_t i = items ? items[k0 + g] : first + k0 + g;
-    if (ml_live(b, i, units_paired)) b.f[i] = ML_F(L, stride, k0 + g, 1);
+    if (ml_live(b, i, units_paired)) b.f[i] = ml_f(L, stride, k0 + g, 1);
   }
 }
 
@@ -329,72 +212,6 @@ __device__ __forceinline__ Fp12 mul_line12_pair(const Fp12& f, const Fp2& l0, co
   return fp12_line_half_join(own, pair_swap(own.m), pair_swap(own.p), h);
 }
 
-#if BLS_LAZY_MLF
-__device__ __forceinline__ LzF pair_swap(const LzF& a) {
-  LzF r;
-#pragma unroll
-  for (int w = 0; w < 14; ++w) r.d[w] = (int32_t)pair_swap((uint32_t)a.d[w]);
-  return r;
-}
-template <class T>
-__device__ __forceinline__ T pair_swap_l(const T& a) {
-  T r;
-#pragma unroll
-  for (int w = 0; w < 14; ++w) r.d[w] = (int32_t)pair_swap((uint32_t)a.d[w]);
-  return r;
-}
-template <class T>
-__device__ __forceinline__ L2<T> pair_swap(const L2<T>& a) {
-  return L2<T>{pair_swap_l(a.c0), pair_swap_l(a.c1)};
-}
-template <class T>
-__device__ __forceinline__ L6<T> pair_swap(const L6<T>& a) {
-  return L6<T>{pair_swap(a.c0), pair_swap(a.c1), pair_swap(a.c2)};
-}
-template <class T>
-__device__ __forceinline__ T lz_sel(bool c, const T& a, const T& b) {
-  T r;
-#pragma unroll
-  for (int w = 0; w < 14; ++w) r.d[w] = c ? a.d[w] : b.d[w];
-  return r;
-}
-template <class T>
-__device__ __forceinline__ L2<T> l2_sel(bool c, const L2<T>& a, const L2<T>& b) {
-  return L2<T>{lz_sel(c, a.c0, b.c0), lz_sel(c, a.c1, b.c1)};
-}
-template <class T>
-__device__ __forceinline__ L6<T> l6_sel(bool c, const L6<T>& a, const L6<T>& b) {
-  return L6<T>{l2_sel(c, a.c0, b.c0), l2_sel(c, a.c1, b.c1), l2_sel(c, a.c2, b.c2)};
-}
-// field.hpp fp12_sqr_half_* / fp12_line_half_* in the lazy form (one f over two lanes)
-__device__ __forceinline__ L12<LzF> sqr12_pair_lz(const L12<LzF>& a, bool h) {
-  const auto s0 = l6_add(a.c0, a.c1);
-  const auto s1 = l6_add(a.c0, l6_mul_v(a.c1));
-  typedef LzMax<LzMax<decltype(s0.c0.c0), decltype(s1.c0.c0)>, LzF> X;
-  const L6<X> x = l6_sel(h, l6_widen<X>(s0), l6_widen<X>(a.c0)), y = l6_sel(h, l6_widen<X>(s1), l6_widen<X>(a.c1));
-  const auto own = l6_mul(x, y);
-  const auto other = pair_swap(own);
-  const auto ab = l6_sel(h, other, own), s = l6_sel(h, own, other);
-  return l12_reduce(l12_make(l6_sub(l6_sub(s, ab), l6_mul_v(ab)), l6_add(ab, ab)));
-}
-__device__ __forceinline__ L12<LzF> mul_line12_pair_lz(const L12<LzF>& f, const L2<LzF>& l0, const L2<LzF>& l2,
-                                                        const L2<LzF>& l3, bool h) {
-  const auto s0 = l6_add(f.c0, f.c1);
-  typedef LzMax<decltype(s0.c0.c0), LzF> X;
-  const L6<X> x = l6_sel(h, l6_widen<X>(s0), l6_widen<X>(f.c0));
-  const auto s2 = l2_add(l2, l3);
-  typedef LzMax<decltype(s2.c0), LzF> Y;
-  const L2<Y> d1 = l2_sel(h, l2_widen<Y>(s2), l2_widen<Y>(l2));
-  const auto m = l6_mul_01(x, l0, d1);
-  const auto p = l2_mul(l2_sel(h, f.c1.c0, f.c1.c2), l3);
-  const auto q = l2_mul(f.c1.c1, l3);
-  const auto m_other = pair_swap(m);
-  const auto p_other = pair_swap(p);
-  const auto aa = l6_sel(h, m_other, m), t = l6_sel(h, m, m_other);
-  const auto bb = l6_make(l2_mul_xi(l2_sel(h, p_other, p)), l2_sel(h, p, p_other), q);
-  return l12_reduce(l12_make(l6_add(aa, l6_mul_v(bb)), l6_sub(l6_sub(t, aa), bb)));
-}
-#endif
 
 template <int W>
 __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlf2(
@@ -407,22 +224,6 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
   if (k >= count) return;
   const uint32_t i = items ? items[k] : first + k;
   if (!ml_live(b, i, units_paired)) return;
-#if BLS_LAZY_MLF
-  L12<LzF> f = l12_one();
-  int e = 0;
-  const uint64_t X = BLS_X_ABS;
-  for (int bit = 62; bit >= 0; --bit) {
-    if (bit != 62) f = sqr12_pair_lz(f, h);
-    const int adds = (int)((X >> bit) & 1ull);
-    for (int a = 0; a <= adds; ++a) {
-      const L2<LzF> l0 = load_l2(L, stride, k, e, 0), l2 = load_l2(L, stride, k, e, 28),
-                    l3 = load_l2(L, stride, k, e, 56);
-      f = mul_line12_pair_lz(f, l0, l2, l3, h);
-      ++e;
-    }
-  }
-  if (!h) b.f[i] = l12_out(l12_conj(f));
-#else
   Fp12 f = fp12_one();
   int e = 0;
   const uint64_t X = BLS_X_ABS;
@@ -437,7 +238,6 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
     }
   }
   if (!h) b.f[i] = fp12_conj(f);
-#endif
 }
 
 // line buffer words for a launch of `count` items (stride padded to a wavefront)

@@ -338,7 +338,7 @@ hipError_t launch_k_mln(const PipeBufs& b, const CoopEnv& env, uint32_t first, u
 // A failing pass's later Miller loops (chunk signature sums, the failed chunks' own loops,
 // the individually verified requests' sums: items that never share f) as cooperative
 // single-pair loops, one wavefront per item: ~1 ms of latency where the SIMT pair
-// k_mlq + k_mlf2 takes ~7 ms (2.6 + 4.6, profiles/r05_cfg5_fallback_coop.json), and the
+// k_mlq + k_mlf2 takes ~7 ms (2.6 + 4.6; profiles/r05_cfg5_fallback.json "step3"), and the
 // items are few.  Up to $BLS_COOP_ML_MAX items (default 8192; 0 turns it off); 0 items
 // or no ml1_1 program: hipErrorNotSupported (the caller takes the SIMT pair).
 uint32_t coop_ml_max() {

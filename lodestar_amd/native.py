@@ -7,6 +7,7 @@ library copies them into pinned staging, so nothing is retained after a call.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -45,6 +46,30 @@ def mapped_hip_runtime() -> list[str]:
             return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
     except OSError:
         return []
+
+
+class _DlInfo(ctypes.Structure):
+    _fields_ = [("dli_fname", ctypes.c_char_p), ("dli_fbase", ctypes.c_void_p), ("dli_sname", ctypes.c_char_p),
+                ("dli_saddr", ctypes.c_void_p)]
+
+
+def library_hip_runtime() -> str | None:
+    """The libamdhip64 file the library's HIP calls bind to: dlsym through the library's
+    own handle searches its dependency scope, dladdr names the object that holds the
+    symbol.  (/proc/self/maps may list two copies once torch is imported after the
+    library: torch loads its bundled one by another name and never initialises it unless
+    torch.cuda is used.)"""
+    lib = load_library()
+    try:
+        addr = ctypes.cast(lib.hipGetDeviceCount, ctypes.c_void_p).value
+    except AttributeError:
+        return None
+    info = _DlInfo()
+    libc = ctypes.CDLL(None)
+    libc.dladdr.argtypes = [ctypes.c_void_p, ctypes.POINTER(_DlInfo)]
+    if not addr or libc.dladdr(ctypes.c_void_p(addr), ctypes.byref(info)) == 0 or not info.dli_fname:
+        return None
+    return os.path.realpath(info.dli_fname.decode())
 
 
 def scratch_plan(n_normal: int, n_high: int, hw_queues: int = 0) -> tuple[bool, dict]:

@@ -15,7 +15,6 @@
 #include "bls/pairing.hpp"
 #include "bls/hash_to_curve.hpp"
 #include "bls/pipeline.hpp"
-#include "bls/lazy12.hpp"
 
 unsigned long long bls_fpm_counter = 0;
 unsigned long long bls_lz_norm_counter = 0;
@@ -527,88 +526,3 @@ void hs_lz_fp2_ops(const uint8_t* a, const uint8_t* b, uint8_t* out) {
 
 }  // extern "C"
 
-// ---- bls/lazy12.hpp: the Miller loop's f-side formulas in the lazy form ----------------
-typedef LzN<2> LzT;  // inputs brought to |value| < 2 p, as the kernels' products leave them
-static L2<LzT> rd_l2(const uint8_t* b) {
-  const Fp2 a = rd_fp2(b);
-  return L2<LzT>{lz_mul(lz_from_fp(a.c0), lz_one()), lz_mul(lz_from_fp(a.c1), lz_one())};
-}
-static L12<LzT> rd_l12(const uint8_t* b) {
-  return L12<LzT>{L6<LzT>{rd_l2(b), rd_l2(b + 2 * 96), rd_l2(b + 4 * 96)},
-                  L6<LzT>{rd_l2(b + 96), rd_l2(b + 3 * 96), rd_l2(b + 5 * 96)}};
-}
-template <class T>
-static void wr_l12(const L12<T>& f, uint8_t* b) {
-  Fp12 r;
-  r.c0 = Fp6{l2_to_fp2(f.c0.c0), l2_to_fp2(f.c0.c1), l2_to_fp2(f.c0.c2)};
-  r.c1 = Fp6{l2_to_fp2(f.c1.c0), l2_to_fp2(f.c1.c1), l2_to_fp2(f.c1.c2)};
-  wr_fp12(r, b);
-}
-extern "C" {
-// f (576 B), lines l = (l0, l2, l3), m (3 x 96 B each): out = lazy sqr, mul_line,
-// mul_line2, conj, then field.hpp's fp12_sqr, fp12_mul_line, fp12_mul_line2 (7 x 576 B)
-void hs_lz_fp12_ops(const uint8_t* fb, const uint8_t* lb, const uint8_t* mb, uint8_t* out) {
-  const auto f = rd_l12(fb);
-  const auto l0 = rd_l2(lb), l2 = rd_l2(lb + 96), l3 = rd_l2(lb + 192);
-  const auto m0 = rd_l2(mb), m2 = rd_l2(mb + 96), m3 = rd_l2(mb + 192);
-  wr_l12(l12_sqr(f), out);
-  wr_l12(l12_mul_line(f, l0, l2, l3), out + 576);
-  wr_l12(l12_mul_line2(f, l0, l2, l3, m0, m2, m3), out + 2 * 576);
-  wr_l12(l12_conj(l12_reduce(l12_sqr(f))), out + 3 * 576);
-  const Fp12 g = rd_fp12(fb);
-  const Fp2 L0 = rd_fp2(lb), L2v = rd_fp2(lb + 96), L3 = rd_fp2(lb + 192);
-  const Fp2 M0 = rd_fp2(mb), M2 = rd_fp2(mb + 96), M3 = rd_fp2(mb + 192);
-  wr_fp12(fp12_sqr(g), out + 4 * 576);
-  wr_fp12(fp12_mul_line(g, L0, L2v, L3), out + 5 * 576);
-  wr_fp12(fp12_mul_line2(g, L0, L2v, L3, M0, M2, M3), out + 6 * 576);
-}
-}  // extern "C"
-
-// pairing.hpp miller_dbl_step / miller_add_step + line evaluation against lazy12.hpp
-// lz_dbl_line / lz_add_line: Q (G2 affine, 192 B), P (G1, 96 B): runs `steps` steps of
-// each kind from T = Q; out = the last dbl line (3 x 96 B), the last add line, T (3 x 96 B)
-// for the lazy form, then the same for the reference form (2 x 864 B)
-extern "C" void hs_lz_line_steps(const uint8_t* qb, const uint8_t* pb, int steps, uint8_t* out) {
-  const G2A q = rd_g2(qb);
-  const G1A p = rd_g1(pb);
-  const G1Eval P = g1_eval_from_aff(p);
-  // lazy
-  {
-    const LEval<LzT> e1{lz_mul(lz_from_fp(P.xz), lz_one()), lz_mul(lz_from_fp(P.y), lz_one()),
-                        lz_mul(lz_from_fp(P.z3), lz_one())};
-    const L2<LzT> qx{lz_mul(lz_from_fp(q.x.c0), lz_one()), lz_mul(lz_from_fp(q.x.c1), lz_one())};
-    const L2<LzT> qy{lz_mul(lz_from_fp(q.y.c0), lz_one()), lz_mul(lz_from_fp(q.y.c1), lz_one())};
-    typedef Lz<3 * LZ_M28, 8> TT;
-    const L2<LzT> one{lz_widen<LzT>(lz_one()), lz_widen<LzT>(lz_zero())};
-    LProj<TT> t{l2_widen<TT>(qx), l2_widen<TT>(qy), l2_widen<TT>(one)};
-    L2<LzL> ld[3], la[3];
-    for (int s = 0; s < steps; ++s) {
-      lz_dbl_line(t, e1, ld);
-      lz_add_line(t, qx, qy, e1, la);
-    }
-    for (int j = 0; j < 3; ++j) {
-      wr_fp2(l2_to_fp2(ld[j]), out + 96 * j);
-      wr_fp2(l2_to_fp2(la[j]), out + 288 + 96 * j);
-    }
-    wr_fp2(l2_to_fp2(t.x), out + 576);
-    wr_fp2(l2_to_fp2(t.y), out + 672);
-    wr_fp2(l2_to_fp2(t.z), out + 768);
-  }
-  // reference
-  {
-    G2Proj T{q.x, q.y, fp2_one()};
-    Fp2 d[3], a[3];
-    for (int s = 0; s < steps; ++s) {
-      miller_dbl_step(T, d[0], d[1], d[2]);
-      miller_add_step(T, q, a[0], a[1], a[2]);
-    }
-    const Fp* ev[3] = {&P.z3, &P.xz, &P.y};
-    for (int j = 0; j < 3; ++j) {
-      wr_fp2(fp2_mul_fp(d[j], *ev[j]), out + 864 + 96 * j);
-      wr_fp2(fp2_mul_fp(a[j], *ev[j]), out + 864 + 288 + 96 * j);
-    }
-    wr_fp2(T.x, out + 864 + 576);
-    wr_fp2(T.y, out + 864 + 672);
-    wr_fp2(T.z, out + 864 + 768);
-  }
-}

@@ -32,28 +32,41 @@ def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
         abi.load_library()
 
 
-def test_default_hw_queues_set_on_load():
-    """Loading the library sets GPU_MAX_HW_QUEUES (unset) to 24 before its first HIP call,
-    so a host that configures nothing gets one hardware queue per context
-    (bls_gpu.hip bls_default_hw_queues); an explicit value is kept."""
+def test_hw_queues_requested_by_the_host_not_the_library():
+    """The library never writes the environment as it loads (a load-time setenv
+    races other threads' getenv and leaks into child processes); the host asks with
+    bls_gpu_request_hw_queues before its first HIP call -- the Python wrapper does as it
+    loads the library -- and an explicit value or $BLS_KEEP_HW_QUEUES=1 is kept.  Before
+    any context, bls_admission reports the count the runtime will read (known = 2)."""
     import os
     import subprocess
     import sys
 
-    # the C environment (os.environ is Python's snapshot from start-up; the library's
-    # constructor calls setenv)
-    code = ("import ctypes, sys; sys.path.insert(0, %r); from lodestar_amd._abi import load_library; load_library(); "
-            "libc = ctypes.CDLL(None); libc.getenv.restype = ctypes.c_char_p; "
-            "v = libc.getenv(b'GPU_MAX_HW_QUEUES'); print(v.decode() if v else None)" % str(ROOT))
+    # the C environment (os.environ is Python's snapshot from start-up)
+    getenv = ("libc = ctypes.CDLL(None); libc.getenv.restype = ctypes.c_char_p; "
+              "v = libc.getenv(b'GPU_MAX_HW_QUEUES'); ")
+    raw = ("import ctypes; lib = ctypes.CDLL(%r); " % str(LIB_PATH)) + getenv + (
+        "a = v.decode() if v else None; r = lib.bls_gpu_request_hw_queues(16); v = libc.getenv(b'GPU_MAX_HW_QUEUES'); "
+        "r2 = lib.bls_gpu_request_hw_queues(8); print(a, r, v.decode() if v else None, r2)")
+    wrapped = ("import ctypes, sys; sys.path.insert(0, %r); from lodestar_amd import _abi; "
+               "from lodestar_amd.native import admission; _abi.load_library(); " % str(ROOT)) + getenv + (
+        "a = admission(0); print(v.decode() if v else None, _abi.HW_QUEUES_REQUEST, a['hw_queues'], "
+        "a['hw_queues_known'])")
     env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "BLS_KEEP_HW_QUEUES")}
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
-    assert out.stdout.strip() == "24", out.stderr[-500:]
-    out = subprocess.run([sys.executable, "-c", code], env=dict(env, GPU_MAX_HW_QUEUES="4"), capture_output=True,
-                         text=True, timeout=120)
-    assert out.stdout.strip() == "4"
-    out = subprocess.run([sys.executable, "-c", code], env=dict(env, BLS_KEEP_HW_QUEUES="1"), capture_output=True,
-                         text=True, timeout=120)
-    assert out.stdout.strip() == "None"
+
+    def run(code, **extra):
+        out = subprocess.run([sys.executable, "-c", code], env=dict(env, **extra), capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, out.stderr[-800:]
+        return out.stdout.split()
+
+    # loading the bare library leaves the environment alone; the request applies once
+    assert run(raw) == ["None", "0", "16", "1"]
+    assert run(raw, GPU_MAX_HW_QUEUES="4") == ["4", "1", "4", "1"]
+    # the Python wrapper asks for 24 unless told not to
+    assert run(wrapped) == ["24", "0", "24", "2"]
+    assert run(wrapped, GPU_MAX_HW_QUEUES="4") == ["4", "1", "4", "2"]
+    assert run(wrapped, BLS_KEEP_HW_QUEUES="1") == ["None", "None", "4", "2"]
 
 
 def test_device_count_without_gpu():
@@ -99,3 +112,19 @@ def test_scratch_admission_accounting():
     finally:
         lib.bls_gpu_set_scratch_budget(0)
     assert scratch_plan(12, 1, 24)[1]["scratch_budget"] == 6 << 30
+
+
+def test_fixture_kernels_scratch_checked():
+    """build.scratch_per_queue counts the verify path's kernels only and refuses a build
+    whose fixture kernels (signing, probes: they run on verifier contexts' streams too)
+    would need more scratch than that figure."""
+    import pytest
+
+    from lodestar_amd.build import scratch_per_queue
+
+    table = [{"name": "_Z7k_chainv", "tu": "k_chain", "device_scratch_bytes": 100},
+             {"name": "_Z6k_signv", "tu": "k_sign", "device_scratch_bytes": 90}]
+    assert scratch_per_queue(table) == (100, "k_chain")
+    table[1]["device_scratch_bytes"] = 101
+    with pytest.raises(RuntimeError, match="fixture kernel"):
+        scratch_per_queue(table)

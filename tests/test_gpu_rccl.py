@@ -93,3 +93,54 @@ def test_rccl_world1_runtime_and_collectives():
     assert out["throughput"] == (4096.0, 0.5)
     assert out["sharded_good"] == (True, {"bad_shards": []})
     assert out["sharded_bad"] == (False, {"bad_shards": [0]})
+
+
+_GLOO_RANK = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["REPO"])
+from lodestar_amd._abi import load_library
+load_library()                       # before torch: the runtime of the N = 1 line
+import torch.distributed as dist
+dist.init_process_group("gloo", rank=0, world_size=1)
+from lodestar_amd import workloads as W
+from lodestar_amd.native import GpuContext, library_hip_runtime, pack_requests
+from lodestar_amd.shard import global_throughput
+out = {"backend": dist.get_backend()}
+with GpuContext(0) as gpu:
+    n = 1024
+    W.load_table([gpu], 64)
+    sks = W.interop_sks(64)
+    msgs = [W.message(j, b"GLOO") for j in range(n)]
+    sigs = W._sign_all(gpu, [sks[j % 64] for j in range(n)], msgs)
+    v, _ = gpu.verify_packed(pack_requests([(True, [([j % 64], msgs[j], sigs[j])]) for j in range(n)]))
+    out["cfg2_valid"] = int((v == 1).sum())
+    out["throughput"] = global_throughput(2048, 0.5, dist, device=None)
+    out["library_hip_runtime"] = library_hip_runtime()
+dist.destroy_process_group()
+print(json.dumps(out))
+"""
+
+
+def test_gloo_rank_binds_library_to_opt_rocm():
+    """The cfg2 / cfg4 / cfg5 rank modes of `bench.py --gpus N` (no data-path collective)
+    load the library before torch and use gloo for the barrier and the max-over-ranks
+    reduction, so a rank's HIP calls go to /opt/rocm's runtime as the N = 1 line's do
+    (VERDICT r5 item 2).  A fresh child process does exactly that (world 1) and verifies a
+    1024-set cfg2 call."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               REPO=str(Path(__file__).resolve().parent.parent))
+    r = subprocess.run([sys.executable, "-c", _GLOO_RANK], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["backend"] == "gloo" and out["cfg2_valid"] == 1024
+    assert out["throughput"] == [4096.0, 0.5]
+    assert out["library_hip_runtime"].startswith("/opt/rocm"), out["library_hip_runtime"]

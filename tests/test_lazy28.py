@@ -114,38 +114,3 @@ def test_lazy28_fp2_ops(hostsim):
         bb = mul(b, b)
         assert r[4] == ((m[0] - bb[0]) % P, (m[1] - bb[1]) % P)
         assert r[5] == (m[0] * b[0] % P, m[1] * b[0] % P)
-
-
-def test_lazy28_fp12_ops(hostsim):
-    """lazy12.hpp's f-side formulas (l12_sqr, l12_mul_line, l12_mul_line2, l12_conj) equal
-    field.hpp's fp12_sqr / fp12_mul_line / fp12_mul_line2 bit for bit on random f and lines
-    (the kernels' inputs: values < 2 p after a product)."""
-    rng = random.Random(12)
-    out = ctypes.create_string_buffer(7 * 576)
-    for k in range(12):
-        f = b"".join(b48(rng.randrange(P) if (k or j) else 1) for j in range(12))
-        lb = b"".join(b48(rng.randrange(P) if k % 4 else P - 1) for _ in range(6))
-        mb = b"".join(b48(rng.randrange(P)) for _ in range(6))
-        hostsim.hs_lz_fp12_ops(f, lb, mb, out)
-        r = [out.raw[576 * i: 576 * i + 576] for i in range(7)]
-        assert r[0] == r[4]
-        assert r[1] == r[5]
-        assert r[2] == r[6]
-        sq = [fp(r[4][48 * i: 48 * i + 48]) for i in range(12)]
-        # conj(reduce(sqr f)): the w^1, w^3, w^5 coefficients (the c1 half) negate
-        want = b"".join(b48((-v) % P if (i // 2) % 2 == 1 else v) for i, v in enumerate(sq))
-        assert r[3] == want
-
-
-def test_lazy28_line_steps(hostsim, oracle):
-    """lazy12.hpp lz_dbl_line / lz_add_line (k_mlq's line side) equal pairing.hpp's
-    miller_dbl_step / miller_add_step and their evaluation at P, bit for bit, after 1, 5
-    and 20 rounds of both steps from T = Q (Q, P: multiples of the generators)."""
-    from tests._codec import g1b, g2b
-
-    out = ctypes.create_string_buffer(2 * 864)
-    for k, steps in ((3, 1), (11, 5), (29, 20)):
-        q = oracle.E2.mul(oracle.G2, k)
-        p = oracle.E1.mul(oracle.G1, 7 * k + 1)
-        hostsim.hs_lz_line_steps(g2b(q), g1b(p), steps, out)
-        assert out.raw[:864] == out.raw[864:]

@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import hashlib
 import json
+import os
 import shutil
 import subprocess
 from pathlib import Path
@@ -20,10 +21,10 @@ pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node
 
 def test_addon_exports():
     code = ("const a = require(process.argv[1]);"
-            "console.log(JSON.stringify(['init','close','loadPubkeys','verify','verifySync','sszRoots']"
+            "console.log(JSON.stringify(['init','close','loadPubkeys','verify','verifySync','sszRoots','partial','finalCheck']"
             ".map(k => typeof a[k])))")
     out = subprocess.run([NODE, "-e", code, str(ADDON)], capture_output=True, text=True, timeout=60, check=True)
-    assert json.loads(out.stdout) == ["function"] * 6
+    assert json.loads(out.stdout) == ["function"] * 8
 
 
 @pytest.mark.gpu
@@ -125,3 +126,46 @@ def test_js_main_thread_lane_not_behind_pool(gpu, tmp_path):
         assert run["main_ok"] is True and run["pool_ok"] is True
         assert run["main_before_pool"], run
         assert run["main_ms"] < 0.7 * run["pool_ms"], run
+
+
+def _multi_checks(r):
+    assert r["slots"] == [2, 2]
+    assert r["gossipOk"] is True
+    assert sum(r["slotSets"]) == 512 and min(r["slotSets"]) > 0, r["slotSets"]
+    assert r["splitValid"] is True and r["splitInvalid"] is False and r["badShards"] == [1]
+    assert r["splitError"] == "BLST_ERROR: BLST_INVALID_SIZE"
+    assert r["splitStats"]["calls"] == 2 and r["splitStats"]["rerouted"] == 1 and r["splitStats"]["failed"] == 1
+    assert r["batchableValid"] is True and r["splitCallsAfterBatchable"] == 2
+
+
+def test_js_multi_device_host_side():
+    """The adapter over two device slots with a stand-in addon (no GPU): per-set gossip
+    calls spread over both slots with their verdicts; a 512-set non-batchable call split
+    in two shards of 256 with one shared seed (addon.partial), one finalCheck over both
+    partials (then one per shard to localise a failing call); an undecodable signature
+    re-runs the call as the reference's jobs and rejects with BLST_INVALID_SIZE."""
+    out = subprocess.run([NODE, str(ROOT / "integration" / "js" / "multiDeviceTest.js"), "--stand-in"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    _multi_checks(r)
+    assert r["partials"] == [[0, 256], [256, 256]] and r["sharedSeed"] is True
+    assert r["finals"] == [2, 2, 1, 1]
+
+
+@pytest.mark.gpu
+def test_js_multi_device_on_one_gpu(gpu, oracle, tmp_path):
+    """The same through the real addon with devices [0, 0] (two slots on the box's one
+    GPU): real signatures, bls_gpu_partial / bls_gpu_final_check for the split call."""
+    n = 512
+    sks = [oracle.interop_secret_key(i % 100).to_bytes(32, "big") for i in range(n)]
+    msgs = [hashlib.sha256(b"jsmulti%d" % i).digest() for i in range(n)]
+    sigs = gpu.sign(b"".join(sks), b"".join(msgs))
+    pks48 = gpu.sk_to_pk(b"".join(sks[:100])).tobytes()
+    f = tmp_path / "work.json"
+    f.write_text(json.dumps({"pubkeys48": pks48.hex(), "sets": [
+        {"idx": i % 100, "msg": msgs[i].hex(), "sig": sigs[i].tobytes().hex()} for i in range(n)]}))
+    out = subprocess.run([NODE, str(ROOT / "integration" / "js" / "multiDeviceTest.js"), str(f)], capture_output=True,
+                         text=True, timeout=300, env=dict(os.environ, UV_THREADPOOL_SIZE="16"))
+    assert out.returncode == 0, out.stderr
+    _multi_checks(json.loads(out.stdout.strip().splitlines()[-1]))

@@ -58,6 +58,17 @@ import json
 for f in ('rehearse_cfg2','rehearse_cfg4'):
   d=json.load(open('$O/'+f+'.json')); print(f, d['n_gpus'], d['value'], d['ms_per_step'], d['data'][-80:])"
 fi
+if [ -n "$NAPI" ]; then
+  # the N-API line: one JS promise per attestation and 1024-set calls, on the adapter's
+  # device slots (NAPI_DEVICES, default "0" and "0,0")
+  for dv in ${NAPI_DEVICES:-0 0,0}; do
+    n=napi_$(echo $dv | tr ',' '_')
+    timeout -k 10 400 python -u bench.py --mode napi --devices $dv --steps ${NAPI_STEPS:-8} --warmup 2 > $O/$n.json 2> $O/$n.err || { echo "$n failed"; tail -20 $O/$n.err; exit 1; }
+    python3 -c "
+import json;d=json.load(open('$O/$n.json'));x=d['napi']
+print('$n', d['value'], x['per_set_calls'].get('slot_sets'), x['calls_of_1024_sets']['sets_per_s'])"
+  done
+fi
 if [ -n "$KPROBE" ]; then
   timeout -k 10 120 python -u tools/kprobe.py > $O/kprobe.json 2> $O/kprobe.err || { echo "kprobe failed"; tail -5 $O/kprobe.err; exit 1; }
   cat $O/kprobe.json
