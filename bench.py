@@ -452,7 +452,11 @@ def run_calls(ctxs, packed, calls_per_pass: int):
     n = len(ctxs)
     start = threading.Barrier(n + 1)
     out = [None] * len(packed)
-    tot = {"batch_retries": 0, "batch_sigs_success": 0, "merged_fail": 0}
+    tot = {"batch_retries": 0, "batch_sigs_success": 0, "merged_fail": 0, "passes": 0,
+           # device time of the passes whose merged check failed / passed, and the failed
+           # passes' per-stage times (bls_stats.stage_ms, summed; the chunk fallback is
+           # device_ms minus the stages)
+           "fail_device_ms": 0.0, "pass_device_ms": 0.0, "fail_stage_ms": np.zeros(8)}
     lock = threading.Lock()
 
     def worker(i):
@@ -467,6 +471,13 @@ def run_calls(ctxs, packed, calls_per_pass: int):
                 tot["batch_retries"] += st.batch_retries
                 tot["batch_sigs_success"] += st.batch_sigs_success
                 tot["merged_fail"] += 1 if st.merged_check == 2 else 0
+                tot["merged_skipped"] = tot.get("merged_skipped", 0) + (1 if st.merged_check == 3 else 0)
+                tot["passes"] += 1
+                if st.merged_check in (2, 3):  # the chunks were checked one by one
+                    tot["fail_device_ms"] += st.device_ms
+                    tot["fail_stage_ms"] += np.array(st.stage_ms[:])
+                else:
+                    tot["pass_device_ms"] += st.device_ms
 
     th = [threading.Thread(target=worker, args=(i,)) for i in range(n)]
     for t in th:
@@ -495,7 +506,7 @@ def steady_state(ctxs, w, pbs, calls_per_pass: int, jobs: int) -> dict:
 
 def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, reps: int = 3,
                 latency_runs: int = 10, cfg4_ctx: int = 4, cfg4_cpp: int = 32, cfg5_sets: int = 131_072,
-                cfg5_roots: int = 256, jobs: int = 5) -> dict:
+                cfg5_roots: int = 256, jobs: int = 5, only: set | None = None) -> dict:
     """BASELINE configs 3 and 4 at N = 1: cfg3, one block-import call
     (latency, sets/s, pubkeys aggregated/s); cfg4 this GPU's slice of the 1M-set range-sync
     job (1/8: shard by call), once with range sync's own non-batchable 128-set calls and
@@ -512,27 +523,31 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
         W.load_table(ctxs, n_keys)
         res["table"] = {"keys": n_keys, "build_s": round(time.perf_counter() - t0, 2)}
         # cfg3: one block
-        w3 = W.cfg3_block(ctxs[0], n_keys)
-        pb3 = W.packed_calls(w3)[0]
-        ctxs[0].verify_packed(pb3)  # warm-up
+        w3 = W.cfg3_block(ctxs[0], n_keys) if only is None or "cfg3" in only else None
+        pb3 = W.packed_calls(w3)[0] if w3 is not None else None
+        if w3 is not None:
+            ctxs[0].verify_packed(pb3)  # warm-up
         lat, stage = [], np.zeros(8)
-        for _ in range(latency_runs):
+        for _ in range(latency_runs if w3 is not None else 0):
             t1 = time.perf_counter()
             v, st = ctxs[0].verify_packed(pb3)
             lat.append(time.perf_counter() - t1)
             stage += np.array(st.stage_ms[:])
             assert W.verdicts_ok(w3, 0, v), "cfg3 block call verdict wrong"
-        p50 = statistics.median(lat)
-        n3 = w3.n_sets
-        keys3 = sum(len(s[0]) for s in w3.calls[0])
-        res["cfg3"] = {"workload": w3.note, "sets": n3, "pubkeys": keys3, "p50_ms": round(p50 * 1e3, 3),
-                       "p99_ms": round(float(np.percentile(np.array(lat) * 1e3, 99)), 3),
-                       "sets_per_s": round(n3 / p50, 1), "pubkeys_aggregated_per_s": round(keys3 / p50, 1),
-                       "stage_ms": {k: round(float(x) / latency_runs, 3) for k, x in zip(STAGE_NAMES, stage)}}
+        if w3 is not None:
+            p50 = statistics.median(lat)
+            n3 = w3.n_sets
+            keys3 = sum(len(s[0]) for s in w3.calls[0])
+            res["cfg3"] = {"workload": w3.note, "sets": n3, "pubkeys": keys3, "p50_ms": round(p50 * 1e3, 3),
+                           "p99_ms": round(float(np.percentile(np.array(lat) * 1e3, 99)), 3),
+                           "sets_per_s": round(n3 / p50, 1), "pubkeys_aggregated_per_s": round(keys3 / p50, 1),
+                           "stage_ms": {k: round(float(x) / latency_runs, 3) for k, x in zip(STAGE_NAMES, stage)}}
         # cfg4: this GPU's slice, both call shapes; calls of 128 sets, cfg4_cpp of them per
         # device pass on cfg4_ctx contexts (sets in flight = the product, stated)
         c4, cpp4 = ctxs[:cfg4_ctx], cfg4_cpp
         for key, batchable in (("cfg4_slice", False), ("cfg4_slice_batchable", True)):
+            if only is not None and key not in only:
+                continue
             w4 = W.cfg4_slice(ctxs[0], n_keys, cfg4_sets, batchable_calls=batchable)
             pbs = W.packed_calls(w4)
             run_calls(c4, pbs[: len(c4) * cpp4], cpp4)  # warm-up
@@ -550,6 +565,7 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
                         "runs": reps,
                         "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
                         "passes_merged_check_failed": tot["merged_fail"],
+                        "passes_merged_check_skipped": tot.get("merged_skipped", 0),
                         "verdicts": "every call matches the sets' validity by construction",
                         **steady_state(c4, w4, pbs, cpp4, jobs)}
         # cfg5: this GPU's slice of the mainnet epoch (1/8 of ~1M attestations over 2048
@@ -560,6 +576,8 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
         # rate -- with 1 invalid set in 2,048 about half of the 1024-set calls fail their
         # merged check and re-verify a chunk's 16 requests alone
         for key, n_invalid in (("cfg5_slice", max(1, cfg5_sets // 2048)), ("cfg5_slice_valid", 0)):
+            if only is not None and key not in only:
+                continue
             w5 = W.cfg5_slice(ctxs[0], n_keys, cfg5_sets, cfg5_roots, invalid=n_invalid)
             pbs = W.packed_calls(w5)
             cpp5 = (len(pbs) + n_ctx - 1) // n_ctx
@@ -577,6 +595,7 @@ def sub_records(n_keys: int, n_ctx: int, calls_per_pass: int, cfg4_sets: int, re
                         "contexts": n_ctx, "calls_per_pass": cpp5, "runs": reps,
                         "batch_retries": tot["batch_retries"], "batch_sigs_success": tot["batch_sigs_success"],
                         "passes_merged_check_failed": tot["merged_fail"],
+                        "passes_merged_check_skipped": tot.get("merged_skipped", 0),
                         "verdicts": "every call matches the sets' validity by construction",
                         **steady_state(ctxs, w5, pbs, cpp5, jobs)}
     finally:
@@ -602,7 +621,11 @@ def run_job_slice(ctxs, w, calls_per_pass: int, steps: int, warmup: int, dist=No
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    tot = {"batch_retries": 0, "batch_sigs_success": 0, "merged_fail": 0}
+    tot = {"batch_retries": 0, "batch_sigs_success": 0, "merged_fail": 0, "passes": 0,
+           # device time of the passes whose merged check failed / passed, and the failed
+           # passes' per-stage times (bls_stats.stage_ms, summed; the chunk fallback is
+           # device_ms minus the stages)
+           "fail_device_ms": 0.0, "pass_device_ms": 0.0, "fail_stage_ms": np.zeros(8)}
     false_req = 0
     for _ in range(steps):
         _, out, st = run_calls(ctxs, pbs, calls_per_pass)
@@ -741,7 +764,7 @@ def run_napi(work_file: Path, steps: int, inflight: int, n_sets: int, per_call: 
                           str(inflight), str(n_sets), str(per_call), str(max_call), devices], capture_output=True,
                          text=True, env=env, timeout=1200)
     if out.returncode != 0:
-        raise SystemExit(f"benchNapi.js failed: {out.stderr[-2000:]}")
+        raise SystemExit(f"benchNapi.js failed (exit {out.returncode}): {out.stderr[-2000:]} {out.stdout[-500:]}")
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
@@ -1061,8 +1084,9 @@ def run_hwq_children(children: dict, value: float | None = None) -> dict:
             "contexts": d["config"]["contexts_per_gpu"], "calls_per_pass": d["config"]["calls_per_pass"],
             "steps": d["steps"],
             "note": "the headline's cfg2 shape in a child process started before the parent's first GPU call, " + (
-                "GPU_MAX_HW_QUEUES unset: what a beacon node that configures nothing runs (the library sets 24 as it "
-                "loads, bls_gpu.hip bls_default_hw_queues)" if q == "unset" else
+                "GPU_MAX_HW_QUEUES unset: what a host that configures nothing runs (the Python wrapper asks for 24 "
+                "queues as it loads the library, lodestar_amd/_abi.py, as the JS adapter does; the library itself "
+                "never writes the environment)" if q == "unset" else
                 f"its HIP runtime given GPU_MAX_HW_QUEUES={q} explicitly" + (" (HIP's own default)" if q == "4" else ""))
                     + "; the headline line runs with 24 (one hardware queue per context)"}
     return res

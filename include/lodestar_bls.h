@@ -70,7 +70,8 @@ typedef struct bls_stats {
                                   k_chain (or k_pset), signature sums, Miller loops (k_mlq + k_mlf),
                                   status + merged / chunk checks, individual */
   uint32_t n_unique_msgs;      /* distinct signing roots hashed to the curve (== n_sets without dedup) */
-  uint32_t merged_check;       /* 0 not run, 1 passed (per-chunk checks skipped), 2 failed (chunks checked) */
+  uint32_t merged_check;       /* 0 not run, 1 passed (per-chunk checks skipped), 2 failed (chunks checked),
+                                  3 skipped: the context's previous pass failed it, chunks checked straight away */
   uint32_t n_ml_units;         /* Miller-loop units (chunk x shared signing root pairings), 0 = one per set */
   uint32_t pass_shape;         /* how the aggregated path ran (0 on the per-set path): bit 0 the merged signature
                                   sum by Pippenger MSM; bits 8-15 items per lane of the f side of the Miller loops
@@ -332,6 +333,9 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
  * $BLS_GROUP_TEST_MIN says (off by default: the tests cut final exponentiations, not
  * the requests' own signature-sum Miller loops, and their extra rounds cost more). */
 #define BLS_DEBUG_GROUP_TEST 128u
+/* Test hook: run the merged check on every pass, also after a pass that failed it (by
+ * default such a context's next pass checks its chunks straight away, merged_check 3). */
+#define BLS_DEBUG_MERGED_EVERY_PASS 256u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

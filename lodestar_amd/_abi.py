@@ -90,6 +90,7 @@ DEBUG_SIGAGG_OFF = 16
 DEBUG_NO_UNITS = 32
 DEBUG_MSM = 64
 DEBUG_GROUP_TEST = 128
+DEBUG_MERGED_EVERY_PASS = 256
 
 
 def DEBUG_MLF_PL(n: int) -> int:

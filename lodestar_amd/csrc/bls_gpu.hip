@@ -855,6 +855,21 @@ static bool sig_total_on() {
   return on;
 }
 
+// After a pass whose merged check failed, a context's next pass skips it and checks its
+// chunks straight away (each chunk's own signature sum paired in the pass's Miller-loop
+// launch, then the per-chunk final exponentiations): a stream with invalid sets in most
+// passes (the cfg4 per-set requests, the cfg5 epoch slice) otherwise pays the merged
+// final exponentiation, then the chunk sums, their Miller loops and the chunk checks one
+// after another on the failing call's path.  The first pass whose chunks all pass turns
+// the merged check back on.  $BLS_MERGED_AFTER_FAIL=1 keeps it on every pass.
+static bool merged_skip_after_fail() {
+  static const bool on = [] {
+    const char* e = getenv("BLS_MERGED_AFTER_FAIL");
+    return !(e && atoi(e) == 1);
+  }();
+  return on;
+}
+
 // Segmented-sum plan for k_gsum over groups of requests: the groups' set indices
 // (group-major) and, per level, (beg, end) segments of at most GSUM_FAN items that
 // never straddle a group; level 0 indexes gsets, level L > 0 the outputs of level
@@ -1098,8 +1113,11 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // all 1 and the per-chunk final exponentiations are skipped.  A failing merged
   // check (or a request with an error status) falls back to k_chunk_coop, so
   // verdicts and stats stay those of the chunked worker (worker.ts:56-88).
-  const bool merged = !partial && plan.chunk_off.size() > 2 && plan.nonbatch_reqs.empty() && n > 0 &&
-                      !(ctx->debug_flags & BLS_DEBUG_NO_MERGED_CHECK);
+  const bool merged_eligible = !partial && plan.chunk_off.size() > 2 && plan.nonbatch_reqs.empty() && n > 0 &&
+                               !(ctx->debug_flags & BLS_DEBUG_NO_MERGED_CHECK);
+  const bool merged_skipped = merged_eligible && ctx->last_merged_failed && merged_skip_after_fail() &&
+                              !(ctx->debug_flags & BLS_DEBUG_MERGED_EVERY_PASS);
+  const bool merged = merged_eligible && !merged_skipped;
   const uint32_t n_chunks = (uint32_t)plan.chunk_off.size() - 1;
   const uint32_t n_pk_idx = in->set_pk_offsets ? in->set_pk_offsets[n] : 0;
   // aggregated-signature path: virtual sets n + chunk and n + n_chunks + individual
@@ -1192,6 +1210,11 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   G2J* gtmp[2] = {nullptr, nullptr};
   uint32_t *unit_rep_dev = nullptr, *ugsets_dev = nullptr, *useg_dev = nullptr;  // Miller-loop units
   uint32_t* own_sets_dev = nullptr;      // the individually verified sets' own Miller loops + the requests' sums (one launch)
+  // SIMT final exponentiations (kernels/k_fin_simt.hip) for a failing pass's many chunk
+  // checks / requests verified alone: 4 Fp12 per task, carved when a pass could need them
+  const uint32_t fe_min = fe_simt_min();
+  const bool fe_simt_possible = fe_min > 0 && (n_chunks >= fe_min || R >= fe_min);
+  Fp12* fe_save = nullptr;
   MsmBufs msm;
   memset(&msm, 0, sizeof(msm));
   G1J* utmp[2] = {nullptr, nullptr};
@@ -1271,6 +1294,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     }
     b.req_status = c.take<int32_t>(R);
     gbufs.f = gt_possible ? c.take<Fp12>(R) : nullptr;
+    fe_save = fe_simt_possible ? c.take<Fp12>(4ull * (n_chunks > R ? n_chunks : R)) : nullptr;
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
       ptree[1] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
@@ -1497,12 +1521,23 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       if (launch_gsum(ctx, b, chunk_gsum, gseg_dev, gsets_dev, gtmp, n, s)) return -1;
       HIPC(ctx, launch_ml_alone(n, n_chunks, nullptr)); dbg_sync(s, "k_mln chunk sums");
     }
-    HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s)); dbg_sync(s, "k_chunk_coop");
+    // many chunk checks: one lane each (a failing pass at the plateau has hundreds, and a
+    // cooperative task holds a SIMD for a whole final exponentiation); few: one wavefront
+    // each, the shorter latency
+    if (fe_save && n_chunks >= fe_min) HIPC(ctx, launch_k_chunk_simt(b, fe_save, s));
+    else HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s));
+    dbg_sync(s, "k_chunk");
     HIPC(ctx, hipStreamSynchronize(s));
     memcpy(chunk_ok.data(), res_host(ctx, b.chunk_ok), sizeof(int32_t) * n_chunks);
   }
+  if (merged_skipped) {
+    // the context keeps skipping the merged check while its passes keep failing a chunk
+    bool all_ok = true;
+    for (uint32_t ch = 0; ch < n_chunks; ++ch) all_ok = all_ok && chunk_ok[ch] == 1;
+    ctx->last_merged_failed = !all_ok;
+  }
   if (stats) {
-    stats->merged_check = merged ? (merged_pass ? 1 : 2) : 0;
+    stats->merged_check = merged ? (merged_pass ? 1 : 2) : (merged_skipped ? 3 : 0);
     stats->pass_shape =
         sigagg ? ((use_msm ? 1u : 0u) | (k_mln_list_ok(b) ? pass_pl << 8 : 0u)) : 0u;
   }
@@ -1595,12 +1630,18 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       // chunk's units or shared loops (its chunk failed) now runs their own Miller loops
       std::vector<uint32_t> own;
       const bool own_list = (use_units || ml_shared) && k_mln_list_ok(b);
+      // a set needs its own Miller loop again only when the first pass did not leave it
+      // one: it was paired in its chunk's unit (f_i = 1), or its f was shared with the
+      // next items of its lane (more than one item per k_mlf lane); at one item per lane
+      // or per lane pair f_i = e(r_i pk_i, H(m_i)) already
+      const bool f_shared = ml_shared && !(pass_pl == 1u || pass_pl == MLF_PAIR);
       if (own_list) {
-        // every set of the failed chunks' requests, in ONE launch with the requests'
+        // every such set of the failed chunks' requests, in ONE launch with the requests'
         // signature sums below (one Miller-loop latency instead of two on the failing
         // call's path, profiles/r05_cfg5_fallback.json)
         for (size_t t = plan.nonbatch_reqs.size(); t < indiv.size(); ++t)
-          for (uint32_t i = in->req_set_offsets[indiv[t]]; i < in->req_set_offsets[indiv[t] + 1]; ++i) own.push_back(i);
+          for (uint32_t i = in->req_set_offsets[indiv[t]]; i < in->req_set_offsets[indiv[t] + 1]; ++i)
+            if (f_shared || (use_units && units.set_unit[i] != UNIT_NONE)) own.push_back(i);
       } else if (use_units || ml_shared) {
         // one launch per run of consecutive sets (a failed chunk's requests are adjacent)
         uint32_t run_beg = 0, run_end = 0;
@@ -1660,7 +1701,9 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       HIPC(ctx, launch_k_fold(b, ctx->coop, s)); dbg_sync(s, "k_fold");
     }
     gbufs.n_direct = n_direct;
-    HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, gbufs, s)); dbg_sync(s, "k_indiv_coop");
+    if (fe_save && b.n_indiv >= fe_min) HIPC(ctx, launch_k_indiv_simt(b, gbufs, fe_save, s));
+    else HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, gbufs, s));
+    dbg_sync(s, "k_indiv");
     if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev[8], s));
   }
   if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev1, s));

@@ -5,14 +5,19 @@ against the oracle's worker semantics (oracle.verify_many_signature_sets over va
 tokens, multithread/worker.ts:32-108), the pass shape against the rule that picked it.
 
 * msm_flip (BLS_MSM=1): the Pippenger signature sum runs on a context whose last pass
-  passed its merged check, and not on the pass after a failing one
-  (bls_gpu.hip verify_impl use_msm, ctx->last_merged_failed): a failing call, then two
-  passing ones -- pass_shape bit 0 goes 1, 0, 1 and every verdict is right.
+  passed its merged check, and not on the pass after a failing one, which checks its
+  chunks straight away (bls_gpu.hip verify_body merged_skipped, ctx->last_merged_failed):
+  a failing call, then two passing ones -- pass_shape bit 0 goes 1, 0, 1, merged_check
+  2, 3, 1, and every verdict is right.
 * fallbacks (BLS_COOP_ML_MAX=1, BLS_INDIV2_MAX=0, BLS_PACK3_INFLIGHT=0): a failing
   aggregated call's later Miller loops above the cooperative limit take the SIMT pair at
   mlf_per_lane_alone's shape (k_pset.hip launch_k_mln_coop -> k_mlq.hip), its requests
   verified alone on one wavefront each (k_fin.hip k_indiv_coop), and a 512-set per-set
   call runs three sets per wavefront (k_pset.hip pack_for -> k_psetn<3>).
+* fe_simt (BLS_FE_SIMT_MIN=1): every chunk check and every request verified alone runs
+  its final exponentiation one lane per task (kernels/k_fin_simt.hip) instead of one
+  wavefront per task -- failing aggregated calls (with and without group testing), the
+  per-set path, non-batchable multi-set requests.
 """
 from __future__ import annotations
 
@@ -58,6 +63,14 @@ with GpuContext(0) as gpu:
         run(sets, msgs, {17, 3500}, True, True)
         run(sets, msgs, set(), True, True)
         run(sets, msgs, set(), True, True)
+    elif case == "fe_simt":
+        sets, msgs = make(1024, b"FESI")
+        run(sets, msgs, {3, 400, 401, 1000}, True, True, 8)      # chunk checks + requests alone, one lane each
+        run(sets, msgs, {5, 77, 78}, True, True, 8 | 128)        # ... with group testing (products only)
+        small, smsgs = make(512, b"FESP")
+        run(small, smsgs, {7, 300}, True, True)                  # per-set path (f holds both pairings)
+        run(small, smsgs, {7, 300}, False, False)                # non-batchable 128-set requests (k_fold groups)
+        run(small, smsgs, set(), False, False, 8)                # ... on the aggregated path, all valid
     else:
         sets, msgs = make(1024, b"FALL")
         run(sets, msgs, {3, 400, 401, 1000}, True, True, 8)  # BLS_DEBUG_SIGAGG_ON: merged check fails
@@ -70,6 +83,7 @@ print(json.dumps(out))
 ENVS = {
     "msm_flip": {"BLS_MSM": "1"},
     "fallbacks": {"BLS_COOP_ML_MAX": "1", "BLS_INDIV2_MAX": "0", "BLS_PACK3_INFLIGHT": "0"},
+    "fe_simt": {"BLS_FE_SIMT_MIN": "1"},
 }
 
 
@@ -103,9 +117,13 @@ def test_env_selected_paths(case, oracle):
         assert c["verdicts"] == v, (case, c["n"], c["bad"])
         assert (c["retries"], c["ok"]) == (retries, ok), (case, c["n"], c["bad"])
     if case == "msm_flip":
-        # the Pippenger sum on the first pass, off after its failed merged check, back on
+        # the Pippenger sum on the first pass; after its failed merged check the next pass
+        # checks its chunks straight away (merged_check 3, no total sum, no MSM); its chunks
+        # all pass, so the third is back on the merged check with the MSM
         assert [c["shape"] & 1 for c in calls] == [1, 0, 1]
-        assert [c["merged"] for c in calls] == [2, 1, 1]
+        assert [c["merged"] for c in calls] == [2, 3, 1]
+    elif case == "fe_simt":
+        assert calls[0]["merged"] == 2 and calls[1]["merged"] == 2 and calls[2]["shape"] == 0
     else:
         assert calls[0]["shape"] != 0 and calls[0]["merged"] == 2  # aggregated path, merged check failed
         assert calls[1]["shape"] == 0  # the per-set path

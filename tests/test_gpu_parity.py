@@ -32,9 +32,13 @@ def verify_path(request, gpu):
     """Every test of this module runs on both per-set paths: the all-cooperative k_pset
     and the aggregated-signature path (k_chain + k_gsum / k_vset + single-pair k_mln),
     whatever the call size would pick."""
-    from lodestar_amd._abi import DEBUG_SIGAGG_OFF, DEBUG_SIGAGG_ON
+    from lodestar_amd._abi import DEBUG_MERGED_EVERY_PASS, DEBUG_SIGAGG_OFF, DEBUG_SIGAGG_ON
 
-    gpu.base_debug_flags = DEBUG_SIGAGG_ON if request.param == "sigagg" else DEBUG_SIGAGG_OFF
+    # the merged check on every pass (a test's merged_check expectation must not depend on
+    # what the previous test left on the shared context); the adaptive skip after a failed
+    # pass is test_merged_check_skipped_after_failing_pass below
+    gpu.base_debug_flags = (DEBUG_SIGAGG_ON if request.param == "sigagg" else DEBUG_SIGAGG_OFF) | \
+        DEBUG_MERGED_EVERY_PASS
     gpu.set_debug_flags(0)
     yield request.param
     gpu.base_debug_flags = 0
@@ -1008,3 +1012,34 @@ def test_mlf_items_per_lane(gpu, oracle, table, verify_path, per_lane):
             assert st.merged_check == (2 if with_bad else 1)
             assert (st.batch_retries, st.batch_sigs_success) == (retries, ok)
             assert (st.pass_shape >> 8) & 0xFF == per_lane and (st.pass_shape & 1) == (1 if extra else 0)
+
+
+def test_merged_check_skipped_after_failing_pass(gpu, oracle, table, verify_path):
+    """A context whose pass failed its merged check checks its next pass's chunks straight
+    away (bls_gpu.hip merged_skip_after_fail: merged_check 3, each chunk's own signature
+    sum paired in the pass), until a pass whose chunks all pass; verdicts and the worker
+    counters are those of the chunked worker either way (worker.ts:56-88)."""
+    from lodestar_amd._abi import DEBUG_SIGAGG_OFF, DEBUG_SIGAGG_ON
+
+    n = 96
+    sks = _keys(oracle, 16)
+    msgs = [_h(b"skip%d" % i) for i in range(n)]
+    sigs = gpu.sign(b"".join(sks[i % 16] for i in range(n)), b"".join(msgs))
+
+    def call(bad):
+        reqs = [(True, [([i % 16], msgs[i] if i not in bad else _h(b"skip-x"), sigs[i].tobytes())]) for i in range(n)]
+        expect = [0 if i in bad else 1 for i in range(n)]
+        v, st = gpu.verify_packed(pack_requests(reqs))
+        assert list(v) == expect
+        assert (st.batch_retries, st.batch_sigs_success) == _expected_stats(oracle, expect)
+        return st.merged_check
+
+    saved = gpu.base_debug_flags
+    gpu.base_debug_flags = DEBUG_SIGAGG_ON if verify_path == "sigagg" else DEBUG_SIGAGG_OFF
+    try:
+        gpu.set_debug_flags(0)
+        call(set())  # whatever the context's history, a passing pass leaves the merged check on
+        assert [call({5}), call({40, 41}), call({90}), call(set()), call(set()), call({7})] == [2, 3, 3, 3, 1, 2]
+    finally:
+        gpu.base_debug_flags = saved
+        gpu.set_debug_flags(0)
