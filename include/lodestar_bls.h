@@ -335,7 +335,7 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
 #define BLS_DEBUG_GROUP_TEST 128u
 /* Test hook: run the merged check on every pass, also after a pass that failed it (by
  * default such a context's next pass checks its chunks straight away, merged_check 3). */
-#define BLS_DEBUG_MERGED_EVERY_PASS 256u
+#define BLS_DEBUG_MERGED_EVERY_PASS 0x8000u
 int bls_gpu_set_debug_flags(bls_gpu_ctx* ctx, uint32_t flags);
 
 #ifdef __cplusplus

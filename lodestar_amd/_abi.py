@@ -90,7 +90,7 @@ DEBUG_SIGAGG_OFF = 16
 DEBUG_NO_UNITS = 32
 DEBUG_MSM = 64
 DEBUG_GROUP_TEST = 128
-DEBUG_MERGED_EVERY_PASS = 256
+DEBUG_MERGED_EVERY_PASS = 0x8000  # (bits 8-9 are BLS_DEBUG_PACK, 12-14 BLS_DEBUG_MLF_PL)
 
 
 def DEBUG_MLF_PL(n: int) -> int:

@@ -128,3 +128,21 @@ def test_fixture_kernels_scratch_checked():
     table[1]["device_scratch_bytes"] = 101
     with pytest.raises(RuntimeError, match="fixture kernel"):
         scratch_per_queue(table)
+
+
+def test_debug_flag_bits_disjoint():
+    """Every BLS_DEBUG_* flag / field of include/lodestar_bls.h owns its own bits (a new
+    flag once landed on BLS_DEBUG_PACK's bits), and the ctypes constants agree."""
+    import lodestar_amd._abi as abi
+
+    hdr = (ROOT / "include" / "lodestar_bls.h").read_text()
+    vals = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define (BLS_DEBUG_\w+) (0x[0-9a-fA-F]+|\d+)u", hdr)}
+    masks = [v for k, v in vals.items() if not k.endswith("_MASK")] + [vals["BLS_DEBUG_PACK_MASK"],
+                                                                        vals["BLS_DEBUG_MLF_PL_MASK"]]
+    seen = 0
+    for v in masks:
+        assert seen & v == 0, hex(v)
+        seen |= v
+    for k, v in vals.items():
+        if not k.endswith("_MASK"):
+            assert getattr(abi, k[len("BLS_"):]) == v, k

@@ -27,7 +27,9 @@ N = 512
 @pytest.fixture(scope="module")
 def multi(golden):
     pks = b"".join(bytes.fromhex(h) for h in golden["kat2_interop_pubkeys"])
-    v = GpuBlsVerifier(devices=[0, 0], n_contexts=2, pubkeys48=pks, split_call_min_sets=256, record_calls=True)
+    # calls of at most 128 sets, so the 512 gossip sets make several calls to route
+    v = GpuBlsVerifier(devices=[0, 0], n_contexts=2, pubkeys48=pks, split_call_min_sets=256, record_calls=True,
+                       max_sets_per_call=128)
     yield v
     v.close()
 
