@@ -330,8 +330,7 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
 #define BLS_DEBUG_MLF_PL(n) ((uint32_t)(n) << 12)
 #define BLS_DEBUG_MLF_PL_MASK 0x7000u
 /* Test / bench hook: group-test failed chunks of >= 4 requests whatever
- * $BLS_GROUP_TEST_MIN says (off by default: the tests cut final exponentiations, not
- * the requests' own signature-sum Miller loops, and their extra rounds cost more). */
+ * $BLS_GROUP_TEST_MIN says (its default is 4 too; 0 turns group testing off). */
 #define BLS_DEBUG_GROUP_TEST 128u
 /* Test hook: run the merged check on every pass, also after a pass that failed it (by
  * default such a context's next pass checks its chunks straight away, merged_check 3). */

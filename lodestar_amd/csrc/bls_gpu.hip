@@ -697,15 +697,17 @@ static void dbg_sync(hipStream_t s, const char* what) {
 // With one invalid request in a chunk of 16 that is 6 final exponentiations instead of
 // 16; verdicts and the worker counters are the reference's (a test that passes is the
 // batch the reference's retry would have passed request by request, with the same
-// soundness).  Off by default: each request still pays its own signature-sum Miller loop
-// (the larger part of its cost on the aggregated path) and the two extra rounds of
-// dependent launches cost more than the saved exponentiations -- cfg4 per-set requests
-// 0.875M vs 0.910M sets/s (profiles/r04_ab_group_test.json).  $BLS_GROUP_TEST_MIN (the
-// smallest chunk tested so; 0 = off) or BLS_DEBUG_GROUP_TEST (chunks of >= 4) turn it on.
+// soundness).  On for chunks of >= 4 requests since round 6: once the failed chunks'
+// requests stopped re-running their sets' own Miller loops and the chunks of a failing
+// stream are checked without the merged check first, the saved final exponentiations
+// outweigh the extra rounds -- cfg4 per-set requests 1.35M -> 1.50M sets/s steady, cfg5
+// level (profiles/r06_ab_group_test.json; in rounds 4-5 it lost or was level,
+// r04_ab_group_test.json, r05_ab_group_test_again.json).  $BLS_GROUP_TEST_MIN sets the
+// smallest chunk tested so (0 = off); BLS_DEBUG_GROUP_TEST forces chunks of >= 4.
 static uint32_t group_test_min(const bls_gpu_ctx* ctx) {
   static const uint32_t v = [] {
     const char* e = getenv("BLS_GROUP_TEST_MIN");
-    const long x = e ? atol(e) : 0;
+    const long x = e ? atol(e) : 4;
     return x <= 0 ? 0xFFFFFFFFu : (uint32_t)(x < 2 ? 2 : x);
   }();
   return (ctx->debug_flags & BLS_DEBUG_GROUP_TEST) ? 4u : v;
