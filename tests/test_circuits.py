@@ -145,9 +145,9 @@ def test_emitted_lane_groups_match_program(progs, tmp_path):
     # pset_phase2 / pset2_phase2 / pset3_phase2 hold the subgroup test's combination-only
     # steps (psi(sig) - [x] sig into PS_DIFF, k_pset.hip's BLST_POINT_NOT_IN_GROUP test): the
     # round-5 GPU failure gpurun_out/r5i/pytest.log (-3 for a valid signature on the 1-set
-    # path) came from an uncommitted first form of the lane-pair combinations, whose pair
-    # sums did not reach the slot a step writes; every program the device
-    # runs with lane groups is checked here
+    # path: a wrong PS_DIFF) came from an uncommitted first form of the lane-pair
+    # combinations; every program the device runs with lane groups is
+    # checked here
     names = ["pset_dbl_all", "pset_add_x", "fin_fe1", "fin_fmul", "pset_norm2", "pset_ml2_w2", "pset_xchain",
              "fin_fe2_w2", "pset_prep", "pset_phase2", "pset_affine2", "pset2_phase2", "pset3_phase2", "pset3_prep",
              "ml1_1", "ml1_2"]
