@@ -137,6 +137,10 @@ struct GroupBufs {
   const uint32_t* members;   // indices t into the indiv list
   uint32_t n;
   int32_t* verdict;          // n: 1 / 0 (host-mapped)
+  // group sums (aggregated path): test g carries its own signature-sum pairing
+  // ML(-g1, sum of its requests' r sig) in sum_f[g], and a group-tested request's F_t
+  // holds its sets' f only; nullptr: each F_t holds its own request sum's pairing
+  const Fp12* sum_f;
 };
 
 BLS_HD void scalar_words_from_be32(const uint8_t* b, uint32_t k[8]) {

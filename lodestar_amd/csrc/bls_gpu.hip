@@ -30,6 +30,7 @@
 #include <zlib.h>
 
 #include <atomic>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -713,11 +714,42 @@ static uint32_t group_test_min(const bls_gpu_ctx* ctx) {
   return (ctx->debug_flags & BLS_DEBUG_GROUP_TEST) ? 4u : v;
 }
 
-// run the tests (goff: offsets into gmem, indices into the indiv list); results in gv
+// Group sums (aggregated path): the tests' own signature sums, sum of r_i sig_i over
+// their requests' sets, paired ML(-g1, .) into sum_f[g] before k_group_coop; returns 0,
+// 1 when the plan does not fit the workspace (the caller tests the requests alone), < 0
+// on an error.  Unset: each request's product already holds its own sum's pairing.
+typedef std::function<int(const std::vector<uint32_t>&, const std::vector<uint32_t>&)> GroupSums;
+
+// group sums (run_group_tests) for a pass with at least $BLS_GROUP_SUMS_MIN (512)
+// group-tested requests; 0 = always, $BLS_GROUP_SUMS=0 = never.  They save Miller loops
+// (cfg4 per-set requests, ~1,300 group-tested requests a pass: 1.52M -> 1.56M sets/s
+// steady) but put a sum + Miller-loop stage in front of each round of tests, where the
+// per-request sums ride in the requests' Miller-loop launch: with a few failed chunks
+// a pass (the cfg5 slice, ~80 requests) that latency costs more (3.29M -> 3.05M)
+// (profiles/r06_ab_group_sums.json)
+static bool group_sums_on(size_t n_group_tested) {
+  static const bool on = [] {
+    const char* e = getenv("BLS_GROUP_SUMS");
+    return !(e && atoi(e) == 0);
+  }();
+  static const size_t min_reqs = [] {
+    const char* e = getenv("BLS_GROUP_SUMS_MIN");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)512;
+  }();
+  return on && n_group_tested >= min_reqs;
+}
+
+// run the tests (goff: offsets into gmem, indices into the indiv list); results in gv;
+// 1 when the group sums do not fit (nothing ran)
 static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, const std::vector<uint32_t>& goff,
-                           const std::vector<uint32_t>& gmem, std::vector<int32_t>& gv, hipStream_t s) {
+                           const std::vector<uint32_t>& gmem, std::vector<int32_t>& gv, hipStream_t s,
+                           const GroupSums* sums) {
   gv.assign(goff.size() - 1, 0);
   if (gv.empty()) return 0;
+  if (sums && *sums) {
+    const int rc = (*sums)(goff, gmem);
+    if (rc != 0) return rc;
+  }
   stage_copy(ctx, g.off, goff.data(), sizeof(uint32_t) * goff.size());  // the stream is idle
   stage_copy(ctx, g.members, gmem.data(), sizeof(uint32_t) * gmem.size());
   g.n = (uint32_t)gv.size();
@@ -729,7 +761,7 @@ static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, co
 
 static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
                          const std::vector<std::pair<uint32_t, uint32_t>>& chunks, std::vector<int32_t>& verdict,
-                         hipStream_t s, size_t grp_cap, size_t grp_mem_cap) {
+                         hipStream_t s, size_t grp_cap, size_t grp_mem_cap, const GroupSums* sums) {
   struct Chunk {
     std::vector<uint32_t> ok;  // indiv indices of the requests of status OK
     bool has_err = false;
@@ -766,10 +798,15 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
     return -3;
   }
   std::vector<int32_t> gv;
-  if (run_group_tests(ctx, b, gbufs, goff, gmem, gv, s)) return -1;
-  // decode pass A; plan pass B
   std::vector<uint32_t> goff_b{0}, gmem_b, alone;  // alone: requests for pass C
   std::vector<size_t> in_b;
+  const int rc_a = run_group_tests(ctx, b, gbufs, goff, gmem, gv, s, sums);
+  if (rc_a < 0) return -1;
+  if (rc_a == 1) {  // the group sums of pass A do not fit: every request alone
+    for (const Chunk& c : cs) alone.insert(alone.end(), c.ok.begin(), c.ok.end());
+    cs.clear();
+  }
+  // decode pass A; plan pass B
   for (size_t i = 0; i < cs.size(); ++i) {
     Chunk& c = cs[i];
     uint32_t idx = c.first;
@@ -796,10 +833,11 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
     goff_b.push_back((uint32_t)gmem_b.size());
     in_b.push_back(i);
   }
-  if (run_group_tests(ctx, b, gbufs, goff_b, gmem_b, gv, s)) return -1;
+  const int rc_b = run_group_tests(ctx, b, gbufs, goff_b, gmem_b, gv, s, sums);
+  if (rc_b < 0) return -1;
   for (size_t q = 0; q < in_b.size(); ++q) {
     Chunk& c = cs[in_b[q]];
-    if (gv[2 * q] == 0 && gv[2 * q + 1] == 1) {
+    if (rc_b == 0 && gv[2 * q] == 0 && gv[2 * q + 1] == 1) {
       for (uint32_t k = 0; k < c.ok.size(); ++k) verdict[c.ok[k]] = (int32_t)k == c.b ? 0 : 1;
     } else {
       alone.insert(alone.end(), c.ok.begin(), c.ok.end());
@@ -808,7 +846,12 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
   // pass C: one test per request
   std::vector<uint32_t> goff_c{0};
   for (size_t k = 0; k < alone.size(); ++k) goff_c.push_back((uint32_t)k + 1);
-  if (run_group_tests(ctx, b, gbufs, goff_c, alone, gv, s)) return -1;
+  const int rc_c = run_group_tests(ctx, b, gbufs, goff_c, alone, gv, s, sums);
+  if (rc_c != 0) {
+    // one request per test always fits the request-sum workspace
+    snprintf(ctx->err, sizeof(ctx->err), "group tests: per-request sums do not fit");
+    return -3;
+  }
   for (size_t k = 0; k < alone.size(); ++k) verdict[alone[k]] = gv[k] == 1 ? 1 : 0;
   return 0;
 }
@@ -1619,6 +1662,12 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       if (pass == 1) gt_chunks.push_back({beg, (uint32_t)indiv.size()});
     }
   const uint32_t n_direct = gt_chunks.empty() ? (uint32_t)indiv.size() : gt_chunks.front().first;
+  // Group sums: on the aggregated path, with many requests group-tested, a group-tested
+  // request pairs no signature sum of its own; each group test pairs ONE sum over its
+  // requests' sets (run_group_tests) -- 4-6 Miller loops per failed chunk of 16 instead of
+  // 16 (group_sums_on).
+  const bool gsums = sigagg && !gt_chunks.empty() && group_sums_on(indiv.size() - n_direct);
+  const uint32_t n_sum = gsums ? n_direct : (uint32_t)indiv.size();  // requests pairing their own sum
   std::vector<int32_t> indiv_verdict(indiv.size() + 1, 0);
   std::vector<uint32_t> groups;  // k_fold groups; outlives the async copy (synchronised below)
   GsumPlan indiv_gsum;           // likewise
@@ -1663,24 +1712,28 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
           run_end = end;
         }
       }
-      std::vector<uint32_t> goff(indiv.size() + 1);
-      for (size_t t = 0; t <= indiv.size(); ++t) goff[t] = (uint32_t)t;
-      plan_gsum(in, goff, indiv, indiv_gsum);
+      std::vector<uint32_t> goff(n_sum + 1);
+      for (size_t t = 0; t <= n_sum; ++t) goff[t] = (uint32_t)t;
+      plan_gsum(in, goff, std::vector<uint32_t>(indiv.begin(), indiv.begin() + n_sum), indiv_gsum);
       if (ensure_rs()) return -1;
       if (indiv_gsum.seg.size() > gseg_cap) {
         snprintf(ctx->err, sizeof(ctx->err), "group-sum plan exceeds its workspace");
         return -3;
       }
-      stage_copy(ctx, gsets_dev, indiv_gsum.gsets.data(), sizeof(uint32_t) * indiv_gsum.gsets.size());
-      stage_copy(ctx, gseg_dev, indiv_gsum.seg.data(), sizeof(uint32_t) * indiv_gsum.seg.size());
-      if (launch_gsum(ctx, b, indiv_gsum, gseg_dev, gsets_dev, gtmp, indiv_vbase, s)) return -1;
+      if (n_sum > 0) {  // (under group sums every request may be group-tested)
+        stage_copy(ctx, gsets_dev, indiv_gsum.gsets.data(), sizeof(uint32_t) * indiv_gsum.gsets.size());
+        stage_copy(ctx, gseg_dev, indiv_gsum.seg.data(), sizeof(uint32_t) * indiv_gsum.seg.size());
+        if (launch_gsum(ctx, b, indiv_gsum, gseg_dev, gsets_dev, gtmp, indiv_vbase, s)) return -1;
+      }
       if (own_list) {
-        for (size_t t = 0; t < indiv.size(); ++t) own.push_back(indiv_vbase + (uint32_t)t);
-        stage_copy(ctx, own_sets_dev, own.data(), sizeof(uint32_t) * own.size());
-        HIPC(ctx, launch_ml_alone(0, (uint32_t)own.size(), own_sets_dev));
-        dbg_sync(s, "k_mln own + indiv (list)");
+        for (size_t t = 0; t < n_sum; ++t) own.push_back(indiv_vbase + (uint32_t)t);
+        if (!own.empty()) {
+          stage_copy(ctx, own_sets_dev, own.data(), sizeof(uint32_t) * own.size());
+          HIPC(ctx, launch_ml_alone(0, (uint32_t)own.size(), own_sets_dev));
+          dbg_sync(s, "k_mln own + indiv (list)");
+        }
       } else {
-        HIPC(ctx, launch_ml_alone(indiv_vbase, (uint32_t)indiv.size(), nullptr)); dbg_sync(s, "k_mln indiv");
+        HIPC(ctx, launch_ml_alone(indiv_vbase, n_sum, nullptr)); dbg_sync(s, "k_mln indiv");
       }
     }
     // groups of BLS_FOLD consecutive sets per request, multiplied in parallel first
@@ -1703,6 +1756,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       HIPC(ctx, launch_k_fold(b, ctx->coop, s)); dbg_sync(s, "k_fold");
     }
     gbufs.n_direct = n_direct;
+    gbufs.sum_f = gsums ? b.f + indiv_vbase + n_direct : nullptr;
     if (fe_save && b.n_indiv >= fe_min) HIPC(ctx, launch_k_indiv_simt(b, gbufs, fe_save, s));
     else HIPC(ctx, launch_k_indiv_coop(b, ctx->coop, gbufs, s));
     dbg_sync(s, "k_indiv");
@@ -1712,7 +1766,29 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   HIPC(ctx, hipStreamSynchronize(s));
   if (!indiv.empty()) memcpy(indiv_verdict.data(), res_host(ctx, b.indiv_verdict), sizeof(int32_t) * indiv.size());
   if (!gt_chunks.empty()) {
-    if (const int rc = verify_groups(ctx, b, gbufs, gt_chunks, indiv_verdict, s, grp_cap, grp_mem_cap)) return rc;
+    // group sums: test g's sum lands in virtual set indiv_vbase + n_direct + g (the
+    // group-tested requests' own slots, unused under group sums; a pass never has more
+    // tests than group-tested requests), paired before k_group_coop
+    GroupSums sums_fn;
+    if (gsums)
+      sums_fn = [&](const std::vector<uint32_t>& goff, const std::vector<uint32_t>& gmem) -> int {
+        const uint32_t T = (uint32_t)(goff.size() - 1);
+        if (n_direct + T > indiv.size()) return 1;
+        std::vector<uint32_t> reqs(gmem.size());
+        for (size_t k = 0; k < gmem.size(); ++k) reqs[k] = indiv[gmem[k]];
+        GsumPlan gp;
+        plan_gsum(in, goff, reqs, gp);
+        if (gp.gsets.size() > n || gp.seg.size() > gseg_cap || (gp.level_off.size() > 1 && gp.level_off[1] > gtmp_cap))
+          return 1;
+        stage_copy(ctx, gsets_dev, gp.gsets.data(), sizeof(uint32_t) * gp.gsets.size());  // the stream is idle
+        stage_copy(ctx, gseg_dev, gp.seg.data(), sizeof(uint32_t) * gp.seg.size());
+        if (launch_gsum(ctx, b, gp, gseg_dev, gsets_dev, gtmp, indiv_vbase + n_direct, s)) return -1;
+        HIPC(ctx, launch_ml_alone(indiv_vbase + n_direct, T, nullptr)); dbg_sync(s, "k_mln group sums");
+        return 0;
+      };
+    if (const int rc = verify_groups(ctx, b, gbufs, gt_chunks, indiv_verdict, s, grp_cap, grp_mem_cap,
+                                     gsums ? &sums_fn : nullptr))
+      return rc;
     HIPC(ctx, hipEventRecord(ctx->ev[8], s));
     HIPC(ctx, hipEventRecord(ctx->ev1, s));
     HIPC(ctx, hipStreamSynchronize(s));

@@ -87,7 +87,9 @@ __global__ __launch_bounds__(COOP_LANES) void k_indiv_coop(PipeBufs b, const Coo
   bool first = true;
   const uint32_t stride = b.fold > 1 ? b.fold : 1u;  // f's pre-multiplied in groups by k_fold
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set(b, env, sh, i, first);
-  if (b.sigagg) fin_accumulate_set(b, env, sh, b.indiv_vbase + t, first);  // the request's own signature sum
+  // the request's own signature sum (a group-tested request under group sums: its tests'
+  // sums instead, k_group_coop)
+  if (b.sigagg && (t < gb.n_direct || !gb.sum_f)) fin_accumulate_set(b, env, sh, b.indiv_vbase + t, first);
   if (t >= gb.n_direct) {  // group-tested: the product only (k_group_coop)
     if (threadIdx.x < 12) reinterpret_cast<Fp*>(&gb.f[t])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
     if (threadIdx.x == 0) b.indiv_verdict[t] = 2;
@@ -116,6 +118,10 @@ __global__ __launch_bounds__(COOP_LANES) void k_group_coop(const CoopEnv* __rest
       coop_load(sh.frame, FIN_G, src, 12);
       coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
     }
+  }
+  if (gb.sum_f) {  // the test's own signature-sum pairing (group sums)
+    coop_load(sh.frame, FIN_G, reinterpret_cast<const Fp*>(&gb.sum_f[g]), 12);
+    coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
   }
   bool ok = fin_finish(env, sh);
   if (threadIdx.x == 0) gb.verdict[g] = ok ? 1 : 0;
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(2 * COOP_LANES) void k_indiv_coop2(PipeBufs b, cons
   bool first = true;
   const uint32_t stride = b.fold > 1 ? b.fold : 1u;
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) fin_accumulate_set2(b, env, sh, i, first, w0);
-  if (b.sigagg) fin_accumulate_set2(b, env, sh, b.indiv_vbase + t, first, w0);
+  if (b.sigagg && (t < gb.n_direct || !gb.sum_f)) fin_accumulate_set2(b, env, sh, b.indiv_vbase + t, first, w0);
   if (t >= gb.n_direct) {
     if (threadIdx.x < 12) reinterpret_cast<Fp*>(&gb.f[t])[threadIdx.x] = coop_get(sh.frame, FIN_F + threadIdx.x);
     if (threadIdx.x == 0) b.indiv_verdict[t] = 2;

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)
   Fp12 F = fp12_one();
   const uint32_t stride = b.fold > 1 ? b.fold : 1u;  // f's pre-multiplied in groups by k_fold
   for (uint32_t i = b.req_off[r]; i < b.req_off[r + 1]; i += stride) F = mul12m<false>(F, &b.f[i]);
-  if (b.sigagg) F = mul12m<false>(F, &b.f[b.indiv_vbase + t]);  // the request's own signature sum
+  if (b.sigagg && (t < gb.n_direct || !gb.sum_f)) F = mul12m<false>(F, &b.f[b.indiv_vbase + t]);  // its own sum
   if (t >= gb.n_direct) {  // group-tested: the product only (k_group_coop)
     gb.f[t] = F;
     b.indiv_verdict[t] = 2;
