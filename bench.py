@@ -214,10 +214,10 @@ def latency_curve(ctxs, works, points, sets_per_call: int, steps: int = 5) -> di
     return res
 
 
-PMC_FILE = "r05f_pmc_timed_12x22.json"   # the committed counter summary the bench line cites (timed shape)
+PMC_FILE = "r06_pmc_timed_12x22.json"    # the committed counter summary the bench line cites (timed shape)
 # the committed rocprofv3 --kernel-trace --stats summary of the timed 12 x 22 shape (the
 # dominant kernels' average launch time with ~12 passes sharing the device)
-KSTATS_FILE = "r05f_kernel_stats_timed_12x22.csv"
+KSTATS_FILE = "r06_kernel_stats_timed_12x22.csv"
 KSTATS_SETS = 22528                      # sets per pass of that run (22 calls x 1024)
 PEAK_FILE = "peak_fixed.json"            # the fixed v_mad_u64_u32 peak (median of the committed measurements)
 
@@ -637,6 +637,7 @@ def run_job_slice(ctxs, w, calls_per_pass: int, steps: int, warmup: int, dist=No
     elapsed = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
+    tot["fail_stage_ms"] = [round(float(x), 3) for x in tot["fail_stage_ms"]]
     return {"elapsed_s": elapsed, "sets": w.n_sets * steps, "calls": len(pbs) * steps, "false_requests": false_req,
             **tot}
 

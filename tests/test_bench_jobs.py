@@ -74,7 +74,8 @@ class OracleCtx:
                                      dtype=np.int32))
             retries += rt
             ok += good
-        return verdicts, SimpleNamespace(batch_retries=retries, batch_sigs_success=ok, merged_check=0)
+        return verdicts, SimpleNamespace(batch_retries=retries, batch_sigs_success=ok, merged_check=0,
+                                         device_ms=0.0, stage_ms=[0.0] * 8)
 
 
 class OraclePartialBackend:
