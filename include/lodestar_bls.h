@@ -326,8 +326,7 @@ int bls_gpu_kernel_probe(bls_gpu_ctx* ctx, const char* name, uint32_t lanes, uin
  * multiplication (kernels/k_msm.hip) whatever $BLS_MSM says. */
 #define BLS_DEBUG_MSM 64u
 /* Test / bench hook: items per lane of the Miller loops' f side (1, 2 or 4; 3 = one item
- * per two lanes; 5 / 6 = four / two items per two lanes; 0 = by the process's sets in
- * flight). */
+ * per two lanes; 0 = by the process's sets in flight). */
 #define BLS_DEBUG_MLF_PL(n) ((uint32_t)(n) << 12)
 #define BLS_DEBUG_MLF_PL_MASK 0x7000u
 /* Test / bench hook: group-test failed chunks of >= 4 requests whatever

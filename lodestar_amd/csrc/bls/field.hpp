@@ -1358,68 +1358,6 @@ BLS_HD Fp12 fp12_line_half_join(const LineHalf& own, const Fp6& m_other, const F
   return Fp12{fp6_add(aa, fp6_mul_v(bb)), fp6_sub(fp6_sub(t, aa), bb)};
 }
 
-// Two lines at once over two lanes (kernels/k_mlq.hip k_mlf2n, four items per lane pair):
-// fp12_mul_line2's 23 Fp2 products as 12 per lane.  Every product takes h-selected
-// operands (a lane-varying branch would run both sides), so both halves run the same code:
-//   stage 1, the lines' product L M: half 0 the diagonal products l_k m_k (k = 0, 2, 3),
-//            half 1 the Karatsuba cross products (l_j + l_k)(m_j + m_k); swapped, both form
-//            P = (a0, a2, m22) + (0, a3, a5) w (fp12_mul_line2's names);
-//   stage 2: half 0 t0 = f.c0 P.c0, half 1 s = (f.c0 + f.c1)(P.c0 + P.c1); the five Fp2
-//            products of u = f.c1 (a3 + a5 v) as three per half (half 0: c2 a5, c2 a3 and a
-//            copy of c0 a3; half 1: c0 a3, c1 a5, (c0 + c1)(a3 + a5)); swapped, both join:
-//            t1 = v u, f' = (t0 + v t1, s - t0 - t1).
-// Host-tested against fp12_mul_line2 with both halves run one after the other
-// (test_hostsim.py::test_fp12_line2_halves).
-struct Line2Stage1 {
-  Fp2 x[3];
-};
-BLS_HD Line2Stage1 fp12_line2_half_prod1(const Fp2& l0, const Fp2& l2, const Fp2& l3, const Fp2& m0, const Fp2& m2,
-                                         const Fp2& m3, bool h) {
-  Line2Stage1 r;
-  r.x[0] = fp2_mul_s(h ? fp2_add_nr(l0, l2) : l0, h ? fp2_add_nr(m0, m2) : m0);
-  r.x[1] = fp2_mul_s(h ? fp2_add_nr(l0, l3) : l2, h ? fp2_add_nr(m0, m3) : m2);
-  r.x[2] = fp2_mul_s(h ? fp2_add_nr(l2, l3) : l3, h ? fp2_add_nr(m2, m3) : m3);
-  return r;
-}
-struct Line2P {
-  Fp2 a0, a2, m22, a3, a5;
-};
-BLS_HD Line2P fp12_line2_half_join1(const Line2Stage1& own, const Line2Stage1& other, bool h) {
-  const Line2Stage1& d = h ? other : own;  // m00, m22, m33
-  const Line2Stage1& c = h ? own : other;  // s02, s03, s23
-  Line2P p;
-  p.a0 = fp2_add(d.x[0], fp2_mul_xi(d.x[2]));
-  p.a2 = fp2_sub(fp2_sub(c.x[0], d.x[0]), d.x[1]);
-  p.a3 = fp2_sub(fp2_sub(c.x[1], d.x[0]), d.x[2]);
-  p.a5 = fp2_sub(fp2_sub(c.x[2], d.x[1]), d.x[2]);
-  p.m22 = d.x[1];
-  return p;
-}
-struct Line2Stage2 {
-  Fp6 z;
-  Fp2 y[3];
-};
-BLS_HD Line2Stage2 fp12_line2_half_prod2(const Fp12& f, const Line2P& p, bool h) {
-  Line2Stage2 r;
-  const Fp6 b0 = Fp6{p.a0, p.a2, p.m22};
-  const Fp6 b1 = Fp6{p.a0, fp2_add(p.a2, p.a3), fp2_add(p.m22, p.a5)};
-  r.z = fp6_mul(h ? fp6_add(f.c0, f.c1) : f.c0, h ? b1 : b0);
-  const Fp6& g = f.c1;
-  r.y[0] = fp2_mul_s(h ? g.c0 : g.c2, h ? p.a3 : p.a5);
-  r.y[1] = fp2_mul_s(h ? g.c1 : g.c2, h ? p.a5 : p.a3);
-  r.y[2] = fp2_mul_s(h ? fp2_add_nr(g.c0, g.c1) : g.c0, h ? fp2_add_nr(p.a3, p.a5) : p.a3);
-  return r;
-}
-BLS_HD Fp12 fp12_line2_half_join2(const Line2Stage2& own, const Line2Stage2& other, bool h) {
-  const Line2Stage2& e = h ? other : own;  // t0; c2 a5, c2 a3
-  const Line2Stage2& o = h ? own : other;  // s; c0 a3, c1 a5, (c0 + c1)(a3 + a5)
-  const Fp2 u0 = fp2_add(o.y[0], fp2_mul_xi(e.y[0]));
-  const Fp2 u1 = fp2_sub(fp2_sub(o.y[2], o.y[0]), o.y[1]);
-  const Fp2 u2 = fp2_add(o.y[1], e.y[1]);
-  const Fp6 t1 = fp6_mul_v(Fp6{u0, u1, u2});
-  return Fp12{fp6_add(e.z, fp6_mul_v(t1)), fp6_sub(fp6_sub(o.z, e.z), t1)};
-}
-
 BLS_HD Fp12 fp12_inv(const Fp12& a) {
   Fp6 n = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
   Fp6 ni = fp6_inv(n);

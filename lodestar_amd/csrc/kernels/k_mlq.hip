@@ -240,91 +240,6 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
   if (!h) b.f[i] = fp12_conj(f);
 }
 
-// ---------------------------------------------------------------------------
-// k_mlf2n: up to four items of one product domain per lane PAIR sharing f (one squaring
-// per bit for all of them, as k_mlf's four items per lane), each step's products split
-// over the pair: the squaring as k_mlf2's halves, two items' lines at once as
-// fp12_line2_half_* (12 Fp2 products per lane where fp12_mul_line2 has 23).  Half the
-// f chain of k_mlf at the same items per f; ~4 % more products per item (one duplicated
-// Fp2 product per line pair) plus the swaps and operand selects.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ Line2Stage1 pair_swap(const Line2Stage1& a) {
-  return Line2Stage1{{pair_swap(a.x[0]), pair_swap(a.x[1]), pair_swap(a.x[2])}};
-}
-__device__ __forceinline__ Line2Stage2 pair_swap(const Line2Stage2& a) {
-  return Line2Stage2{pair_swap(a.z), {pair_swap(a.y[0]), pair_swap(a.y[1]), pair_swap(a.y[2])}};
-}
-
-__device__ __forceinline__ Fp12 mul_line2_pair(const Fp12& f, const Fp2& l0, const Fp2& l2, const Fp2& l3,
-                                               const Fp2& m0, const Fp2& m2, const Fp2& m3, bool h) {
-  const Line2Stage1 s1 = fp12_line2_half_prod1(l0, l2, l3, m0, m2, m3, h);
-  const Line2P p = fp12_line2_half_join1(s1, pair_swap(s1), h);
-  const Line2Stage2 s2 = fp12_line2_half_prod2(f, p, h);
-  return fp12_line2_half_join2(s2, pair_swap(s2), h);
-}
-
-// ml_f over a lane pair: both lanes end with the same f
-__device__ __forceinline__ Fp12 ml_f_pair(const uint32_t* L, uint32_t stride, uint32_t k0, uint32_t n, bool h) {
-  Fp12 f = fp12_one();
-  int e = 0;
-  const uint64_t X = BLS_X_ABS;
-  for (int bit = 62; bit >= 0; --bit) {
-    if (bit != 62) f = sqr12_pair(f, h);
-    const int adds = (int)((X >> bit) & 1ull);
-    for (int a = 0; a <= adds; ++a) {
-      uint32_t g = 0;
-#pragma unroll 1
-      for (; g + 1 < n; g += 2) {
-        Fp2 l0, l2, l3, m0, m2, m3;
-        load_line(L, stride, k0 + g, e, l0, l2, l3);
-        load_line(L, stride, k0 + g + 1, e, m0, m2, m3);
-        f = mul_line2_pair(f, l0, l2, l3, m0, m2, m3, h);
-      }
-#pragma unroll 1
-      for (; g < n; ++g) {
-        Fp2 l0, l2, l3;
-        load_line(L, stride, k0 + g, e, l0, l2, l3);
-        f = mul_line12_pair(f, l0, l2, l3, h);
-      }
-      ++e;
-    }
-  }
-  return fp12_conj(f);
-}
-
-template <int W>
-__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W))) void k_mlf2n(
-    PipeBufs b, uint32_t first, uint32_t count, uint32_t units_paired, const uint32_t* L, uint32_t stride,
-    const uint32_t* items, uint32_t per_pair) {
-  const uint32_t t = blockIdx.x * BLS_BLOCK + threadIdx.x;
-  const uint32_t k0 = per_pair * (t >> 1);
-  const bool h = (t & 1u) != 0u;
-  // both lanes of a pair read the same items and take the same branches: the partner of
-  // every swap is active
-  if (k0 >= count) return;
-  const uint32_t n = min(per_pair, count - k0);
-  const uint32_t i0 = items ? items[k0] : first + k0;
-  bool share = n > 1 && units_paired && b.ml_dom && !items && ml_live(b, i0, units_paired);
-  for (uint32_t g = 1; share && g < n; ++g) {
-    const uint32_t i = first + k0 + g;
-    share = ml_live(b, i, units_paired) && i < b.indiv_vbase && b.ml_dom[i] == b.ml_dom[i0];
-  }
-  if (share) {
-    const Fp12 f = ml_f_pair(L, stride, k0, n, h);
-    if (!h) b.f[i0] = f;
-    else
-      for (uint32_t g = 1; g < n; ++g) b.f[first + k0 + g] = fp12_one();
-    return;
-  }
-  for (uint32_t g = 0; g < n; ++g) {
-    const uint32_t i = items ? items[k0 + g] : first + k0 + g;
-    if (ml_live(b, i, units_paired)) {
-      const Fp12 f = ml_f_pair(L, stride, k0 + g, 1, h);
-      if (!h) b.f[i] = f;
-    }
-  }
-}
-
 // line buffer words for a launch of `count` items (stride padded to a wavefront)
 size_t mlq_line_words(uint32_t count) {
   const size_t stride = ((size_t)count + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
@@ -345,8 +260,9 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
   // flight, 2.76M vs 2.90M with 128k (profiles/r03_ab_mlq_mlf.json).  By default the
   // process's sets in flight (every context's verify call, bls_sets_in_flight) pick:
   // 2 above $BLS_MLF_PL2_MIN (default 98,304) sets, 4 above $BLS_MLF_PL4_MIN (200,000:
-  // 3.55M vs 3.41M sets/s at 12 x 22), else 1.  $BLS_MLF_PER_LANE = 1, 2, 4, 3 (MLF_PAIR),
-  // 5 (MLF_PAIR4: four items per lane pair, k_mlf2n) or 6 (MLF_PAIR2: two) fixes it.
+  // 3.55M vs 3.41M sets/s at 12 x 22), else 1.  $BLS_MLF_PER_LANE = 1, 2, 4 or 3 (MLF_PAIR)
+  // fixes it.  (Four items sharing f per lane PAIR, the squarings and line products split
+  // over the pair, lost 6-11 %: spills and ~9 % more lane work, profiles/r06_ab_mlf_pair4.json.)
   // Up to $BLS_MLF_PAIR_MAX (16,384) sets in flight: two lanes per item (k_mlf2, MLF_PAIR;
   // at two waves per SIMD, $BLS_MLF2_WAVES=1 for one): a solo pass's f side 4.7 vs 7.1 ms
   // at 8,192 sets, 5.2 vs 7.2 ms at 16,384, but 8.8 vs 7.4 ms at 32,768
@@ -361,14 +277,6 @@ hipError_t launch_k_mlqf(const PipeBufs& b, uint32_t first, uint32_t count, bool
     else k_mlf2<1><<<bls_grid_for(2 * count), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items);
     return hipGetLastError();
   }
-  if (per_lane == MLF_PAIR4 || per_lane == MLF_PAIR2) {
-    // up to four (or two) items sharing f per lane PAIR (k_mlf2n), one wavefront per SIMD
-    // (at two it needs 3,168 B/lane of scratch: 415 MB per queue, past k_chain's reservation)
-    const uint32_t pp = per_lane == MLF_PAIR4 ? 4u : 2u;
-    const uint32_t pair_lanes = 2 * ((count + pp - 1) / pp);
-    k_mlf2n<1><<<bls_grid_for(pair_lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, pp);
-    return hipGetLastError();
-  }
   const uint32_t lanes = (count + per_lane - 1) / per_lane;
   k_mlf<1><<<bls_grid_for(lanes), BLS_BLOCK, 0, s>>>(b, first, count, up, lines, stride, items, per_lane);
   return hipGetLastError();
@@ -378,9 +286,7 @@ uint32_t mlf_per_lane_fixed() {
   static const uint32_t fixed = [] {
     const char* e = getenv("BLS_MLF_PER_LANE");
     const int v = e ? atoi(e) : 0;
-    return (v == 1 || v == 2 || v == 4 || v == (int)MLF_PAIR || v == (int)MLF_PAIR4 || v == (int)MLF_PAIR2)
-               ? (uint32_t)v
-               : 0u;
+    return (v == 1 || v == 2 || v == 4 || v == (int)MLF_PAIR) ? (uint32_t)v : 0u;
   }();
   return fixed;
 }

@@ -48,9 +48,6 @@ size_t msm_seg_cap(uint32_t n_sets);
 #define MSM_MAX_SETS (1u << 21)
 // mlf_per_lane(): one item per TWO f lanes (kernels/k_mlq.hip k_mlf2)
 #define MLF_PAIR 3u
-// ... up to four (MLF_PAIR4) or two (MLF_PAIR2) items sharing f per TWO lanes (k_mlf2n)
-#define MLF_PAIR4 5u
-#define MLF_PAIR2 6u
 // the merged signature sum into the chunk groups' virtual sets vbase .. vbase + groups
 hipError_t launch_k_msm(const bls::PipeBufs& b, const MsmBufs& m, uint32_t groups, uint32_t vbase, hipStream_t s);
 hipError_t launch_k_gsum(const bls::PipeBufs& b, const uint32_t* seg, uint32_t n_seg, const bls::G2J* in,

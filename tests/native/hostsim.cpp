@@ -215,19 +215,6 @@ void hs_fp12_mul_line2(const uint8_t* f, const uint8_t* l, const uint8_t* m, uin
                          rd_fp2(m + 192)),
           out);
 }
-// two lines at once over two lanes (k_mlf2n): both halves' stage products, swapped, joined
-// by each half; out: half 0's result then half 1's
-void hs_fp12_mul_line2_pair(const uint8_t* f, const uint8_t* l, const uint8_t* m, uint8_t* out) {
-  const Fp12 x = rd_fp12(f);
-  const Fp2 l0 = rd_fp2(l), l2 = rd_fp2(l + 96), l3 = rd_fp2(l + 192);
-  const Fp2 m0 = rd_fp2(m), m2 = rd_fp2(m + 96), m3 = rd_fp2(m + 192);
-  const Line2Stage1 a0 = fp12_line2_half_prod1(l0, l2, l3, m0, m2, m3, false);
-  const Line2Stage1 a1 = fp12_line2_half_prod1(l0, l2, l3, m0, m2, m3, true);
-  const Line2P p0 = fp12_line2_half_join1(a0, a1, false), p1 = fp12_line2_half_join1(a1, a0, true);
-  const Line2Stage2 b0 = fp12_line2_half_prod2(x, p0, false), b1 = fp12_line2_half_prod2(x, p1, true);
-  wr_fp12(fp12_line2_half_join2(b0, b1, false), out);
-  wr_fp12(fp12_line2_half_join2(b1, b0, true), out + 576);
-}
 void hs_final_exp(const uint8_t* a, uint8_t* out) { wr_fp12(final_exponentiation(rd_fp12(a)), out); }
 
 void hs_miller_loop(const uint8_t* g1, const uint8_t* g2, uint8_t* out) {

@@ -972,11 +972,10 @@ def test_msm_signature_sum_matches_chains(gpu, oracle, table, verify_path):
         assert (st.batch_retries, st.batch_sigs_success) == (ref_st.batch_retries, ref_st.batch_sigs_success) == (retries, ok)
 
 
-@pytest.mark.parametrize("per_lane", [1, 2, 4, 3, 5, 6])
+@pytest.mark.parametrize("per_lane", [1, 2, 4, 3])
 def test_mlf_items_per_lane(gpu, oracle, table, verify_path, per_lane):
-    """The f side of the split Miller loops with 1, 2 or 4 items per lane, one item per
-    two lanes (3 = MLF_PAIR, k_mlf2) or four / two items sharing f per two lanes (5 / 6 =
-    MLF_PAIR4 / MLF_PAIR2, k_mlf2n) (the library picks by the sets in flight;
+    """The f side of the split Miller loops with 1, 2 or 4 items per lane or one item per
+    two lanes (3 = MLF_PAIR, k_mlf2) (the library picks by the sets in flight;
     BLS_DEBUG_MLF_PL forces it), with and without the
     Pippenger signature sum: invalid sets at a chunk's first, middle and last position and
     in the last chunk, and an undecodable signature, so lanes whose items do not all share

@@ -235,25 +235,6 @@ def test_fp12_pair_halves(hostsim):
         assert o2.raw[:576] == o2.raw[576:] == o1.raw
 
 
-def test_fp12_line2_halves(hostsim):
-    """Two lines at once over two lanes (k_mlf2n, field.hpp fp12_line2_half_*): each half's
-    stage products, swapped with the other's, give both halves fp12_mul_line2's result."""
-    rng = random.Random(15)
-    o1, o2 = _buf(576), _buf(2 * 576)
-    for _ in range(20):
-        f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
-        ls = [b"".join(f2b((rng.randrange(P), rng.randrange(P))) for _ in range(3)) for _ in range(2)]
-        hostsim.hs_fp12_mul_line2(f12b(f), ls[0], ls[1], o1)
-        hostsim.hs_fp12_mul_line2_pair(f12b(f), ls[0], ls[1], o2)
-        assert o2.raw[:576] == o2.raw[576:] == o1.raw
-    # canonical extremes: every coefficient p - 1
-    e = (P - 1, P - 1)
-    hostsim.hs_fp12_mul_line2(f12b([e] * 6), b"".join(f2b(e) for _ in range(3)), b"".join(f2b(e) for _ in range(3)), o1)
-    hostsim.hs_fp12_mul_line2_pair(f12b([e] * 6), b"".join(f2b(e) for _ in range(3)),
-                                   b"".join(f2b(e) for _ in range(3)), o2)
-    assert o2.raw[:576] == o2.raw[576:] == o1.raw
-
-
 def test_hash_to_g2_golden(hostsim, golden):
     o = _buf(192)
     for v in golden["hash_to_g2"]:
