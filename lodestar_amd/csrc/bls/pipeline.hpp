@@ -141,6 +141,11 @@ struct GroupBufs {
   // ML(-g1, sum of its requests' r sig) in sum_f[g], and a group-tested request's F_t
   // holds its sets' f only; nullptr: each F_t holds its own request sum's pairing
   const Fp12* sum_f;
+  // complement inference (bls_gpu.hip verify_groups): test g's final exponentiation kept
+  // in fe[g] (canonical), and k_group_cmp sets bit 1 of verdict[g] when it equals that of
+  // test ref[g] (its chunk's test of all requests; ~0u: none); fe nullptr: neither
+  Fp12* fe;
+  const uint32_t* ref;
 };
 
 BLS_HD void scalar_words_from_be32(const uint8_t* b, uint32_t k[8]) {

@@ -688,15 +688,17 @@ static void dbg_sync(hipStream_t s, const char* what) {
 // aggregated path, its own signature-sum pairing) is left by k_indiv_coop; a test is
 // FE(prod of a group's F_t) == 1 (k_group_coop), the same random-scalar batch check the
 // reference runs over a chunk.  With the chunk's requests of status OK indexed 0 .. m-1:
-//   pass A: the group of all of them if the chunk failed on an erroneous request (its
-//           batch would throw, worker.ts:81-87: the others may all be valid), and for
-//           each bit j of the index the group of those with bit j set;
-//   a single invalid request b fails exactly the bit groups of b's index, so
-//   pass B: {b} alone (must fail) and the others together (must pass);
-//   pass C: any other outcome (two or more invalid, an index past m): every request
-//           alone.
-// With one invalid request in a chunk of 16 that is 6 final exponentiations instead of
-// 16; verdicts and the worker counters are the reference's (a test that passes is the
+//   pass A: the group of all of them (A), and for each bit j of the index the group G_j
+//           of those with bit j set; each G_j's final exponentiation is also compared with
+//           A's (k_group_cmp): FE(G_j) FE(rest_j) = FE(A), so FE(rest_j) == 1 iff
+//           FE(G_j) == FE(A) -- every test answers for its complement too;
+//   a single invalid request b fails exactly one of G_j, rest_j for every j (G_j where
+//   b's bit j is set), which names b, and every other request sits in a passing test;
+//   pass C: any other outcome (both of some G_j, rest_j failing: two or more invalid; an
+//           index past m): every request alone.
+// With one invalid request in a chunk of 16 that is 5 final exponentiations in one round
+// instead of 16 (round 6; before it, without the comparison, pass B tested {b} alone and
+// the rest together: 6 in two rounds, $BLS_GROUP_EQ=0 restores that); verdicts and the worker counters are the reference's (a test that passes is the
 // batch the reference's retry would have passed request by request, with the same
 // soundness).  On for chunks of >= 4 requests since round 6: once the failed chunks'
 // requests stopped re-running their sets' own Miller loops and the chunks of a failing
@@ -739,11 +741,24 @@ static bool group_sums_on(size_t n_group_tested) {
   return on && n_group_tested >= min_reqs;
 }
 
-// run the tests (goff: offsets into gmem, indices into the indiv list); results in gv;
+// complement inference in the group tests (verify_groups): pass A carries each chunk's
+// test of all its requests and compares the bit groups' final exponentiations with it, so
+// one invalid request is found without pass B ({b} alone, the rest together);
+// $BLS_GROUP_EQ=0 restores the two rounds
+static bool group_eq_on() {
+  static const bool on = [] {
+    const char* e = getenv("BLS_GROUP_EQ");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// run the tests (goff: offsets into gmem, indices into the indiv list); results in gv
+// (bit 0: passed; bit 1, with ref: its final exponentiation equals test ref[g]'s);
 // 1 when the group sums do not fit (nothing ran)
 static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, const std::vector<uint32_t>& goff,
                            const std::vector<uint32_t>& gmem, std::vector<int32_t>& gv, hipStream_t s,
-                           const GroupSums* sums) {
+                           const GroupSums* sums, const std::vector<uint32_t>* ref = nullptr) {
   gv.assign(goff.size() - 1, 0);
   if (gv.empty()) return 0;
   if (sums && *sums) {
@@ -753,7 +768,10 @@ static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, co
   stage_copy(ctx, g.off, goff.data(), sizeof(uint32_t) * goff.size());  // the stream is idle
   stage_copy(ctx, g.members, gmem.data(), sizeof(uint32_t) * gmem.size());
   g.n = (uint32_t)gv.size();
-  HIPC(ctx, launch_k_group_coop(b, ctx->coop, g, s)); dbg_sync(s, "k_group_coop");
+  GroupBufs gg = g;
+  if (ref) stage_copy(ctx, g.ref, ref->data(), sizeof(uint32_t) * ref->size());
+  else gg.fe = nullptr;
+  HIPC(ctx, launch_k_group_coop(b, ctx->coop, gg, s)); dbg_sync(s, "k_group_coop");
   HIPC(ctx, hipStreamSynchronize(s));
   memcpy(gv.data(), res_host(ctx, g.verdict), sizeof(int32_t) * gv.size());
   return 0;
@@ -769,10 +787,12 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
     int32_t b = -1;            // the one invalid request's position in ok (pass B), -1 none
   };
   std::vector<Chunk> cs;
-  std::vector<uint32_t> goff{0}, gmem;
-  auto add_test = [&](const std::vector<uint32_t>& m) {
+  std::vector<uint32_t> goff{0}, gmem, ref;
+  const bool eq = group_eq_on() && gbufs.fe;
+  auto add_test = [&](const std::vector<uint32_t>& m, uint32_t r) {
     gmem.insert(gmem.end(), m.begin(), m.end());
     goff.push_back((uint32_t)gmem.size());
+    ref.push_back(r);
   };
   for (const auto& ch : chunks) {
     Chunk c;
@@ -782,14 +802,14 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
     }
     if (c.ok.empty()) continue;
     c.first = (uint32_t)goff.size() - 1;
-    if (c.has_err || c.ok.size() == 1) add_test(c.ok);
+    if (eq || c.has_err || c.ok.size() == 1) add_test(c.ok, ~0u);
     const uint32_t m = (uint32_t)c.ok.size();
     while (m > 1 && (1u << c.nbits) < m) ++c.nbits;
     for (uint32_t j = 0; j < c.nbits; ++j) {
       std::vector<uint32_t> g;
       for (uint32_t k = 0; k < m; ++k)
         if ((k >> j) & 1u) g.push_back(c.ok[k]);
-      add_test(g);
+      add_test(g, c.first);
     }
     cs.push_back(std::move(c));
   }
@@ -800,12 +820,41 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
   std::vector<int32_t> gv;
   std::vector<uint32_t> goff_b{0}, gmem_b, alone;  // alone: requests for pass C
   std::vector<size_t> in_b;
-  const int rc_a = run_group_tests(ctx, b, gbufs, goff, gmem, gv, s, sums);
+  const int rc_a = run_group_tests(ctx, b, gbufs, goff, gmem, gv, s, sums, eq ? &ref : nullptr);
   if (rc_a < 0) return -1;
   if (rc_a == 1) {  // the group sums of pass A do not fit: every request alone
     for (const Chunk& c : cs) alone.insert(alone.end(), c.ok.begin(), c.ok.end());
     cs.clear();
   }
+  // complement inference: with the test of all the chunk's requests (A) beside each bit
+  // group G_j, FE(G_j) FE(rest_j) = FE(A) decides the complement too (FE(rest_j) == 1 iff
+  // FE(G_j) == FE(A)), so a single invalid request b shows as exactly one failing test per
+  // bit -- G_j where b's bit j is set, rest_j where it is clear -- and every other request
+  // sits in a passing test: no pass B.  Both G_j and rest_j failing (two or more invalid)
+  // or an index past m: pass C.
+  for (size_t i = 0; eq && i < cs.size(); ++i) {
+    const Chunk& c = cs[i];
+    const uint32_t m = (uint32_t)c.ok.size();
+    const bool pass = (gv[c.first] & 1) != 0;
+    if (pass || m == 1) {
+      for (uint32_t t : c.ok) verdict[t] = pass ? 1 : 0;
+      continue;
+    }
+    uint32_t bad = 0;
+    bool consistent = true;
+    for (uint32_t j = 0; j < c.nbits; ++j) {
+      const int32_t v = gv[c.first + 1 + j];
+      const bool one = (v & 1) != 0, same = (v & 2) != 0;
+      if (one == same) consistent = false;
+      if (!one) bad |= 1u << j;
+    }
+    if (!consistent || bad >= m) {
+      alone.insert(alone.end(), c.ok.begin(), c.ok.end());
+      continue;
+    }
+    for (uint32_t k = 0; k < m; ++k) verdict[c.ok[k]] = k == bad ? 0 : 1;
+  }
+  if (eq) cs.clear();
   // decode pass A; plan pass B
   for (size_t i = 0; i < cs.size(); ++i) {
     Chunk& c = cs[i];
@@ -833,7 +882,7 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
     goff_b.push_back((uint32_t)gmem_b.size());
     in_b.push_back(i);
   }
-  const int rc_b = run_group_tests(ctx, b, gbufs, goff_b, gmem_b, gv, s, sums);
+  const int rc_b = in_b.empty() ? 0 : run_group_tests(ctx, b, gbufs, goff_b, gmem_b, gv, s, sums);
   if (rc_b < 0) return -1;
   for (size_t q = 0; q < in_b.size(); ++q) {
     Chunk& c = cs[in_b[q]];
@@ -1294,6 +1343,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.indiv_reqs = c.take<uint32_t>(R);
     gbufs.off = c.take<uint32_t>(gt_possible ? grp_cap + 1 : 0);
     gbufs.members = c.take<uint32_t>(grp_mem_cap);
+    gbufs.ref = c.take<uint32_t>(gt_possible ? grp_cap : 0);
     own_sets_dev = sigagg ? c.take<uint32_t>((size_t)n + R) : nullptr;
     b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
     b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
@@ -1339,6 +1389,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     }
     b.req_status = c.take<int32_t>(R);
     gbufs.f = gt_possible ? c.take<Fp12>(R) : nullptr;
+    gbufs.fe = gt_possible ? c.take<Fp12>(grp_cap) : nullptr;
     fe_save = fe_simt_possible ? c.take<Fp12>(4ull * (n_chunks > R ? n_chunks : R)) : nullptr;
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);

@@ -124,12 +124,31 @@ __global__ __launch_bounds__(COOP_LANES) void k_group_coop(const CoopEnv* __rest
     coop_run(env, env.fin_fmul, sh.frame, sh.cbank, &sh.flag);
   }
   bool ok = fin_finish(env, sh);
+  if (gb.fe && threadIdx.x < 12)
+    reinterpret_cast<Fp*>(&gb.fe[g])[threadIdx.x] = fp_reduce_once(coop_get(sh.frame, FIN_F + threadIdx.x));
   if (threadIdx.x == 0) gb.verdict[g] = ok ? 1 : 0;
+}
+
+// bit 1 of verdict[g]: FE of test g == FE of test ref[g] (one lane per test, after
+// k_group_coop in stream order)
+__global__ __launch_bounds__(BLS_BLOCK) void k_group_cmp(GroupBufs gb) {
+  const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  if (g >= gb.n) return;
+  const uint32_t r = gb.ref[g];
+  if (r >= gb.n) return;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(&gb.fe[g]);
+  const uint32_t* c = reinterpret_cast<const uint32_t*>(&gb.fe[r]);
+  uint32_t diff = 0;
+  for (int k = 0; k < 144; ++k) diff |= a[k] ^ c[k];
+  if (diff == 0) gb.verdict[g] |= 2;
 }
 
 hipError_t launch_k_group_coop(const PipeBufs&, const CoopEnv& env, const GroupBufs& g, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   k_group_coop<<<g.n, COOP_LANES, 0, s>>>(env.dev, g);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !g.fe || !g.ref) return e;
+  k_group_cmp<<<bls_grid_for(g.n), BLS_BLOCK, 0, s>>>(g);
   return hipGetLastError();
 }
 

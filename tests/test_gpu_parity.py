@@ -895,8 +895,10 @@ def test_failed_chunk_requests_verified_alone(gpu, oracle, table, n, bad):
 
 
 def test_failed_chunks_group_tested(gpu, oracle, table, verify_path):
-    """Failed chunks are group-tested (bls_gpu.hip verify_groups: bit-index groups, then
-    the decoded request alone and the rest together, else every request alone): one
+    """Failed chunks are group-tested (bls_gpu.hip verify_groups: the test of all the
+    chunk's requests beside its bit-index groups, each group's final exponentiation also
+    compared with the whole's, so a single invalid request is decoded in one round, else
+    every request alone): one
     invalid request at the first / a middle / the last position, two in one chunk (the
     every-request-alone pass), an undecodable signature with every other request valid
     (the group of the rest passes), an undecodable one next to an invalid one, and the
