@@ -124,6 +124,8 @@ struct PipeBufs {
   // outputs
   int32_t* chunk_ok;       // n_chunks: 1 ok, 0 failed (retry)
   int32_t* indiv_verdict;  // n_indiv: 1 / 0 / -code (2: product left for the group tests)
+  Fp12* chunk_fe;          // n_chunks: k_chunk_coop's final exponentiation (canonical), for
+                           // the group tests' complement inference; nullptr: not kept
 };
 
 // Group tests over failed chunks' requests (bls_gpu.hip verify_groups; kernels/k_fin.hip):
@@ -143,10 +145,14 @@ struct GroupBufs {
   const Fp12* sum_f;
   // complement inference (bls_gpu.hip verify_groups): test g's final exponentiation kept
   // in fe[g] (canonical), and k_group_cmp sets bit 1 of verdict[g] when it equals that of
-  // test ref[g] (its chunk's test of all requests; ~0u: none); fe nullptr: neither
+  // test ref[g] (its chunk's test of all requests; REF_NONE: none); fe nullptr: neither
   Fp12* fe;
   const uint32_t* ref;
+  // ref[g] = REF_CHUNK | c: compare with chunk c's checked value ref_fe[c] instead
+  const Fp12* ref_fe;
 };
+#define REF_CHUNK 0x80000000u
+#define REF_NONE 0xFFFFFFFFu  // no comparison (the chunk indices stay far below 2^31 - 1)
 
 BLS_HD void scalar_words_from_be32(const uint8_t* b, uint32_t k[8]) {
   for (int i = 0; i < 8; ++i) {

@@ -743,15 +743,18 @@ static bool group_sums_on(size_t n_group_tested) {
 
 // complement inference in the group tests (verify_groups): pass A carries each chunk's
 // test of all its requests and compares the bit groups' final exponentiations with it, so
-// one invalid request is found without pass B ({b} alone, the rest together);
-// $BLS_GROUP_EQ=0 restores the two rounds
-static bool group_eq_on() {
-  static const bool on = [] {
+// one invalid request is found without pass B ({b} alone, the rest together); the whole's
+// value is the failed chunk check's own final exponentiation where that ran over the same
+// requests (k_chunk_coop keeps it in b.chunk_fe), else a test of them.  $BLS_GROUP_EQ=0
+// restores the two rounds, =2 always tests the whole
+static int group_eq_mode() {
+  static const int mode = [] {
     const char* e = getenv("BLS_GROUP_EQ");
-    return !(e && atoi(e) == 0);
+    return e ? atoi(e) : 1;
   }();
-  return on;
+  return mode;
 }
+static bool group_eq_on() { return group_eq_mode() != 0; }
 
 // run the tests (goff: offsets into gmem, indices into the indiv list); results in gv
 // (bit 0: passed; bit 1, with ref: its final exponentiation equals test ref[g]'s);
@@ -777,12 +780,18 @@ static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, co
   return 0;
 }
 
-static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
-                         const std::vector<std::pair<uint32_t, uint32_t>>& chunks, std::vector<int32_t>& verdict,
-                         hipStream_t s, size_t grp_cap, size_t grp_mem_cap, const GroupSums* sums) {
+struct GtChunk {
+  uint32_t beg, end;  // its requests in the indiv list
+  uint32_t ch;        // its chunk (b.chunk_fe)
+};
+
+static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs, const std::vector<GtChunk>& chunks,
+                         std::vector<int32_t>& verdict, hipStream_t s, size_t grp_cap, size_t grp_mem_cap,
+                         const GroupSums* sums) {
   struct Chunk {
     std::vector<uint32_t> ok;  // indiv indices of the requests of status OK
     bool has_err = false;
+    bool whole = false;        // a test of all of ok at `first` (else the chunk check's value)
     uint32_t first = 0, nbits = 0;
     int32_t b = -1;            // the one invalid request's position in ok (pass B), -1 none
   };
@@ -796,20 +805,24 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
   };
   for (const auto& ch : chunks) {
     Chunk c;
-    for (uint32_t t = ch.first; t < ch.second; ++t) {
+    for (uint32_t t = ch.beg; t < ch.end; ++t) {
       if (verdict[t] == 2) c.ok.push_back(t);
       else c.has_err = true;  // its -code stays
     }
     if (c.ok.empty()) continue;
     c.first = (uint32_t)goff.size() - 1;
-    if (eq || c.has_err || c.ok.size() == 1) add_test(c.ok, ~0u);
+    // the whole's value: the failed chunk check's own final exponentiation when it ran
+    // over exactly these requests (no erroneous one), else a test of them
+    const bool from_check = eq && group_eq_mode() != 2 && gbufs.ref_fe && !c.has_err && c.ok.size() > 1;
+    c.whole = !from_check && (eq || c.has_err || c.ok.size() == 1);
+    if (c.whole) add_test(c.ok, REF_NONE);
     const uint32_t m = (uint32_t)c.ok.size();
     while (m > 1 && (1u << c.nbits) < m) ++c.nbits;
     for (uint32_t j = 0; j < c.nbits; ++j) {
       std::vector<uint32_t> g;
       for (uint32_t k = 0; k < m; ++k)
         if ((k >> j) & 1u) g.push_back(c.ok[k]);
-      add_test(g, c.first);
+      add_test(g, from_check ? (REF_CHUNK | ch.ch) : c.first);
     }
     cs.push_back(std::move(c));
   }
@@ -835,15 +848,17 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs,
   for (size_t i = 0; eq && i < cs.size(); ++i) {
     const Chunk& c = cs[i];
     const uint32_t m = (uint32_t)c.ok.size();
-    const bool pass = (gv[c.first] & 1) != 0;
+    // without a whole test the whole is the failed chunk check (it failed)
+    const bool pass = c.whole && (gv[c.first] & 1) != 0;
     if (pass || m == 1) {
       for (uint32_t t : c.ok) verdict[t] = pass ? 1 : 0;
       continue;
     }
+    const uint32_t bits_at = c.first + (c.whole ? 1u : 0u);
     uint32_t bad = 0;
     bool consistent = true;
     for (uint32_t j = 0; j < c.nbits; ++j) {
-      const int32_t v = gv[c.first + 1 + j];
+      const int32_t v = gv[bits_at + j];
       const bool one = (v & 1) != 0, same = (v & 2) != 0;
       if (one == same) consistent = false;
       if (!one) bad |= 1u << j;
@@ -1390,6 +1405,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     b.req_status = c.take<int32_t>(R);
     gbufs.f = gt_possible ? c.take<Fp12>(R) : nullptr;
     gbufs.fe = gt_possible ? c.take<Fp12>(grp_cap) : nullptr;
+    b.chunk_fe = gt_possible ? c.take<Fp12>(n_chunks) : nullptr;
     fe_save = fe_simt_possible ? c.take<Fp12>(4ull * (n_chunks > R ? n_chunks : R)) : nullptr;
     if (partial || merged) {
       ptree[0] = c.take<Fp12>((n_total + FPROD_FAN - 1) / FPROD_FAN);
@@ -1605,6 +1621,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     if (merged) read_merged();
   }
   bool merged_pass = merged && merged_verdict == 1;
+  bool chunk_fe_kept = false;
   for (uint32_t r = 0; merged_pass && r < R; ++r) merged_pass = merged_status[r] == BLS_OK;
   if (merged) ctx->last_merged_failed = !merged_pass;
   if (merged_pass) {
@@ -1621,7 +1638,10 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     // cooperative task holds a SIMD for a whole final exponentiation); few: one wavefront
     // each, the shorter latency
     if (fe_save && n_chunks >= fe_min) HIPC(ctx, launch_k_chunk_simt(b, fe_save, s));
-    else HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s));
+    else {
+      HIPC(ctx, launch_k_chunk_coop(b, ctx->coop, s));
+      chunk_fe_kept = b.chunk_fe != nullptr;  // the checked chunks' final exponentiations
+    }
     dbg_sync(s, "k_chunk");
     HIPC(ctx, hipStreamSynchronize(s));
     memcpy(chunk_ok.data(), res_host(ctx, b.chunk_ok), sizeof(int32_t) * n_chunks);
@@ -1701,7 +1721,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
   // instead of paying one final exponentiation per request (verify_groups below); its
   // requests follow the directly verified ones in the list.
   std::vector<uint32_t> indiv = plan.nonbatch_reqs;
-  std::vector<std::pair<uint32_t, uint32_t>> gt_chunks;  // [beg, end) of a group-tested chunk in indiv
+  std::vector<GtChunk> gt_chunks;  // [beg, end) of a group-tested chunk in indiv, its chunk
   const uint32_t gt_min = group_test_min(ctx);
   for (int pass = 0; pass < 2; ++pass)
     for (uint32_t ch = 0; ch < n_chunks; ++ch) {
@@ -1710,9 +1730,9 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       if ((m >= gt_min) != (pass == 1)) continue;
       const uint32_t beg = (uint32_t)indiv.size();
       for (uint32_t k = plan.chunk_off[ch]; k < plan.chunk_off[ch + 1]; ++k) indiv.push_back(plan.chunk_reqs[k]);
-      if (pass == 1) gt_chunks.push_back({beg, (uint32_t)indiv.size()});
+      if (pass == 1) gt_chunks.push_back({beg, (uint32_t)indiv.size(), ch});
     }
-  const uint32_t n_direct = gt_chunks.empty() ? (uint32_t)indiv.size() : gt_chunks.front().first;
+  const uint32_t n_direct = gt_chunks.empty() ? (uint32_t)indiv.size() : gt_chunks.front().beg;
   // Group sums: on the aggregated path, with many requests group-tested, a group-tested
   // request pairs no signature sum of its own; each group test pairs ONE sum over its
   // requests' sets (run_group_tests) -- 4-6 Miller loops per failed chunk of 16 instead of
@@ -1837,6 +1857,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
         HIPC(ctx, launch_ml_alone(indiv_vbase + n_direct, T, nullptr)); dbg_sync(s, "k_mln group sums");
         return 0;
       };
+    gbufs.ref_fe = chunk_fe_kept ? b.chunk_fe : nullptr;
     if (const int rc = verify_groups(ctx, b, gbufs, gt_chunks, indiv_verdict, s, grp_cap, grp_mem_cap,
                                      gsums ? &sums_fn : nullptr))
       return rc;

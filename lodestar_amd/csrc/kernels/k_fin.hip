@@ -69,6 +69,8 @@ __global__ __launch_bounds__(COOP_LANES) void k_chunk_coop(PipeBufs b, const Coo
   if (b.unit_off)
     for (uint32_t u = b.unit_off[c]; u < b.unit_off[c + 1]; ++u) fin_accumulate_set(b, env, sh, b.unit_base + u, first);
   bool ok = fin_finish(env, sh);
+  if (b.chunk_fe && threadIdx.x < 12)
+    reinterpret_cast<Fp*>(&b.chunk_fe[c])[threadIdx.x] = fp_reduce_once(coop_get(sh.frame, FIN_F + threadIdx.x));
   if (threadIdx.x == 0) b.chunk_ok[c] = ok ? 1 : 0;
 }
 
@@ -129,15 +131,17 @@ __global__ __launch_bounds__(COOP_LANES) void k_group_coop(const CoopEnv* __rest
   if (threadIdx.x == 0) gb.verdict[g] = ok ? 1 : 0;
 }
 
-// bit 1 of verdict[g]: FE of test g == FE of test ref[g] (one lane per test, after
-// k_group_coop in stream order)
+// bit 1 of verdict[g]: FE of test g == FE of test ref[g], or of checked chunk
+// ref[g] & ~REF_CHUNK (one lane per test, after k_group_coop in stream order)
 __global__ __launch_bounds__(BLS_BLOCK) void k_group_cmp(GroupBufs gb) {
   const uint32_t g = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (g >= gb.n) return;
   const uint32_t r = gb.ref[g];
-  if (r >= gb.n) return;
+  if (r == REF_NONE) return;
+  const Fp12* other = r < gb.n ? &gb.fe[r] : ((r & REF_CHUNK) && gb.ref_fe ? &gb.ref_fe[r & ~REF_CHUNK] : nullptr);
+  if (!other) return;
   const uint32_t* a = reinterpret_cast<const uint32_t*>(&gb.fe[g]);
-  const uint32_t* c = reinterpret_cast<const uint32_t*>(&gb.fe[r]);
+  const uint32_t* c = reinterpret_cast<const uint32_t*>(other);
   uint32_t diff = 0;
   for (int k = 0; k < 144; ++k) diff |= a[k] ^ c[k];
   if (diff == 0) gb.verdict[g] |= 2;

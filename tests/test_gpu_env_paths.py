@@ -22,7 +22,9 @@ tokens, multithread/worker.ts:32-108), the pass shape against the rule that pick
   its requests' sets); gsums_off (BLS_GROUP_SUMS=0): the same calls with every
   group-tested request pairing its own signature sum; group_eq_off (BLS_GROUP_EQ=0): the
   same calls with the two-round group tests (bit groups, then the decoded request alone
-  and the rest together) instead of the complement inference.
+  and the rest together) instead of the complement inference; group_eq_whole
+  (BLS_GROUP_EQ=2): the complement inference against a test of the chunk's whole request
+  list instead of the failed chunk check's own final exponentiation.
 """
 from __future__ import annotations
 
@@ -68,7 +70,7 @@ with GpuContext(0) as gpu:
         run(sets, msgs, {17, 3500}, True, True)
         run(sets, msgs, set(), True, True)
         run(sets, msgs, set(), True, True)
-    elif case in ("fe_simt", "gsums_off", "group_eq_off"):
+    elif case in ("fe_simt", "gsums_off", "group_eq_off", "group_eq_whole"):
         sets, msgs = make(1024, b"FESI")
         run(sets, msgs, {3, 400, 401, 1000}, True, True, 8)      # chunk checks + requests alone, one lane each
         run(sets, msgs, {5, 77, 78}, True, True, 8 | 128)        # ... with group testing (products only)
@@ -91,6 +93,7 @@ ENVS = {
     "fe_simt": {"BLS_FE_SIMT_MIN": "1", "BLS_GROUP_SUMS_MIN": "0"},
     "gsums_off": {"BLS_GROUP_SUMS": "0"},
     "group_eq_off": {"BLS_GROUP_EQ": "0"},
+    "group_eq_whole": {"BLS_GROUP_EQ": "2"},
 }
 
 
@@ -129,7 +132,7 @@ def test_env_selected_paths(case, oracle):
         # all pass, so the third is back on the merged check with the MSM
         assert [c["shape"] & 1 for c in calls] == [1, 0, 1]
         assert [c["merged"] for c in calls] == [2, 3, 1]
-    elif case in ("fe_simt", "gsums_off", "group_eq_off"):
+    elif case in ("fe_simt", "gsums_off", "group_eq_off", "group_eq_whole"):
         # the second call follows a failed merged check: its chunks are checked straight away
         assert calls[0]["merged"] == 2 and calls[1]["merged"] == 3 and calls[2]["shape"] == 0
     else:
