@@ -214,10 +214,11 @@ def latency_curve(ctxs, works, points, sets_per_call: int, steps: int = 5) -> di
     return res
 
 
-PMC_FILE = "r06_pmc_timed_12x22.json"    # the committed counter summary the bench line cites (timed shape)
-# the committed rocprofv3 --kernel-trace --stats summary of the timed 12 x 22 shape (the
+TIMED_SHAPE = "16 x 22"                    # the default timed region: contexts x calls per pass
+PMC_FILE = "r06_pmc_timed_16x22.json"    # the committed counter summary the bench line cites (timed shape)
+# the committed rocprofv3 --kernel-trace --stats summary of the timed 16 x 22 shape (the
 # dominant kernels' average launch time with ~12 passes sharing the device)
-KSTATS_FILE = "r06_kernel_stats_timed_12x22.csv"
+KSTATS_FILE = "r06_kernel_stats_timed_16x22.csv"
 KSTATS_SETS = 22528                      # sets per pass of that run (22 calls x 1024)
 PEAK_FILE = "peak_fixed.json"            # the fixed v_mad_u64_u32 peak (median of the committed measurements)
 
@@ -867,14 +868,16 @@ def main() -> None:
     ap.add_argument("--latency-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--inflight", type=int, default=12, help="verifier contexts (HIP streams) per GPU")
-    # default 12 contexts x 22 calls (profiles/r03_knee.json): the rate follows the sets in
-    # flight (4 x 16 2.29M at 29 ms per pass, 12 x 16 3.09M at 64 ms, 12 x 22 3.52-3.60M at
-    # 75-77 ms: past 200k sets in flight the library switches to the Pippenger signature sum
-    # and four items per k_mlf lane); a call's verdicts arrive when its pass ends, inside the
-    # reference's 100 ms job buffering (multithread/index.ts:57 MAX_BUFFER_WAIT_MS).  12
-    # contexts keep the scratch the runtime reserves per hardware queue (k_chain: 464 MiB)
-    # well under the ~8 GiB at which it aborts queues (20 contexts did,
+    ap.add_argument("--inflight", type=int, default=16, help="verifier contexts (HIP streams) per GPU")
+    # default 16 contexts x 22 calls: the rate follows the sets in flight (profiles/r03_knee.json:
+    # 4 x 16 2.29M at 29 ms per pass, 12 x 16 3.09M at 64 ms; past 200k sets in flight the
+    # library switches to the Pippenger signature sum and four items per k_mlf lane).  Round 6
+    # (profiles/r06_knee.json, alternated on one box): 12 x 22 3.51-3.56M at 76-77 ms, 16 x 16
+    # 3.62-3.64M at 72 ms, 16 x 22 3.70-3.75M at 96-97 ms; 12 x 32 was faster still but past
+    # 100 ms per pass.  A call's verdicts arrive when its pass ends, inside the reference's
+    # 100 ms job buffering (multithread/index.ts:57 MAX_BUFFER_WAIT_MS).  16 contexts reserve
+    # 16 x 322 MiB of scratch (k_chain), inside the library's 6 GiB admission budget (20 are
+    # refused cleanly: BLS_ERR_ADMISSION; the runtime aborted queues past ~8 GiB,
     # profiles/r03_scratch_out_of_resources.txt)
     ap.add_argument("--calls-per-pass", type=int, default=22,
                     help="calls each context submits together per pass (bls_gpu_verify_many; each call keeps "
@@ -1322,7 +1325,7 @@ def _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, 
                         "launch_ms_timed_committed": round(ns / 1e6, 3),
                         "achieved_timed": round(mads / (ns * 1e-9) / 1e12, 4),
                         "frac_timed": round(mads / (ns * 1e-9) / 1e12 / pf, 4) if pf else None,
-                        "source": f"profiles/{KSTATS_FILE} (copied: rocprofv3 kernel trace of the timed 12 x 22 "
+                        "source": f"profiles/{KSTATS_FILE} (copied: rocprofv3 kernel trace of the timed {TIMED_SHAPE} "
                                   f"shape, {KSTATS_SETS} sets per launch, four items per k_mlf lane; frac against "
                                   "peak_fixed)"})
             for v in kern.values():

@@ -6,7 +6,7 @@
 #   CFGS="12x22 4x16"  cfg2 lines at contexts x calls per pass (ENVS as in gpu_r3_ab.sh)
 #   SWEEP4=1  tools/sweep_cfg4.py (the cfg4 slice's knee)
 #   PMC=1     SQ / HBM counter passes + a kernel trace of the timed region's shape:
-#             --inflight $PMC_CTX (12) --calls-per-pass $PMC_CPP (22), one step, no warm-up
+#             --inflight $PMC_CTX (16) --calls-per-pass $PMC_CPP (22), one step, no warm-up
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${TAG:-r4}
@@ -98,7 +98,7 @@ if [ -n "$PMC" ]; then
   P3="GRBM_GUI_ACTIVE GRBM_COUNT"
   P4="FETCH_SIZE"
   P5="WRITE_SIZE"
-  PB="python3 $R/bench.py --probe-only --inflight ${PMC_CTX:-12} --calls-per-pass ${PMC_CPP:-22} --steps 1 --warmup 0"
+  PB="python3 $R/bench.py --probe-only --inflight ${PMC_CTX:-16} --calls-per-pass ${PMC_CPP:-22} --steps 1 --warmup 0"
   k=0
   for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
     k=$((k+1))
@@ -106,6 +106,6 @@ if [ -n "$PMC" ]; then
   done
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o run --output-format csv -- $PB > $R/$O/trace.log 2>&1 || { tail -20 $R/$O/trace.log; exit 1; }
   cd $R
-  python3 tools/pmc_summary.py --sets-per-pass $(( ${PMC_CPP:-22} * 1024 )) $O/pmc_summary.json "the timed region's shape: ${PMC_CTX:-12} contexts x ${PMC_CPP:-22} calls of 1024 cfg2 sets, one pass each (bench.py --probe-only --inflight ${PMC_CTX:-12} --calls-per-pass ${PMC_CPP:-22} --steps 1 --warmup 0; the pass shape chosen by the sets in flight as in the timed region); counter collection serialises the kernels, so per-dispatch figures, not the overlap; setup kernels (k_sign, k_sk_to_pk, k_load_pubkeys, k_aggregate) are input synthesis" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5 > $O/pmc_summary.txt
+  python3 tools/pmc_summary.py --sets-per-pass $(( ${PMC_CPP:-22} * 1024 )) $O/pmc_summary.json "the timed region's shape: ${PMC_CTX:-16} contexts x ${PMC_CPP:-22} calls of 1024 cfg2 sets, one pass each (bench.py --probe-only --inflight ${PMC_CTX:-16} --calls-per-pass ${PMC_CPP:-22} --steps 1 --warmup 0; the pass shape chosen by the sets in flight as in the timed region); counter collection serialises the kernels, so per-dispatch figures, not the overlap; setup kernels (k_sign, k_sk_to_pk, k_load_pubkeys, k_aggregate) are input synthesis" $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/pmc5 > $O/pmc_summary.txt
 fi
 echo done
