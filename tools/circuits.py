@@ -331,7 +331,9 @@ def _hoist_lins(groups, lanes):
         keep = []
         for n in out[r]:
             ready = 1 + max((prod[x[1]] for x in _refs(n.a)), default=-1)
-            q = next((g for g in range(ready, r) if len(out[g]) < lanes), None)
+            # (not into a linear-only step that hoisting has emptied: it would survive
+            # as a step of its own where the combination could ride in a later product step)
+            q = next((g for g in range(ready, r) if 0 < len(out[g]) < lanes), None)
             if q is None:
                 keep.append(n)
                 continue

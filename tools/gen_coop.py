@@ -193,6 +193,34 @@ class T:
         n[5] = self.add2(self.sc2(self.add2(b1, c[5]), 2), b1)
         return self.from_coefs(n)
 
+    def csqr12_pipe(self, f_lin, f_mat):
+        """csqr12 for a squaring chain at one product step per squaring: the products take
+        their operands from f_lin (the previous squaring's output as an unmaterialised
+        combination of its products and the materialised value before it), the output's
+        -2 c / +2 c terms reference f_mat (f materialised, computed beside these products),
+        so the materialisation of each output runs in the next squaring's product step
+        instead of a step of its own."""
+        c = [self.coef(f_lin, k) for k in range(6)]
+        m = [self.coef(f_mat, k) for k in range(6)]
+
+        def fp4(x, y):
+            t0 = self.sqr2(x)
+            t1 = self.sqr2(y)
+            return self.add2(t0, self.xi2(t1)), self.sub2(self.sub2(self.sqr2(self.add2(x, y)), t0), t1)
+
+        a0, a1 = fp4(c[0], c[3])
+        b0, b1 = fp4(c[1], c[4])
+        d0, d1 = fp4(c[2], c[5])
+        n = [None] * 6
+        n[0] = self.sub2(self.sc2(a0, 3), self.sc2(m[0], 2))
+        n[3] = self.add2(self.sc2(a1, 3), self.sc2(m[3], 2))
+        xd1 = self.xi2(d1)
+        n[1] = self.add2(self.sc2(xd1, 3), self.sc2(m[1], 2))
+        n[4] = self.sub2(self.sc2(d0, 3), self.sc2(m[4], 2))
+        n[2] = self.sub2(self.sc2(b0, 3), self.sc2(m[2], 2))
+        n[5] = self.add2(self.sc2(b1, 3), self.sc2(m[5], 2))
+        return self.from_coefs(n)
+
     def mul_line(self, f, l0, l2, l3):
         """f * (l0 + l2 w^2 + l3 w^3) (field.hpp fp12_mul_line)."""
         def mul01(a, d0, d1):
@@ -353,14 +381,24 @@ def miller_loop(t: T, qx, qy, pxz: Lin, py: Lin, pz3: Lin | None):
     return t.conj12(f)
 
 
-def cexp_x(t: T, f):
-    """f^x = conj(f^|x|) for cyclotomic f."""
+def cexp_x(t: T, f, pipe: bool = True):
+    """f^x = conj(f^|x|) for cyclotomic f.  pipe: the squarings as csqr12_pipe (each
+    squaring's products read the previous output unmaterialised; its materialisation
+    runs beside the next products), so a run of squarings costs one step each."""
     r = f
+    if not pipe:
+        for i in range(62, -1, -1):
+            r = t.mat12(t.csqr12(r))
+            if (X_ABS >> i) & 1:
+                r = t.mat12(t.mul12(r, f))
+        return t.conj12(r)
+    r_lin = r_mat = f
     for i in range(62, -1, -1):
-        r = t.mat12(t.csqr12(r))
+        nl = t.csqr12_pipe(r_lin, r_mat)
+        r_lin, r_mat = nl, t.mat12(nl)
         if (X_ABS >> i) & 1:
-            r = t.mat12(t.mul12(r, f))
-    return t.conj12(r)
+            r_lin = r_mat = t.mat12(t.mul12(r_mat, f))
+    return t.conj12(r_mat)
 
 
 # ----------------------------------------------------------------------------
