@@ -3,7 +3,7 @@
 //   k_mlq  one lane per item: the twist point T runs from Q = HQ through the 63
 //          doubling and 5 addition steps of |x| = 0xd201000000010000 (bls/pairing.hpp
 //          miller_dbl_step / miller_add_step) and writes each step's line, already
-//          evaluated at P = RP (l0 z^3, l2 XZ, l3 Y: 6 Fp), to a line buffer -- 68
+//          evaluated at P = RP made affine (l0, l2 x, l3 y: 6 Fp), to a line buffer -- 68
 //          lines x 288 B per item, laid out line-major and lane-minor so a wavefront's
 //          stores and loads are 256-byte rows;
 //   k_mlf  one lane per TWO items of one product domain (a chunk, or a non-batchable
@@ -41,9 +41,10 @@ __device__ __forceinline__ size_t line_at(uint32_t stride, uint32_t k, int e, in
   return ((size_t)e * LINE_WORDS + w) * stride + k;
 }
 
+// P affine (g1_eval_affine_from_jac, z3 = 1): l0 is c0 itself
 __device__ __forceinline__ void store_line(uint32_t* L, uint32_t stride, uint32_t k, int e, const G1Eval& P,
                                            const Fp2& c0, const Fp2& c1, const Fp2& c2) {
-  const Fp2 l[3] = {fp2_mul_fp(c0, P.z3), fp2_mul_fp(c1, P.xz), fp2_mul_fp(c2, P.y)};
+  const Fp2 l[3] = {c0, fp2_mul_fp(c1, P.xz), fp2_mul_fp(c2, P.y)};
 #pragma unroll
   for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(W, W)
   rp.x = ch[CH_RP + 0];
   rp.y = ch[CH_RP + 1];
   rp.z = ch[CH_RP + 2];
-  const G1Eval P = g1_eval_from_jac(rp);
+  const G1Eval P = g1_eval_affine_from_jac(rp);
   G2A q;
   q.x = Fp2{ch[CH_HQ + 0], ch[CH_HQ + 1]};
   q.y = Fp2{ch[CH_HQ + 2], ch[CH_HQ + 3]};

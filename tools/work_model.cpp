@@ -74,7 +74,7 @@ int main() {
     rp += tick();
     // k_mlq: the twist-point chain and its 68 lines evaluated at P
     {
-      const G1Eval P = g1_eval_from_jac(rpk);
+      const G1Eval P = g1_eval_affine_from_jac(rpk);  // (the inversion is no Fp product)
       G2Proj T;
       T.x = sig.x;
       T.y = sig.y;
@@ -82,10 +82,10 @@ int main() {
       Fp2 c0, c1, c2;
       for (int bit = 62; bit >= 0; --bit) {
         miller_dbl_step(T, c0, c1, c2);
-        (void)fp2_mul_fp(c0, P.z3), (void)fp2_mul_fp(c1, P.xz), (void)fp2_mul_fp(c2, P.y);
+        (void)fp2_mul_fp(c1, P.xz), (void)fp2_mul_fp(c2, P.y);
         if ((BLS_X_ABS >> bit) & 1ull) {
           miller_add_step(T, sig, c0, c1, c2);
-          (void)fp2_mul_fp(c0, P.z3), (void)fp2_mul_fp(c1, P.xz), (void)fp2_mul_fp(c2, P.y);
+          (void)fp2_mul_fp(c1, P.xz), (void)fp2_mul_fp(c2, P.y);
         }
       }
       mlq += tick();
