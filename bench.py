@@ -1003,7 +1003,9 @@ def main() -> None:
     # The deployable configuration (hw_queues_4 / hw_queues_16): the same cfg2 shape in
     # child processes whose HIP runtime gets GPU_MAX_HW_QUEUES = 4 (HIP's default, what a
     # beacon node that sets nothing runs) and 16, started now -- before this process makes
-    # any GPU call -- and released one at a time after this process's own GPU work
+    # any GPU call -- and released one at a time after this process's own GPU work; each
+    # times the parent's steps after the parent's warm-up (at least 2: the first passes
+    # pick their shape from fewer sets in flight)
     hwq_children = {}
     if args.hwq_child:
         args.probe_only = True
@@ -1019,7 +1021,7 @@ def main() -> None:
             hwq_children["torch_world1"] = subprocess.Popen(
                 [sys.executable, str(Path(__file__).resolve()), "--torch-world1-child", "--inflight",
                  str(args.inflight), "--calls-per-pass", str(args.calls_per_pass), "--steps",
-                 str(max(3, args.steps // 3)), "--warmup", "1", "--sets", str(args.sets)],
+                 str(args.steps), "--warmup", str(max(2, args.warmup)), "--sets", str(args.sets)],
                 env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     if (world == 1 and args.mode == "cfg2" and args.roots == 0 and not args.no_sub_records and not args.probe_only
             and args.hw_queues and not args.hwq_child and not args.torch_world1_child):
@@ -1029,8 +1031,8 @@ def main() -> None:
                 env["GPU_MAX_HW_QUEUES"] = str(int(q))
             hwq_children[q] = subprocess.Popen(
                 [sys.executable, str(Path(__file__).resolve()), "--hwq-child", "--inflight", str(args.inflight),
-                 "--calls-per-pass", str(args.calls_per_pass), "--steps", str(max(3, args.steps // 3)), "--warmup", "1",
-                 "--sets", str(args.sets)],
+                 "--calls-per-pass", str(args.calls_per_pass), "--steps", str(args.steps),
+                 "--warmup", str(max(2, args.warmup)), "--sets", str(args.sets)],
                 env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
         _main_gpu(args, world, rank, local_rank, dist, device, share, barrier_sync, hwq_children)
