@@ -32,11 +32,14 @@
  *       -L lodestar_amd/_native -llodestar_bls -Wl,-rpath,'$ORIGIN' -o lodestar_amd/_native/lodestar_bls.node
  */
 #define NAPI_VERSION 4
+#include <execinfo.h>
 #include <node_api.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "lodestar_bls.h"
 
@@ -59,20 +62,24 @@ typedef struct {
   int closed;
 } bls_handle;
 
+/* a closed handle with nothing in flight: release its device context and free it (the
+ * caller does not touch h afterwards) */
 static void handle_release_if_idle(bls_handle* h) {
-  if (h->closed && h->inflight == 0 && h->ctx) {
-    bls_gpu_close(h->ctx);
+  if (h->closed && h->inflight == 0) {
+    if (h->ctx) bls_gpu_close(h->ctx);
     h->ctx = NULL;
+    free(h);
   }
 }
 
+/* GC of a handle that was never closed (jobs hold a reference to the handle object, so
+ * nothing is in flight then) */
 static void handle_finalize(napi_env env, void* data, void* hint) {
   (void)env;
   (void)hint;
   bls_handle* h = (bls_handle*)data;
   h->closed = 1;
   handle_release_if_idle(h);
-  free(h);
 }
 
 static napi_value js_init(napi_env env, napi_callback_info info) {
@@ -101,15 +108,27 @@ static napi_value js_init(napi_env env, napi_callback_info info) {
   }
   bls_handle* h = (bls_handle*)calloc(1, sizeof(bls_handle));
   h->ctx = ctx;
-  napi_value ext;
-  CHECK(env, napi_create_external(env, h, handle_finalize, NULL, &ext));
-  return ext;
+  /* the handle is a plain object wrapping h: close() removes the wrap, so a closed
+   * handle leaves no finalizer for V8 to run at environment teardown (Node 12 ran such
+   * finalizers during FreeEnvironment and crashed the process at exit, 1 run in ~3 of
+   * the 16-context N-API bench; profiles/r06_napi_exit_crash.txt) */
+  napi_value obj;
+  CHECK(env, napi_create_object(env, &obj));
+  if (napi_wrap(env, obj, h, handle_finalize, NULL, NULL) != napi_ok) {
+    bls_gpu_close(ctx);
+    free(h);
+    napi_throw_error(env, NULL, "lodestar_bls: N-API failure");
+    return NULL;
+  }
+  return obj;
 }
 
 /* the live handle behind v, or NULL (not a handle, or closed: use after close) */
 static bls_handle* get_handle(napi_env env, napi_value v) {
   void* p = NULL;
-  if (napi_get_value_external(env, v, &p) != napi_ok || !p) return NULL;
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_object) return NULL;
+  if (napi_unwrap(env, v, &p) != napi_ok || !p) return NULL;
   bls_handle* h = (bls_handle*)p;
   return h->closed ? NULL : h;
 }
@@ -120,8 +139,10 @@ static napi_value js_close(napi_env env, napi_callback_info info) {
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   bls_handle* h = get_handle(env, argv[0]);
   if (h) {
+    void* p = NULL;
+    (void)napi_remove_wrap(env, argv[0], &p);  /* no finalizer from here on */
     h->closed = 1;
-    handle_release_if_idle(h);
+    handle_release_if_idle(h);  /* now, or when its last call completes */
   }
   return NULL;
 }
@@ -481,7 +502,31 @@ static napi_value js_ssz_roots(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* $BLS_NAPI_SEGV_TRACE=1 (diagnostics): a native backtrace on stderr if the process takes
+ * SIGSEGV / SIGABRT / SIGBUS, then the default action; and a note when the process
+ * reaches exit handlers, so a crash at exit can be placed */
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  static const char head[] = "lodestar_bls: fatal signal, native backtrace:\n";
+  (void)!write(2, head, sizeof(head) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+static void exit_note(void) {
+  static const char msg[] = "lodestar_bls: exit handlers running\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+}
+
 static napi_value module_init(napi_env env, napi_value exports) {
+  const char* tr = getenv("BLS_NAPI_SEGV_TRACE");
+  if (tr && *tr == '1') {
+    signal(SIGSEGV, segv_trace);
+    signal(SIGABRT, segv_trace);
+    signal(SIGBUS, segv_trace);
+    atexit(exit_note);
+  }
   napi_property_descriptor d[] = {
       {"init", NULL, js_init, NULL, NULL, NULL, napi_default, NULL},
       {"close", NULL, js_close, NULL, NULL, NULL, napi_default, NULL},

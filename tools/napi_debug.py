@@ -28,13 +28,18 @@ def main():
         wf = Path(td) / "work.json"
         wf.write_text(json.dumps({"pubkeys48": pks48.hex(),
                                   "sets": [{"idx": pk[0], "msg": m.hex(), "sig": s.hex()} for pk, m, s in sets]}))
-        for name, args in (("small", ["2", "2", "4096", "1", "1024", "0"]),
-                           ("batched", ["2", "12", str(len(sets)), "1024", str(len(sets)), "0"]),
-                           ("per_set", ["2", "12", str(len(sets)), "1", str(len(sets)), "0"])):
-            env = dict(os.environ, UV_THREADPOOL_SIZE="16")
+        ctx = os.environ.get("NAPI_CTX", "16")
+        runs = os.environ.get("NAPI_RUNS", "small,batched,per_set").split(",")
+        cfgs = {"small": ["2", "2", "4096", "1", "1024", "0"],
+                "batched": ["8", ctx, str(len(sets)), "1024", str(len(sets)), "0"],
+                "per_set": ["8", ctx, str(len(sets)), "1", str(len(sets)), "0"]}
+        for name in runs:
+            args = cfgs[name.rstrip("0123456789")]
+            # BLS_NAPI_SEGV_TRACE: the addon prints a native backtrace on a fatal signal
+            env = dict(os.environ, UV_THREADPOOL_SIZE=str(int(ctx) + 2), BLS_NAPI_SEGV_TRACE="1")
             p = subprocess.run([node, str(bench.ROOT / "integration" / "js" / "benchNapi.js"), str(wf), *args],
                                capture_output=True, text=True, env=env, timeout=240)
-            out[name] = {"rc": p.returncode, "stderr": p.stderr[-1500:], "stdout": p.stdout[-600:]}
+            out[name] = {"rc": p.returncode, "stderr": p.stderr[-8000:], "stdout": p.stdout[-600:]}
             print(name, p.returncode, file=sys.stderr, flush=True)
             if p.returncode != 0:
                 break
