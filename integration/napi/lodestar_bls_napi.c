@@ -55,7 +55,8 @@
  * (verify_execute only touches ctx on a libuv worker), so the counters need no
  * locking.  close() while verifies are queued or running only marks the handle; the
  * last completing verify releases the device context.  Each queued job also holds a
- * reference to the handle's external, so the GC finalizer cannot run under it. */
+ * reference to the handle object, so the GC finalizer cannot run under it; close()
+ * removes the wrap, so a closed handle has no finalizer at all. */
 typedef struct {
   bls_gpu_ctx* ctx;
   uint32_t inflight;
@@ -201,7 +202,7 @@ typedef struct {
   bls_gpu_ctx* ctx;
   bls_batch batch;
   napi_ref keep;          /* the request object: keeps the input buffers alive */
-  napi_ref keep_handle;   /* the handle's external: no finalizer while the job is out */
+  napi_ref keep_handle;   /* the handle object: no finalizer while the job is out */
   int32_t* verdicts;
   bls_stats stats;
   double t_start_ns, t_end_ns;
