@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -100,6 +100,9 @@ class PackedBatch:
     pk_indices: np.ndarray | None = None  # uint32[...]
     signature_lens: np.ndarray | None = None  # uint32[n_sets]
     seed: bytes | None = None
+    # the bls_batch view of these arrays, built on first use (GpuContext._batch_struct):
+    # a pass of 64 calls re-packed its 64 structs under the GIL at every submission
+    _cstruct: object = field(default=None, repr=False, compare=False)
 
     @property
     def n_sets(self) -> int:
@@ -218,6 +221,10 @@ class GpuContext:
     # -- verification -------------------------------------------------------------
     @staticmethod
     def _batch_struct(pb: PackedBatch):
+        # cached on the batch: its arrays are not modified after packing (a caller that
+        # edits one in place must build a new PackedBatch)
+        if pb._cstruct is not None:
+            return pb._cstruct
         keep = []
         b = BlsBatch()
         b.n_sets = pb.n_sets
@@ -234,6 +241,7 @@ class GpuContext:
             seed_buf = ctypes.create_string_buffer(bytes(pb.seed), 32)
             b.seed = ctypes.cast(seed_buf, ctypes.c_void_p)
         keep.append(seed_buf)
+        pb._cstruct = (b, keep)
         return b, keep
 
     def verify_packed(self, pb: PackedBatch) -> tuple[np.ndarray, BlsStats]:

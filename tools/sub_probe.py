@@ -22,11 +22,12 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--jobs", type=int, default=5)
     ap.add_argument("--detail", action="store_true", help="per-pass device times of each --only slice instead")
+    ap.add_argument("--contexts", type=int, default=12, help="contexts opened (cfg5 runs on all; cfg4 on 8)")
     a = ap.parse_args()
     if a.detail:
         print(json.dumps({k: detail(k) for k in a.only.split(",")}))
         return
-    res = bench.sub_records(a.table_keys, 12, 22, 125_000, reps=a.reps, cfg4_ctx=8, cfg4_cpp=64, jobs=a.jobs,
+    res = bench.sub_records(a.table_keys, a.contexts, 22, 125_000, reps=a.reps, cfg4_ctx=8, cfg4_cpp=64, jobs=a.jobs,
                             only=set(a.only.split(",")))
     res["env"] = {k: v for k, v in os.environ.items() if k.startswith("BLS_")}
     print(json.dumps(res))
