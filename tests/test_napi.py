@@ -169,3 +169,28 @@ def test_js_multi_device_on_one_gpu(gpu, oracle, tmp_path):
                          text=True, timeout=300, env=dict(os.environ, UV_THREADPOOL_SIZE="16"))
     assert out.returncode == 0, out.stderr
     _multi_checks(json.loads(out.stdout.strip().splitlines()[-1]))
+
+
+@pytest.mark.gpu
+def test_js_bench_exits_cleanly_with_16_contexts(gpu, tmp_path):
+    """benchNapi.js at the bench's 16 contexts (plus the main lane) exits with status 0
+    after closing every handle: before the handles were wrapped objects whose wrap
+    close() removes, Node ran their finalizers during environment teardown and the
+    16-context bench died at exit with SIGSEGV (profiles/r06_napi_exit_crash.txt)."""
+    from lodestar_amd import workloads as W
+
+    n, keys = 4096, 1024
+    sks = W.interop_sks(keys)
+    pks48 = gpu.sk_to_pk(b"".join(s.to_bytes(32, "big") for s in sks)).tobytes()
+    msgs = [W.message(j, b"EXIT") for j in range(n)]
+    sigs = gpu.sign(b"".join(sks[j % keys].to_bytes(32, "big") for j in range(n)), b"".join(msgs))
+    f = tmp_path / "work.json"
+    f.write_text(json.dumps({"pubkeys48": pks48.hex(), "sets": [
+        {"idx": j % keys, "msg": msgs[j].hex(), "sig": sigs[j].tobytes().hex()} for j in range(n)]}))
+    for per_call in ("1024", "1"):
+        out = subprocess.run([NODE, str(ROOT / "integration" / "js" / "benchNapi.js"), str(f), "2", "16", str(n),
+                              per_call, str(n), "0"], capture_output=True, text=True, timeout=300,
+                             env=dict(os.environ, UV_THREADPOOL_SIZE="18"))
+        assert out.returncode == 0, (per_call, out.returncode, out.stderr[-2000:])
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        assert r["contexts"] == 16 and r["sets_per_step"] == 16 * n
