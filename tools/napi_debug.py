@@ -37,7 +37,8 @@ def main():
             args = cfgs[name.rstrip("0123456789")]
             # BLS_NAPI_SEGV_TRACE: the addon prints a native backtrace on a fatal signal
             env = dict(os.environ, UV_THREADPOOL_SIZE=str(int(ctx) + 2), BLS_NAPI_SEGV_TRACE="1")
-            p = subprocess.run([node, str(bench.ROOT / "integration" / "js" / "benchNapi.js"), str(wf), *args],
+            flags = os.environ.get("NODE_FLAGS", "").split()  # e.g. --max-semi-space-size=64
+            p = subprocess.run([node, *flags, str(bench.ROOT / "integration" / "js" / "benchNapi.js"), str(wf), *args],
                                capture_output=True, text=True, env=env, timeout=240)
             out[name] = {"rc": p.returncode, "stderr": p.stderr[-8000:], "stdout": p.stdout[-600:]}
             print(name, p.returncode, file=sys.stderr, flush=True)
