@@ -221,8 +221,8 @@ class GpuContext:
     # -- verification -------------------------------------------------------------
     @staticmethod
     def _batch_struct(pb: PackedBatch):
-        # cached on the batch: its arrays are not modified after packing (a caller that
-        # edits one in place must build a new PackedBatch)
+        # cached on the batch: the view points at the batch's arrays, so edits in place
+        # are seen; a caller that replaces one of them must build a new PackedBatch
         if pb._cstruct is not None:
             return pb._cstruct
         keep = []

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-6 f-side A/B on the GPU box (k_mlf at four items per lane vs k_mlf2n at four items
-# per lane pair): the items-per-lane parity tests, cfg2 lines at the CFGS shapes for each
-# ENVS label (alternated), and a kernel trace of the timed 12 x 22 shape per TRACE label.
+# Round-6 A/B step on the GPU box (first used for the f side's lane-pair variant,
+# profiles/r06_ab_mlf_pair4.json; then the timed-region shapes, r06_knee.json): GPU tests
+# (TESTK filter), cfg2 lines at the CFGS shapes for each ENVS label (alternated), and a
+# kernel trace of the 12 x 22 shape per TRACE label.
 # Each step has its own time limit; the script stops at the first failure.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
