@@ -35,6 +35,7 @@
 #include <string>
 #include <vector>
 
+#include "bls/group_decode.hpp"
 #include "launchers.hpp"
 
 using namespace bls;
@@ -850,24 +851,12 @@ static int verify_groups(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& gbufs, 
     const uint32_t m = (uint32_t)c.ok.size();
     // without a whole test the whole is the failed chunk check (it failed)
     const bool pass = c.whole && (gv[c.first] & 1) != 0;
-    if (pass || m == 1) {
-      for (uint32_t t : c.ok) verdict[t] = pass ? 1 : 0;
-      continue;
-    }
-    const uint32_t bits_at = c.first + (c.whole ? 1u : 0u);
-    uint32_t bad = 0;
-    bool consistent = true;
-    for (uint32_t j = 0; j < c.nbits; ++j) {
-      const int32_t v = gv[bits_at + j];
-      const bool one = (v & 1) != 0, same = (v & 2) != 0;
-      if (one == same) consistent = false;
-      if (!one) bad |= 1u << j;
-    }
-    if (!consistent || bad >= m) {
+    const int32_t bad = group_decode(m, c.nbits, pass, gv.data() + c.first + (c.whole ? 1u : 0u));
+    if (bad < 0) {
       alone.insert(alone.end(), c.ok.begin(), c.ok.end());
       continue;
     }
-    for (uint32_t k = 0; k < m; ++k) verdict[c.ok[k]] = k == bad ? 0 : 1;
+    for (uint32_t k = 0; k < m; ++k) verdict[c.ok[k]] = (int32_t)k == bad ? 0 : 1;
   }
   if (eq) cs.clear();
   // decode pass A; plan pass B

@@ -15,6 +15,7 @@
 #include "bls/pairing.hpp"
 #include "bls/hash_to_curve.hpp"
 #include "bls/pipeline.hpp"
+#include "bls/group_decode.hpp"
 
 unsigned long long bls_fpm_counter = 0;
 unsigned long long bls_lz_norm_counter = 0;
@@ -216,6 +217,10 @@ void hs_fp12_mul_line2(const uint8_t* f, const uint8_t* l, const uint8_t* m, uin
           out);
 }
 void hs_final_exp(const uint8_t* a, uint8_t* out) { wr_fp12(final_exponentiation(rd_fp12(a)), out); }
+// bls_gpu.hip verify_groups' decode of one failed chunk (bls/group_decode.hpp)
+int hs_group_decode(uint32_t m, uint32_t nbits, int whole_pass, const int32_t* v) {
+  return group_decode(m, nbits, whole_pass != 0, v);
+}
 
 void hs_miller_loop(const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
   wr_fp12(miller_loop(g1_eval_from_aff(rd_g1(g1)), rd_g2(g2)), out);

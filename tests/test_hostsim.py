@@ -235,6 +235,42 @@ def test_fp12_pair_halves(hostsim):
         assert o2.raw[:576] == o2.raw[576:] == o1.raw
 
 
+def test_group_decode_complement_inference(hostsim):
+    """bls_gpu.hip verify_groups' decode of a failed chunk (bls/group_decode.hpp) against a
+    model of the tests: each request's final exponentiation is a group element (1 for a
+    valid request; a random non-identity one for an invalid), a test's value the product
+    over its requests.  With one invalid request the decode names it (the others valid);
+    with none it says all valid; with two or more it never names one -- it sends the
+    chunk to one test per request -- for every chunk size 1..16 and every position."""
+    import itertools
+
+    q = (1 << 61) - 1  # additive model of the target group: value 0 = identity
+    rng = random.Random(41)
+    vbuf = (ctypes.c_int32 * 8)()
+    hostsim.hs_group_decode.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+
+    def decode(m, bad):
+        val = {b: rng.randrange(1, q) for b in bad}
+        whole = sum(val.values()) % q
+        nbits = 0
+        while m > 1 and (1 << nbits) < m:
+            nbits += 1
+        for j in range(nbits):
+            g = sum(val.get(k, 0) for k in range(m) if (k >> j) & 1) % q
+            vbuf[j] = (1 if g == 0 else 0) | (2 if g == whole else 0)
+        return hostsim.hs_group_decode(m, nbits, int(whole == 0), ctypes.addressof(vbuf))
+
+    for m in range(1, 17):
+        assert decode(m, set()) == m
+        for b in range(m):
+            assert decode(m, {b}) == b, (m, b)
+        for pair in itertools.combinations(range(m), 2):
+            assert decode(m, set(pair)) == -1, (m, pair)
+        for _ in range(20):
+            if m >= 3:
+                assert decode(m, set(rng.sample(range(m), rng.randrange(3, m + 1)))) == -1
+
+
 def test_hash_to_g2_golden(hostsim, golden):
     o = _buf(192)
     for v in golden["hash_to_g2"]:
