@@ -405,22 +405,36 @@ def cpu_baseline(sets, raw96, threads: int | None = None, seconds: float = 10.0,
 # modes
 # ---------------------------------------------------------------------------
 def timed_calls(ctxs, batches, steps: int):
-    """Every context runs `steps` passes of its calls back to back, all starting at one
-    barrier (a pass: one call, or a list of calls submitted together through
-    bls_gpu_verify_many); returns (elapsed s, mean stage_ms, all verdicts valid)."""
+    """`steps` x len(ctxs) passes (a pass: one call, or a list of calls submitted together
+    through bls_gpu_verify_many), all contexts starting at one barrier; each pass goes to
+    whichever context is idle -- a shared count of the passes left, as the adapter hands
+    queued jobs to an idle context (multithread/index.ts runJob) -- so a context the
+    device happens to serve more slowly does fewer passes instead of holding the region
+    open while the others idle (with a fixed `steps` each, the contexts' pass times spread
+    84-97 ms at 16 x 22 and the region ended on the slowest, tools/pass_gap_probe.py).
+    Context i runs its own calls batches[i].  Returns (elapsed s, mean stage_ms, all
+    verdicts valid)."""
     n = len(ctxs)
     start = threading.Barrier(n + 1)
     stage_sum = np.zeros(8)
     ok = [True]
     shapes: dict[int, int] = {}
     lock = threading.Lock()
+    left = [steps * n]
+
+    def take() -> bool:
+        with lock:
+            if left[0] <= 0:
+                return False
+            left[0] -= 1
+            return True
 
     def worker(i):
         start.wait()
         acc = np.zeros(8)
         good = True
         mine: dict[int, int] = {}
-        for _ in range(steps):
+        while take():
             if isinstance(batches[i], list):
                 vs, st = ctxs[i].verify_many(batches[i])
                 good = good and all(bool((v == 1).all()) for v in vs)
@@ -447,9 +461,9 @@ def timed_calls(ctxs, batches, steps: int):
 
 
 def run_calls(ctxs, packed, calls_per_pass: int):
-    """Every call of `packed` once: context i takes calls i, i + B, ... and submits them
-    `calls_per_pass` at a time through bls_gpu_verify_many; all contexts start at one
-    barrier.  Returns (elapsed s, verdict arrays in call order, summed stats dict)."""
+    """Every call of `packed` once, `calls_per_pass` consecutive calls per
+    bls_gpu_verify_many pass, each pass on whichever context is idle; all contexts start
+    at one barrier.  Returns (elapsed s, verdict arrays in call order, summed stats dict)."""
     n = len(ctxs)
     start = threading.Barrier(n + 1)
     out = [None] * len(packed)
@@ -460,11 +474,19 @@ def run_calls(ctxs, packed, calls_per_pass: int):
            "fail_device_ms": 0.0, "pass_device_ms": 0.0, "fail_stage_ms": np.zeros(8)}
     lock = threading.Lock()
 
+    # passes of calls_per_pass consecutive calls, each to whichever context is idle (a
+    # shared queue, as in timed_calls)
+    groups = [list(range(g, min(g + calls_per_pass, len(packed)))) for g in range(0, len(packed), calls_per_pass)]
+    nxt = [0]
+
     def worker(i):
-        mine = list(range(i, len(packed), n))
         start.wait()
-        for g in range(0, len(mine), calls_per_pass):
-            ks = mine[g:g + calls_per_pass]
+        while True:
+            with lock:
+                if nxt[0] >= len(groups):
+                    return
+                ks = groups[nxt[0]]
+                nxt[0] += 1
             vs, st = ctxs[i].verify_many([packed[k] for k in ks])
             for k, v in zip(ks, vs):
                 out[k] = v.copy()
