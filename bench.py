@@ -929,9 +929,12 @@ def main() -> None:
     ap.add_argument("--table-keys", type=int, default=1 << 20, help="device pubkey table of the cfg3 / cfg4 records")
     ap.add_argument("--cfg4-sets", type=int, default=125_000,
                     help="sets of this GPU's cfg4 slice (1M sets over 8 GPUs by call)")
-    # the cfg4 slice's knee (profiles/r04_sweep_cfg4.json: 4 x 32 0.47M, 8 x 32 0.85M, 12 x 32 1.06M,
-    # 8 x 64 1.49M, 12 x 64 1.38M non-batchable sets/s -- 12 x 64 leaves contexts short of a second pass)
-    ap.add_argument("--cfg4-contexts", type=int, default=8, help="contexts of the cfg4 sub-record")
+    # the cfg4 slice's knee: 8 x 64 in rounds 4-6 (profiles/r04_sweep_cfg4.json, one job: 12 x 64 left
+    # contexts short of a second pass); with passes handed to idle contexts 12 x 64 leads in the steady
+    # state (r06_sweep_cfg4.json: 2.56-2.62M / 1.89-1.92M vs 2.26-2.30M / 1.78-1.80M calls / per-set
+    # requests; 16 x 64 2.72-2.78M / 1.61-1.64M)
+    ap.add_argument("--cfg4-contexts", type=int, default=12,
+                    help="contexts of the cfg4 sub-record (12 x 64: profiles/r06_sweep_cfg4.json)")
     ap.add_argument("--cfg4-calls-per-pass", type=int, default=64, help="128-set calls per pass of the cfg4 sub-record")
     ap.add_argument("--hw-queues", default="unset,4,16",
                     help="GPU_MAX_HW_QUEUES values of the deployable-configuration sub-records ('unset': the "

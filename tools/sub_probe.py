@@ -22,12 +22,15 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--jobs", type=int, default=5)
     ap.add_argument("--detail", action="store_true", help="per-pass device times of each --only slice instead")
-    ap.add_argument("--contexts", type=int, default=12, help="contexts opened (cfg5 runs on all; cfg4 on 8)")
+    ap.add_argument("--contexts", type=int, default=12, help="contexts opened (cfg5 runs on all; cfg4 on --cfg4-contexts)")
+    ap.add_argument("--cfg4-contexts", type=int, default=12)
+    ap.add_argument("--cfg4-calls-per-pass", type=int, default=64)
     a = ap.parse_args()
     if a.detail:
         print(json.dumps({k: detail(k) for k in a.only.split(",")}))
         return
-    res = bench.sub_records(a.table_keys, a.contexts, 22, 125_000, reps=a.reps, cfg4_ctx=8, cfg4_cpp=64, jobs=a.jobs,
+    res = bench.sub_records(a.table_keys, a.contexts, 22, 125_000, reps=a.reps, cfg4_ctx=a.cfg4_contexts,
+                            cfg4_cpp=a.cfg4_calls_per_pass, jobs=a.jobs,
                             only=set(a.only.split(",")))
     res["env"] = {k: v for k, v in os.environ.items() if k.startswith("BLS_")}
     print(json.dumps(res))
