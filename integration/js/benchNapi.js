@@ -43,6 +43,7 @@ async function main() {
     for (const v of r) if (v !== true) throw Error("a valid set did not verify");
   };
   check(await step()); // warm-up
+  const cpu0 = process.cpuUsage();
   const t0 = process.hrtime.bigint();
   const pending = [];
   for (let s = 0; s < steps; s++) {
@@ -51,10 +52,11 @@ async function main() {
   }
   for (const p of pending) check(await p);
   const dt = Number(process.hrtime.bigint() - t0) / 1e9;
+  const cpu = process.cpuUsage(cpu0); // the process's CPU time over the timed steps (every thread)
   const st = pool.stats;
   await pool.close();
   console.log(JSON.stringify({sets_per_s: (steps * per) / dt, elapsed_s: dt, steps, sets_per_step: per,
-                              sets_per_call: perCall, max_sets_per_gpu_call: maxSetsPerCall, contexts: inflight,
+                              cpu_s_per_wall_s: (cpu.user + cpu.system) / 1e6 / dt, sets_per_call: perCall, max_sets_per_gpu_call: maxSetsPerCall, contexts: inflight,
                               gpu_calls: st.jobGroupsStarted, jobs: st.jobsStarted, devices,
                               slot_sets: pool.slotStats.map((x) => x.sets)}));
 }

@@ -45,6 +45,10 @@ struct bls_gpu_ctx {
   hipStream_t stream;
   hipEvent_t ev0, ev1;
   hipEvent_t ev[9];  // stage boundaries of the last verify call
+  // the event the verify path polls instead of spinning in hipStreamSynchronize when
+  // the call's pass is large (wait_block, pass_wait)
+  hipEvent_t ev_wait;
+  bool wait_block;
   char err[512];
   // device pubkey table (affine, Montgomery)
   G1A* table;
@@ -522,6 +526,8 @@ int bls_gpu_init_priority(int device, int priority, bls_gpu_ctx** out) {
     return fail("hipEventCreate", e);
   for (int i = 0; i < 9; ++i)
     if ((e = hipEventCreate(&ctx->ev[i])) != hipSuccess) return fail("hipEventCreate", e);
+  if ((e = hipEventCreateWithFlags(&ctx->ev_wait, hipEventDisableTiming)) != hipSuccess)
+    return fail("hipEventCreateWithFlags", e);
   if (load_coop_tables(ctx) != 0) {
     init_fail("bls_gpu_init: %s", ctx->err);
     bls_gpu_close(ctx);
@@ -559,6 +565,7 @@ void bls_gpu_close(bls_gpu_ctx* ctx) {
   if (ctx->msm_state) (void)hipFree(ctx->msm_state);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->ev_wait) (void)hipEventDestroy(ctx->ev_wait);
   for (int i = 0; i < 9; ++i)
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   if (ctx->coop_dev) (void)hipFree(ctx->coop_dev);
@@ -760,6 +767,8 @@ static bool group_eq_on() { return group_eq_mode() != 0; }
 // run the tests (goff: offsets into gmem, indices into the indiv list); results in gv
 // (bit 0: passed; bit 1, with ref: its final exponentiation equals test ref[g]'s);
 // 1 when the group sums do not fit (nothing ran)
+static hipError_t pass_wait(bls_gpu_ctx* ctx, hipStream_t s);  // below, before verify_body
+
 static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, const std::vector<uint32_t>& goff,
                            const std::vector<uint32_t>& gmem, std::vector<int32_t>& gv, hipStream_t s,
                            const GroupSums* sums, const std::vector<uint32_t>* ref = nullptr) {
@@ -776,7 +785,7 @@ static int run_group_tests(bls_gpu_ctx* ctx, const PipeBufs& b, GroupBufs& g, co
   if (ref) stage_copy(ctx, g.ref, ref->data(), sizeof(uint32_t) * ref->size());
   else gg.fe = nullptr;
   HIPC(ctx, launch_k_group_coop(b, ctx->coop, gg, s)); dbg_sync(s, "k_group_coop");
-  HIPC(ctx, hipStreamSynchronize(s));
+  HIPC(ctx, pass_wait(ctx, s));
   memcpy(gv.data(), res_host(ctx, g.verdict), sizeof(int32_t) * gv.size());
   return 0;
 }
@@ -1168,6 +1177,33 @@ struct InFlight {
   ~InFlight() { g_sets_in_flight.fetch_sub(n, std::memory_order_relaxed); }
 };
 
+// How the verify path's host thread waits for its stream.  hipStreamSynchronize spins
+// (so does hipEventSynchronize on a hipEventBlockingSync event in this runtime): with 16
+// contexts each waiting through a ~95 ms pass the process held ~15.7 CPUs and the job's
+// 16-CPU quota throttled it (profiles/r06_ab_sync_wait.json) -- CPU a beacon node's main
+// thread and its other work need.  A pass of >= 512 sets (the aggregated path, tens of
+// ms) polls an event with 50 us sleeps instead; smaller calls -- the latency path, a few
+// ms -- keep the spin.  $BLS_SYNC=spin / poll forces either.
+static int sync_mode() {
+  static const int m = [] {
+    const char* e = getenv("BLS_SYNC");
+    return e && !strcmp(e, "spin") ? 1 : e && !strcmp(e, "poll") ? 2 : 0;
+  }();
+  return m;
+}
+static bool wait_blocks(uint32_t n_sets) {
+  const int m = sync_mode();
+  return m == 2 || (m == 0 && n_sets >= 512);
+}
+static hipError_t pass_wait(bls_gpu_ctx* ctx, hipStream_t s) {
+  if (!ctx->wait_block || s != ctx->stream) return hipStreamSynchronize(s);
+  hipError_t e = hipEventRecord(ctx->ev_wait, s);
+  if (e != hipSuccess) return e;
+  const struct timespec nap = {0, 50000};
+  while ((e = hipEventQuery(ctx->ev_wait)) == hipErrorNotReady) nanosleep(&nap, nullptr);
+  return e;
+}
+
 static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts, bls_stats* stats,
                        uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status, uint32_t* partial_err,
                        const std::vector<uint32_t>* req_bounds);
@@ -1179,6 +1215,7 @@ static int verify_impl(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
                        uint32_t scalar_base, uint8_t* partial_out, int32_t* partial_status,
                        uint32_t* partial_err = nullptr, const std::vector<uint32_t>* req_bounds = nullptr) {
   CTX_LOCK(ctx);
+  ctx->wait_block = wait_blocks(in->n_sets);
   const int rc = verify_body(ctx, in, verdicts, stats, scalar_base, partial_out, partial_status, partial_err,
                              req_bounds);
   if (rc < 0 && ctx->msm_state) {
@@ -1596,7 +1633,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     merged_verdict = *res_host(ctx, merged_ok);
     memcpy(merged_status.data(), res_host(ctx, b.req_status_host), sizeof(int32_t) * R);
   };
-  HIPC(ctx, hipStreamSynchronize(s));
+  HIPC(ctx, pass_wait(ctx, s));
   if (merged) read_merged();
   if (n > 0) flagged = *res_host(ctx, b.flag_count_host);
   if (flagged) {
@@ -1606,7 +1643,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     HIPC(ctx, launch_k_exact(b, s)); dbg_sync(s, "k_exact");
     HIPC(ctx, launch_k_status(b, s)); dbg_sync(s, "k_status");
     if (merged && launch_merged()) return -1;
-    HIPC(ctx, hipStreamSynchronize(s));
+    HIPC(ctx, pass_wait(ctx, s));
     if (merged) read_merged();
   }
   bool merged_pass = merged && merged_verdict == 1;
@@ -1632,7 +1669,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       chunk_fe_kept = b.chunk_fe != nullptr;  // the checked chunks' final exponentiations
     }
     dbg_sync(s, "k_chunk");
-    HIPC(ctx, hipStreamSynchronize(s));
+    HIPC(ctx, pass_wait(ctx, s));
     memcpy(chunk_ok.data(), res_host(ctx, b.chunk_ok), sizeof(int32_t) * n_chunks);
   }
   if (merged_skipped) {
@@ -1669,7 +1706,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       HIPC(ctx, hipMemcpyAsync(pks.data(), b.pk_status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
       HIPC(ctx, hipMemcpyAsync(sgs.data(), b.sig_status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
       HIPC(ctx, hipMemcpyAsync(inf.data(), b.pk_inf, n, hipMemcpyDeviceToHost, s));
-      HIPC(ctx, hipStreamSynchronize(s));
+      HIPC(ctx, pass_wait(ctx, s));
       uint32_t cls = 3, idx = 0;
       int32_t code = 0;
       for (uint32_t i = 0; i < n && cls > 0; ++i)
@@ -1694,7 +1731,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       ++lvl;
     }
     HIPC(ctx, hipMemcpyAsync(partial_out, cur, sizeof(Fp12), hipMemcpyDeviceToHost, s));
-    HIPC(ctx, hipStreamSynchronize(s));
+    HIPC(ctx, pass_wait(ctx, s));
     if (stats) {
       float ms = 0.f;
       HIPC(ctx, hipEventRecord(ctx->ev1, s));
@@ -1823,7 +1860,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev[8], s));
   }
   if (gt_chunks.empty()) HIPC(ctx, hipEventRecord(ctx->ev1, s));
-  HIPC(ctx, hipStreamSynchronize(s));
+  HIPC(ctx, pass_wait(ctx, s));
   if (!indiv.empty()) memcpy(indiv_verdict.data(), res_host(ctx, b.indiv_verdict), sizeof(int32_t) * indiv.size());
   if (!gt_chunks.empty()) {
     // group sums: test g's sum lands in virtual set indiv_vbase + n_direct + g (the
@@ -1852,7 +1889,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       return rc;
     HIPC(ctx, hipEventRecord(ctx->ev[8], s));
     HIPC(ctx, hipEventRecord(ctx->ev1, s));
-    HIPC(ctx, hipStreamSynchronize(s));
+    HIPC(ctx, pass_wait(ctx, s));
   }
   assemble_verdicts(in, plan, chunk_ok.data(), indiv, indiv_verdict.data(), verdicts, stats);
   if (stats) {

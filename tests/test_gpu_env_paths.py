@@ -25,6 +25,10 @@ tokens, multithread/worker.ts:32-108), the pass shape against the rule that pick
   and the rest together) instead of the complement inference; group_eq_whole
   (BLS_GROUP_EQ=2): the complement inference against a test of the chunk's whole request
   list instead of the failed chunk check's own final exponentiation.
+* sync_spin / sync_poll (BLS_SYNC): the host thread waits every call in
+  hipStreamSynchronize's spin, or polls its event with sleeps on every call, where the
+  default polls only passes of >= 512 sets (bls_gpu.hip pass_wait) -- the fallbacks'
+  calls, verdicts unchanged.
 """
 from __future__ import annotations
 
@@ -94,6 +98,8 @@ ENVS = {
     "gsums_off": {"BLS_GROUP_SUMS": "0"},
     "group_eq_off": {"BLS_GROUP_EQ": "0"},
     "group_eq_whole": {"BLS_GROUP_EQ": "2"},
+    "sync_spin": {"BLS_SYNC": "spin"},
+    "sync_poll": {"BLS_SYNC": "poll"},
 }
 
 
