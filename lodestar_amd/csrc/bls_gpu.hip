@@ -1181,9 +1181,10 @@ struct InFlight {
 // (so does hipEventSynchronize on a hipEventBlockingSync event in this runtime): with 16
 // contexts each waiting through a ~95 ms pass the process held ~15.7 CPUs and the job's
 // 16-CPU quota throttled it (profiles/r06_ab_sync_wait.json) -- CPU a beacon node's main
-// thread and its other work need.  A pass of >= 512 sets (the aggregated path, tens of
-// ms) polls an event with 50 us sleeps instead; smaller calls -- the latency path, a few
-// ms -- keep the spin.  $BLS_SYNC=spin / poll forces either.
+// thread and its other work need.  A pass of more than 2,048 sets (only the aggregated
+// path takes those; tens of ms) polls an event with 50 us sleeps instead; smaller calls
+// keep the spin: they can take the per-set path, a few ms, where polling at 1024-set
+// calls cost 4 x 1 calls 7.2 -> 7.8 ms.  $BLS_SYNC=spin / poll forces either.
 static int sync_mode() {
   static const int m = [] {
     const char* e = getenv("BLS_SYNC");
@@ -1193,7 +1194,7 @@ static int sync_mode() {
 }
 static bool wait_blocks(uint32_t n_sets) {
   const int m = sync_mode();
-  return m == 2 || (m == 0 && n_sets >= 512);
+  return m == 2 || (m == 0 && n_sets > 2048);
 }
 static hipError_t pass_wait(bls_gpu_ctx* ctx, hipStream_t s) {
   if (!ctx->wait_block || s != ctx->stream) return hipStreamSynchronize(s);

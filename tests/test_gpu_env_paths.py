@@ -27,7 +27,7 @@ tokens, multithread/worker.ts:32-108), the pass shape against the rule that pick
   list instead of the failed chunk check's own final exponentiation.
 * sync_spin / sync_poll (BLS_SYNC): the host thread waits every call in
   hipStreamSynchronize's spin, or polls its event with sleeps on every call, where the
-  default polls only passes of >= 512 sets (bls_gpu.hip pass_wait) -- the fallbacks'
+  default polls only passes of more than 2,048 sets (bls_gpu.hip pass_wait) -- the fallbacks'
   calls, verdicts unchanged.
 """
 from __future__ import annotations
