@@ -67,7 +67,7 @@ struct PipeBufs {
   const uint32_t* chunk_off;   // n_chunks + 1 into chunk_reqs
   const uint32_t* chunk_reqs;
   const uint32_t* indiv_reqs;  // n_indiv
-  const uint32_t* fold_groups; // n_fold [beg, end) pairs: k_fold multiplies f[beg+1..end) into f[beg]
+  const uint32_t* fold_groups; // n_fold [beg, end) pairs: k_fold multiplies f[beg + step], f[beg + 2 step].. < end into f[beg]
   uint32_t n_fold;
   uint32_t fold;               // stride of the folded f's an individual request multiplies (0 or 1: none)
   // intermediates

@@ -1387,7 +1387,7 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
     gbufs.members = c.take<uint32_t>(grp_mem_cap);
     gbufs.ref = c.take<uint32_t>(gt_possible ? grp_cap : 0);
     own_sets_dev = sigagg ? c.take<uint32_t>((size_t)n + R) : nullptr;
-    b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD + R + 1));
+    b.fold_groups = c.take<uint32_t>(2ull * (n / BLS_FOLD1 + R + 1) + 2ull * (n / BLS_FOLD + R + 1));
     b.ml_dom = ml_shared ? c.take<uint32_t>(indiv_vbase) : nullptr;
     gsets_dev = sigagg ? c.take<uint32_t>(n) : nullptr;
     gseg_dev = sigagg ? c.take<uint32_t>(gseg_cap) : nullptr;
@@ -1834,15 +1834,26 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
         HIPC(ctx, launch_ml_alone(indiv_vbase, n_sum, nullptr)); dbg_sync(s, "k_mln indiv");
       }
     }
-    // groups of BLS_FOLD consecutive sets per request, multiplied in parallel first
+    // groups of BLS_FOLD consecutive sets per request, multiplied in parallel first: as
+    // groups of BLS_FOLD1, then those partial products BLS_FOLD / BLS_FOLD1 at a time
     bool any_fold = false;
+    for (uint32_t r : indiv) {
+      const uint32_t beg = in->req_set_offsets[r], end = in->req_set_offsets[r + 1];
+      for (uint32_t g = beg; g < end; g += BLS_FOLD1) {
+        const uint32_t ge = g + BLS_FOLD1 < end ? g + BLS_FOLD1 : end;
+        groups.push_back(g);
+        groups.push_back(ge);
+        any_fold = any_fold || ge - g > 1;
+      }
+    }
+    const uint32_t n_fold1 = (uint32_t)(groups.size() / 2);
     for (uint32_t r : indiv) {
       const uint32_t beg = in->req_set_offsets[r], end = in->req_set_offsets[r + 1];
       for (uint32_t g = beg; g < end; g += BLS_FOLD) {
         const uint32_t ge = g + BLS_FOLD < end ? g + BLS_FOLD : end;
+        if (ge - g <= BLS_FOLD1) continue;  // one first-level group: already folded
         groups.push_back(g);
         groups.push_back(ge);
-        any_fold = any_fold || ge - g > 1;
       }
     }
     b.fold = 1;
@@ -1851,7 +1862,9 @@ static int verify_body(bls_gpu_ctx* ctx, const bls_batch* in, int32_t* verdicts,
       b.fold = BLS_FOLD;
       b.n_fold = (uint32_t)(groups.size() / 2);
       stage_copy(ctx, b.fold_groups, groups.data(), sizeof(uint32_t) * groups.size());
-      HIPC(ctx, launch_k_fold(b, ctx->coop, s)); dbg_sync(s, "k_fold");
+      HIPC(ctx, launch_k_fold(b, ctx->coop, b.fold_groups, n_fold1, 1, s)); dbg_sync(s, "k_fold");
+      HIPC(ctx, launch_k_fold(b, ctx->coop, b.fold_groups + 2ull * n_fold1, b.n_fold - n_fold1, BLS_FOLD1, s));
+      dbg_sync(s, "k_fold2");
     }
     gbufs.n_direct = n_direct;
     gbufs.sum_f = gsums ? b.f + indiv_vbase + n_direct : nullptr;

@@ -79,13 +79,15 @@ hipError_t launch_k_indiv_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, 
                               hipStream_t s);
 hipError_t launch_k_group_coop(const bls::PipeBufs& b, const bls::CoopEnv& env, const bls::GroupBufs& g,
                               hipStream_t s);
-hipError_t launch_k_fold(const bls::PipeBufs& b, const bls::CoopEnv& env, hipStream_t s);
+hipError_t launch_k_fold(const bls::PipeBufs& b, const bls::CoopEnv& env, const uint32_t* groups, uint32_t n_groups,
+                         uint32_t step, hipStream_t s);
 // SIMT final exponentiations, one lane per chunk / request (kernels/k_fin_simt.hip), for
 // a failing pass's many tasks: save = 4 Fp12 of device memory per task
 uint32_t fe_simt_min();
 hipError_t launch_k_chunk_simt(const bls::PipeBufs& b, bls::Fp12* save, hipStream_t s);
 hipError_t launch_k_indiv_simt(const bls::PipeBufs& b, const bls::GroupBufs& g, bls::Fp12* save, hipStream_t s);
-#define BLS_FOLD 16u  // sets per k_fold group
+#define BLS_FOLD 16u  // sets per k_fold group (what k_indiv strides by)
+#define BLS_FOLD1 4u  // sets per first-level k_fold group
 hipError_t launch_k_coop_probe(const bls::CoopEnv& env, bls::CoopProg pg, uint32_t blocks, uint32_t reps,
                                uint32_t* sink, uint64_t* stamps, hipStream_t s);
 #define FPROD_FAN 16u
