@@ -31,9 +31,14 @@ __device__ __forceinline__ uint32_t pre_rpts_base(const PipeBufs& b) {
   return (pre_lanes(b) + BLS_BLOCK - 1) / BLS_BLOCK * BLS_BLOCK;
 }
 
-// two wavefronts per SIMD (the rate on the aggregated path): the GLV lanes' registers
-// must not lower it, so they spill instead
-__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_pre(PipeBufs b) {
+// three wavefronts per SIMD (168 VGPRs, 1,664 B/lane of scratch: 327 MiB per queue, under
+// k_chain's 337): cfg2 3.85-3.87M vs 3.79-3.81M sets/s at two per SIMD (255 VGPRs), the
+// k_pre stage 9.0 vs 10.8-11.9 ms, p50 @128 level; one per SIMD 3.61M; four would reserve
+// 570 MiB per queue, past the admission budget at 16 contexts (profiles/r06_ab_pre_occ.json)
+#ifndef BLS_PRE_WAVES
+#define BLS_PRE_WAVES 3
+#endif
+__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(BLS_PRE_WAVES))) void k_pre(PipeBufs b) {
   const uint32_t t = blockIdx.x * BLS_BLOCK + threadIdx.x;
   const uint32_t base = pre_rpts_base(b);
   if (t < base) stage_pre(b, t);
