@@ -142,7 +142,13 @@ __global__ __launch_bounds__(BLS_BLOCK) void k_msm_scatter(PipeBufs b, MsmBufs m
 }
 
 // lane s: segment s of the bucket whose [seg_off[k], seg_off[k + 1]) holds it
-__global__ __launch_bounds__(BLS_BLOCK) void k_msm_seg(PipeBufs b, MsmBufs m, uint32_t seg) {
+// two wavefronts per SIMD (256 VGPRs, 864 B/lane of scratch) rather than the one that
+// 352 registers gave: cfg2 +0.6 % in five alternated pairs, the signature-sum stage
+// ~0.7 ms shorter (profiles/r06_ab_msm_occ.json)
+#ifndef BLS_MSM_WAVES
+#define BLS_MSM_WAVES 2
+#endif
+__global__ __launch_bounds__(BLS_BLOCK) __attribute__((amdgpu_waves_per_eu(BLS_MSM_WAVES))) void k_msm_seg(PipeBufs b, MsmBufs m, uint32_t seg) {
   BLS_TAIL_PRIO();
   const uint32_t s = blockIdx.x * BLS_BLOCK + threadIdx.x;
   if (s >= m.seg_off[MSM_NB]) return;
